@@ -1,0 +1,120 @@
+/*
+ * r0hip — MI355X (gfx950) HAL for risc0-zkp: the C ABI a Rust `HipHal` binds.
+ *
+ * Drop-in boundary: every entry point below replaces one `extern "C"` symbol the
+ * reference's CUDA HAL binds (risc0/zkp/src/hal/cuda.rs -> risc0/sys) or one piece
+ * of the `cust` driver crate that cannot run on ROCm. Conventions, mirroring
+ * risc0/sys/src/lib.rs:53-75 and SURVEY.md §8(b):
+ *   - return NULL on success, else a malloc'd message the caller frees with free()
+ *     (the reference's ffi_wrap contract); r0hip_free_error() is provided too;
+ *   - pointers are device pointers to raw Montgomery u32 words unless named h_*;
+ *     FpExt = 4 consecutive words (AoS), digests = 8 words, matrices column-major;
+ *   - sizes/counts are 64-bit element counts (the CUDA ABI's u32 overflows at po2=24);
+ *   - every call is complete when it returns (cuda.h:77-100 semantics): results are
+ *     visible to the next call and to D2H copies. Work is queued on one HIP stream
+ *     per process; r0hip_prove_segment runs whole proofs without per-op syncs.
+ * Suites: R0HIP_POSEIDON2 = 0, R0HIP_SHA256 = 1 (zkp/src/core/hash/mod.rs:90-100).
+ */
+#ifndef R0HIP_H
+#define R0HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define R0HIP_POSEIDON2 0
+#define R0HIP_SHA256 1
+
+/* ---- device / memory (replaces the `cust` crate; zkp/src/hal/cuda.rs:235-381,397-421) ---- */
+const char* r0hip_init(int device_ordinal);                       /* sppark_init (sys/src/cuda.rs:20) */
+const char* r0hip_device_info(char* name, size_t name_cap, uint64_t* total_mem);
+const char* r0hip_alloc(void** d_ptr, size_t bytes);
+const char* r0hip_free(void* d_ptr);
+const char* r0hip_memset32(void* d_dst, uint32_t value, size_t count); /* alloc_elem_init (hal/mod.rs:72-83) */
+const char* r0hip_memcpy_h2d(void* d_dst, const void* h_src, size_t bytes);
+const char* r0hip_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes);
+const char* r0hip_memcpy_d2d(void* d_dst, const void* d_src, size_t bytes);
+const char* r0hip_synchronize(void);
+void r0hip_free_error(const char* err);
+
+/* ---- NTT family (sppark_batch_* in sys/src/cuda.rs:22-46; CPU semantics cpu.rs:305-408) ---- */
+/* expand each of `count` polys of 2^(lg_out-expand_bits) bit-reversed coeffs into out (count x 2^lg_out)
+ * and evaluate: Hal::batch_expand_into_evaluate_ntt (hal/mod.rs:102-108; cuda.rs:529-570) */
+const char* r0hip_batch_expand_into_evaluate_ntt(uint32_t* d_out, const uint32_t* d_in, size_t count,
+                                                 uint32_t lg_out, uint32_t expand_bits);
+/* Hal::batch_interpolate_ntt (hal/mod.rs:110; cuda.rs:572-590 -> sppark_batch_iNTT) */
+const char* r0hip_batch_interpolate_ntt(uint32_t* d_io, size_t count, uint32_t lg_size);
+/* Hal::zk_shift (hal/mod.rs:123; cuda.rs:690-708 -> sppark_batch_zk_shift) */
+const char* r0hip_zk_shift(uint32_t* d_io, size_t count, uint32_t lg_size);
+/* Hal::batch_bit_reverse (risc0_zkp_cuda_batch_bit_reverse, ffi.cu:89-91) */
+const char* r0hip_batch_bit_reverse(uint32_t* d_io, size_t count, uint32_t lg_size);
+
+/* ---- polynomial ops ---- */
+/* risc0_zkp_cuda_batch_evaluate_any (ffi.cu:93-101): out[k] = sum_i coeffs[which[k]][i] * xs[k]^i */
+const char* r0hip_batch_evaluate_any(uint32_t* d_out, const uint32_t* d_coeffs, size_t poly_count,
+                                     uint32_t lg_poly_size, const uint32_t* d_which, const uint32_t* d_xs,
+                                     size_t eval_count);
+/* risc0_zkp_cuda_mix_poly_coeffs (ffi.cu:79-87); mix_start / mix are host FpExt (4 words) */
+const char* r0hip_mix_poly_coeffs(uint32_t* d_out, const uint32_t* d_in, const uint32_t* h_combos,
+                                  const uint32_t* h_mix_start, const uint32_t* h_mix, size_t input_size,
+                                  size_t count);
+/* risc0_zkp_cuda_fri_fold (ffi.cu:75-77): out is 4 x count, in is 4 x 16 x count (SoA planes) */
+const char* r0hip_fri_fold(uint32_t* d_out, const uint32_t* d_in, const uint32_t* h_mix, size_t count);
+/* risc0_zkp_cuda_combos_prepare (ffi.cu:125-143); host arrays, CHECK_SIZE = 16 */
+const char* r0hip_combos_prepare(uint32_t* d_combos, const uint32_t* h_coeff_u, size_t combo_count,
+                                 size_t cycles, const uint32_t* h_reg_sizes, const uint32_t* h_reg_combo_ids,
+                                 size_t reg_count, const uint32_t* h_mix);
+/* supra_poly_divide (sys/src/cuda.rs:74-79): in-place division of a poly of `size` FpExt by (x - z);
+ * h_remainder receives the remainder (Hal::combos_divide asserts it is zero, hal/mod.rs:236-257) */
+const char* r0hip_poly_divide(uint32_t* d_poly, size_t size, uint32_t* h_remainder, const uint32_t* h_z);
+/* Hal::combos_divide batched over all combos: chunk i divides combos[i*cycles..] by each z in
+ * h_pows[h_begin[i]..h_begin[i+1]); *bad_chunk = first chunk with a nonzero remainder or -1 */
+const char* r0hip_combos_divide(uint32_t* d_combos, size_t nchunks, const uint32_t* h_pows,
+                                const uint32_t* h_begin, size_t cycles, int64_t* bad_chunk);
+
+/* ---- element-wise (ffi.cu:27-73) ---- */
+const char* r0hip_eltwise_add_elem(uint32_t* d_out, const uint32_t* d_a, const uint32_t* d_b, size_t count);
+const char* r0hip_eltwise_copy_elem(uint32_t* d_out, const uint32_t* d_in, size_t count);
+const char* r0hip_eltwise_zeroize_elem(uint32_t* d_io, size_t count);
+/* out (4 x count SoA) = sum over to_add of in (to_add x count FpExt) */
+const char* r0hip_eltwise_sum_extelem(uint32_t* d_out, const uint32_t* d_in, size_t to_add, size_t count);
+const char* r0hip_eltwise_copy_elem_slice(uint32_t* d_into, const uint32_t* d_from, size_t from_rows,
+                                          size_t from_cols, size_t from_offset, size_t from_stride,
+                                          size_t into_offset, size_t into_stride);
+const char* r0hip_gather_sample(uint32_t* d_dst, const uint32_t* d_src, size_t idx, size_t size, size_t stride);
+/* CSR scatter (ffi.cu:108-114): index has cycles+1 entries */
+const char* r0hip_scatter(uint32_t* d_into, const uint32_t* d_index, const uint32_t* d_offsets,
+                          const uint32_t* d_values, size_t cycles);
+const char* r0hip_prefix_products(uint32_t* d_io, size_t count);
+
+/* ---- hashing (sppark_poseidon2_{rows,fold}, risc0_zkp_cuda_sha_{rows,fold}) ---- */
+/* out[row] = H(matrix[col*rows + row] for col < cols) */
+const char* r0hip_hash_rows(int suite, uint32_t* d_out, const uint32_t* d_matrix, size_t rows, size_t cols);
+/* io[output_size + i] = H(io[input_size + 2i], io[input_size + 2i + 1]) (cpu.rs:569-581) */
+const char* r0hip_hash_fold(int suite, uint32_t* d_io, size_t input_size, size_t output_size);
+
+/* ---- circuits (risc0_circuit_{rv32im,recursion}_cuda_eval_check) ---- */
+/* circuit: "rv32im" | "recursion". groups[g] = evaluated register group g (accum=0, code=1, data=2),
+ * d_check = 4 x 4*2^po2, h_poly_mix = the poly_mix FpExt (powers are expanded on the host) */
+const char* r0hip_eval_check(const char* circuit, uint32_t* d_check, const uint32_t* const* d_groups,
+                             const uint32_t* d_mix, const uint32_t* d_global, const uint32_t* h_poly_mix,
+                             uint32_t po2);
+
+/* ---- whole segment proof (risc0_zkp::prove::Prover driven as by the circuit's segment prover:
+ * circuit/rv32im/src/prove/hal/mod.rs:143-224, circuit/recursion/src/prove/mod.rs:164-230) ----
+ * Witness groups are device buffers (column-major, 2^po2 rows); d_global (output_size words) is
+ * zeroized in place; h_mix_out (optional) receives the mix values drawn from the transcript.
+ * The seal (Vec<u32>) is written to h_seal; *seal_len is its length in words. */
+const char* r0hip_prove_segment(const char* circuit, int suite, uint32_t po2, const uint32_t* d_code,
+                                const uint32_t* d_data, const uint32_t* d_accum, uint32_t* d_global,
+                                int write_version, uint32_t version, uint32_t* h_seal, size_t seal_cap,
+                                size_t* seal_len, uint32_t* h_mix_out);
+/* per-phase device timings (ms) of the last r0hip_prove_segment, as "name=ms;..." */
+const char* r0hip_last_profile(char* buf, size_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* R0HIP_H */

@@ -1,0 +1,12 @@
+"""risc0_amd — MI355X-native STARK prover backend for risc0-zkp.
+
+The product is libr0hip.so (risc0_amd/lib, built from risc0_amd/csrc by
+__graft_entry__.build()): hand-written HIP kernels for gfx950 behind the C ABI
+in include/r0hip.h, plus a C++ segment prover. This package is a thin ctypes
+mirror of the reference's `Hal` trait for tests and the benchmark.
+"""
+from .hal import (POSEIDON2, SHA256, Buffer, HipHal, R0HipError, check, exported_symbols, last_profile, lib,
+                  prove_segment)
+
+__all__ = ["POSEIDON2", "SHA256", "Buffer", "HipHal", "R0HipError", "check", "exported_symbols", "last_profile",
+           "lib", "prove_segment"]

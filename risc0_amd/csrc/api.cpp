@@ -1,0 +1,287 @@
+// C ABI (include/r0hip.h): the symbols a Rust `HipHal` binds in place of the
+// reference's risc0_zkp_cuda_* / sppark_* / cust calls. Each entry point runs its
+// kernels on the library stream and returns only when they have finished
+// (risc0/sys/kernels/zkp/cuda/cuda.h:77-100 semantics); errors come back as a
+// malloc'd string (risc0/sys/src/lib.rs:53-75 convention).
+#include "../../include/r0hip.h"
+
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <vector>
+
+#include "circuit.h"
+#include "devmem.h"
+#include "runtime.h"
+
+namespace r0 {
+void combos_sub(hipStream_t s, uint32_t* combos, const uint32_t* deltas, size_t rows, size_t width,
+                size_t cycles);
+void run_eval_check(const CircuitDef& c, uint32_t* check, const uint32_t* const* groups, const uint32_t* mix,
+                    const uint32_t* global, FpExt poly_mix, size_t po2);
+std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2, const uint32_t* code,
+                                    const uint32_t* data, const uint32_t* accum, uint32_t* global,
+                                    bool write_version, uint32_t version, std::vector<uint32_t>* mix_out);
+std::string last_profile();
+}  // namespace r0
+
+using namespace r0;
+
+namespace {
+template <typename F>
+const char* wrap(F f) {
+  try {
+    f();
+    HIP_OK(hipStreamSynchronize(stream()));
+  } catch (const std::exception& e) {
+    return strdup(e.what());
+  } catch (...) {
+    return strdup("r0hip: unknown error");
+  }
+  return nullptr;
+}
+uint32_t lg(size_t n, const char* what) {
+  uint32_t r = 0;
+  while ((size_t(1) << r) < n) r++;
+  if ((size_t(1) << r) != n) throw std::runtime_error(std::string("r0hip: ") + what + " is not a power of two");
+  return r;
+}
+FpExt fe(const uint32_t* w) { return FpExt{{w[0], w[1], w[2], w[3]}}; }
+}  // namespace
+
+extern "C" {
+
+const char* r0hip_init(int device_ordinal) {
+  return wrap([&] {
+    set_device(device_ordinal);
+    // warm the module (loads every code object once)
+    (void)stream();
+  });
+}
+
+const char* r0hip_device_info(char* name, size_t name_cap, uint64_t* total_mem) {
+  return wrap([&] {
+    ensure_init();
+    int dev = 0;
+    HIP_OK(hipGetDevice(&dev));
+    hipDeviceProp_t p;
+    HIP_OK(hipGetDeviceProperties(&p, dev));
+    if (name && name_cap) {
+      strncpy(name, p.gcnArchName, name_cap - 1);
+      name[name_cap - 1] = 0;
+    }
+    if (total_mem) *total_mem = p.totalGlobalMem;
+  });
+}
+
+const char* r0hip_alloc(void** d_ptr, size_t bytes) {
+  return wrap([&] { *d_ptr = dev_alloc(bytes); });
+}
+const char* r0hip_free(void* d_ptr) {
+  return wrap([&] { dev_free(d_ptr); });
+}
+const char* r0hip_memset32(void* d_dst, uint32_t value, size_t count) {
+  return wrap([&] { HIP_OK(hipMemsetD32Async(d_dst, int(value), count, stream())); });
+}
+const char* r0hip_memcpy_h2d(void* d_dst, const void* h_src, size_t bytes) {
+  return wrap([&] { HIP_OK(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, stream())); });
+}
+const char* r0hip_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes) {
+  return wrap([&] { HIP_OK(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, stream())); });
+}
+const char* r0hip_memcpy_d2d(void* d_dst, const void* d_src, size_t bytes) {
+  return wrap([&] { HIP_OK(hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, stream())); });
+}
+const char* r0hip_synchronize(void) {
+  return wrap([] {});
+}
+void r0hip_free_error(const char* err) { free(const_cast<char*>(err)); }
+
+const char* r0hip_batch_expand_into_evaluate_ntt(uint32_t* d_out, const uint32_t* d_in, size_t count, uint32_t lg_out,
+                                                 uint32_t expand_bits) {
+  return wrap([&] {
+    R0_REQUIRE(lg_out >= expand_bits && lg_out <= 27, "bad NTT size");
+    ntt_evaluate(stream(), d_out, d_in, count, lg_out, expand_bits);
+  });
+}
+const char* r0hip_batch_interpolate_ntt(uint32_t* d_io, size_t count, uint32_t lg_size) {
+  return wrap([&] {
+    R0_REQUIRE(lg_size <= 27, "bad NTT size");
+    ntt_interpolate(stream(), d_io, count, lg_size, false);
+  });
+}
+const char* r0hip_zk_shift(uint32_t* d_io, size_t count, uint32_t lg_size) {
+  return wrap([&] { zk_shift(stream(), d_io, count, lg_size); });
+}
+const char* r0hip_batch_bit_reverse(uint32_t* d_io, size_t count, uint32_t lg_size) {
+  return wrap([&] { bit_reverse(stream(), d_io, count, lg_size); });
+}
+
+const char* r0hip_batch_evaluate_any(uint32_t* d_out, const uint32_t* d_coeffs, size_t poly_count,
+                                     uint32_t lg_poly_size, const uint32_t* d_which, const uint32_t* d_xs,
+                                     size_t eval_count) {
+  return wrap([&] { batch_evaluate_any(stream(), d_coeffs, poly_count, lg_poly_size, d_which, d_xs, d_out, eval_count); });
+}
+
+const char* r0hip_mix_poly_coeffs(uint32_t* d_out, const uint32_t* d_in, const uint32_t* h_combos,
+                                  const uint32_t* h_mix_start, const uint32_t* h_mix, size_t input_size,
+                                  size_t count) {
+  return wrap([&] {
+    std::vector<uint32_t> combos(h_combos, h_combos + input_size);
+    uint32_t* d = static_cast<uint32_t*>(scratch(input_size * 4 + 16, 50));
+    upload_async(d, combos.data(), input_size * 4);
+    mix_poly_coeffs(stream(), d_out, d_in, d, combos, fe(h_mix_start), fe(h_mix), input_size, count);
+  });
+}
+
+const char* r0hip_fri_fold(uint32_t* d_out, const uint32_t* d_in, const uint32_t* h_mix, size_t count) {
+  return wrap([&] { fri_fold(stream(), d_out, d_in, fe(h_mix), count); });
+}
+
+const char* r0hip_combos_prepare(uint32_t* d_combos, const uint32_t* h_coeff_u, size_t combo_count, size_t cycles,
+                                 const uint32_t* h_reg_sizes, const uint32_t* h_reg_combo_ids, size_t reg_count,
+                                 const uint32_t* h_mix) {
+  return wrap([&] {
+    size_t width = 1;
+    for (size_t r = 0; r < reg_count; r++) width = std::max<size_t>(width, h_reg_sizes[r]);
+    std::vector<FpExt> deltas((combo_count + 1) * width, fe_zero());
+    FpExt cur = fe_one(), mix = fe(h_mix);
+    size_t pos = 0;
+    for (size_t r = 0; r < reg_count; r++) {
+      for (size_t i = 0; i < h_reg_sizes[r]; i++) {
+        FpExt& d = deltas[h_reg_combo_ids[r] * width + i];
+        d = fe_add(d, fe_mul(cur, fe(h_coeff_u + 4 * (pos + i))));
+      }
+      cur = fe_mul(cur, mix);
+      pos += h_reg_sizes[r];
+    }
+    for (size_t i = 0; i < 16; i++) {
+      FpExt& d = deltas[combo_count * width];
+      d = fe_add(d, fe_mul(cur, fe(h_coeff_u + 4 * pos)));
+      pos++;
+      cur = fe_mul(cur, mix);
+    }
+    uint32_t* dd = static_cast<uint32_t*>(scratch(deltas.size() * 16, 51));
+    upload_async(dd, deltas.data(), deltas.size() * 16);
+    combos_sub(stream(), d_combos, dd, combo_count + 1, width, cycles);
+  });
+}
+
+const char* r0hip_poly_divide(uint32_t* d_poly, size_t size, uint32_t* h_remainder, const uint32_t* h_z) {
+  return wrap([&] {
+    std::vector<std::vector<FpExt>> zs{{fe(h_z)}};
+    uint32_t* rem = static_cast<uint32_t*>(scratch(16, 52));
+    poly_divide_rows(stream(), d_poly, size, zs, rem);
+    HIP_OK(hipMemcpyAsync(h_remainder, rem, 16, hipMemcpyDeviceToHost, stream()));
+  });
+}
+
+const char* r0hip_combos_divide(uint32_t* d_combos, size_t nchunks, const uint32_t* h_pows, const uint32_t* h_begin,
+                                size_t cycles, int64_t* bad_chunk) {
+  return wrap([&] {
+    std::vector<std::vector<FpExt>> zs(nchunks);
+    size_t maxz = 0;
+    for (size_t i = 0; i < nchunks; i++) {
+      for (uint32_t k = h_begin[i]; k < h_begin[i + 1]; k++) zs[i].push_back(fe(h_pows + 4 * k));
+      maxz = std::max(maxz, zs[i].size());
+    }
+    std::vector<uint32_t> h(nchunks * std::max<size_t>(maxz, 1) * 4, 0);
+    uint32_t* rem = static_cast<uint32_t*>(scratch(h.size() * 4 + 16, 53));
+    HIP_OK(hipMemsetAsync(rem, 0, h.size() * 4, stream()));
+    poly_divide_rows(stream(), d_combos, cycles, zs, rem);
+    HIP_OK(hipMemcpyAsync(h.data(), rem, h.size() * 4, hipMemcpyDeviceToHost, stream()));
+    HIP_OK(hipStreamSynchronize(stream()));
+    *bad_chunk = -1;
+    for (size_t i = 0; i < h.size(); i++)
+      if (h[i]) {
+        *bad_chunk = int64_t(i / (std::max<size_t>(maxz, 1) * 4));
+        break;
+      }
+  });
+}
+
+const char* r0hip_eltwise_add_elem(uint32_t* d_out, const uint32_t* d_a, const uint32_t* d_b, size_t count) {
+  return wrap([&] { eltwise_add(stream(), d_out, d_a, d_b, count); });
+}
+const char* r0hip_eltwise_copy_elem(uint32_t* d_out, const uint32_t* d_in, size_t count) {
+  return wrap([&] { eltwise_copy(stream(), d_out, d_in, count); });
+}
+const char* r0hip_eltwise_zeroize_elem(uint32_t* d_io, size_t count) {
+  return wrap([&] { eltwise_zeroize(stream(), d_io, count); });
+}
+const char* r0hip_eltwise_sum_extelem(uint32_t* d_out, const uint32_t* d_in, size_t to_add, size_t count) {
+  return wrap([&] { eltwise_sum_extelem(stream(), d_out, d_in, count, to_add); });
+}
+const char* r0hip_eltwise_copy_elem_slice(uint32_t* d_into, const uint32_t* d_from, size_t from_rows,
+                                          size_t from_cols, size_t from_offset, size_t from_stride,
+                                          size_t into_offset, size_t into_stride) {
+  return wrap([&] {
+    copy_elem_slice(stream(), d_into, d_from, from_rows, from_cols, from_offset, from_stride, into_offset,
+                    into_stride);
+  });
+}
+const char* r0hip_gather_sample(uint32_t* d_dst, const uint32_t* d_src, size_t idx, size_t size, size_t stride) {
+  return wrap([&] { gather_sample(stream(), d_dst, d_src, idx, size, stride); });
+}
+const char* r0hip_scatter(uint32_t* d_into, const uint32_t* d_index, const uint32_t* d_offsets,
+                          const uint32_t* d_values, size_t cycles) {
+  return wrap([&] { scatter(stream(), d_into, d_index, d_offsets, d_values, cycles); });
+}
+const char* r0hip_prefix_products(uint32_t* d_io, size_t count) {
+  return wrap([&] { prefix_products(stream(), d_io, count); });
+}
+
+const char* r0hip_hash_rows(int suite, uint32_t* d_out, const uint32_t* d_matrix, size_t rows, size_t cols) {
+  return wrap([&] {
+    R0_REQUIRE(suite == 0 || suite == 1, "unknown hash suite");
+    hash_rows(stream(), suite, d_out, d_matrix, rows, cols);
+  });
+}
+const char* r0hip_hash_fold(int suite, uint32_t* d_io, size_t input_size, size_t output_size) {
+  return wrap([&] {
+    R0_REQUIRE(suite == 0 || suite == 1, "unknown hash suite");
+    hash_fold(stream(), suite, d_io, input_size, output_size);
+  });
+}
+
+const char* r0hip_eval_check(const char* circuit, uint32_t* d_check, const uint32_t* const* d_groups,
+                             const uint32_t* d_mix, const uint32_t* d_global, const uint32_t* h_poly_mix,
+                             uint32_t po2) {
+  return wrap([&] {
+    const CircuitDef* c = find_circuit(circuit ? circuit : "");
+    R0_REQUIRE(c, std::string("unknown circuit ") + (circuit ? circuit : "(null)"));
+    stage_reset();
+    run_eval_check(*c, d_check, d_groups, d_mix, d_global, fe(h_poly_mix), po2);
+  });
+}
+
+const char* r0hip_prove_segment(const char* circuit, int suite, uint32_t po2, const uint32_t* d_code,
+                                const uint32_t* d_data, const uint32_t* d_accum, uint32_t* d_global,
+                                int write_version, uint32_t version, uint32_t* h_seal, size_t seal_cap,
+                                size_t* seal_len, uint32_t* h_mix_out) {
+  return wrap([&] {
+    const CircuitDef* c = find_circuit(circuit ? circuit : "");
+    R0_REQUIRE(c, std::string("unknown circuit ") + (circuit ? circuit : "(null)"));
+    std::vector<uint32_t> mix;
+    std::vector<uint32_t> seal = prove_segment(*c, suite, po2, d_code, d_data, d_accum, d_global, write_version != 0,
+                                               version, &mix);
+    if (seal_len) *seal_len = seal.size();
+    if (h_mix_out) memcpy(h_mix_out, mix.data(), mix.size() * 4);
+    if (h_seal) {
+      R0_REQUIRE(seal.size() <= seal_cap, "seal buffer too small");
+      memcpy(h_seal, seal.data(), seal.size() * 4);
+    }
+  });
+}
+
+const char* r0hip_last_profile(char* buf, size_t cap) {
+  return wrap([&] {
+    std::string p = last_profile();
+    if (buf && cap) {
+      strncpy(buf, p.c_str(), cap - 1);
+      buf[cap - 1] = 0;
+    }
+  });
+}
+
+}  // extern "C"

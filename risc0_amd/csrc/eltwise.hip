@@ -1,0 +1,509 @@
+// Element-wise and polynomial HAL kernels for CDNA4: mix_poly_coeffs,
+// batch_evaluate_any, fri_fold, eltwise_{add,copy,zeroize,sum_extelem},
+// gather_sample, scatter, copy_elem_slice, prefix_products and the parallel
+// synthetic division behind combos_divide. Semantics follow
+// risc0/zkp/src/hal/cpu.rs (line refs on each kernel). All HBM-bound except
+// evaluate_any/poly_divide, which are integer-VALU bound.
+#include "runtime.h"
+
+#include <algorithm>
+
+namespace r0 {
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ FpExt ld_fe(const uint32_t* p) {
+  uint4 v = *reinterpret_cast<const uint4*>(p);
+  return FpExt{{v.x, v.y, v.z, v.w}};
+}
+__device__ __forceinline__ void st_fe(uint32_t* p, FpExt a) {
+  *reinterpret_cast<uint4*>(p) = make_uint4(a.c[0], a.c[1], a.c[2], a.c[3]);
+}
+
+// ---- element-wise ---------------------------------------------------------------
+__global__ void add_kernel(uint32_t* o, const uint32_t* a, const uint32_t* b, uint64_t n) {
+  uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (i < n) o[i] = fp_add(a[i], b[i]);
+}
+// cpu.rs:518-522: INVALID (0xffffffff) -> 0
+__global__ void zeroize_kernel(uint32_t* io, uint64_t n) {
+  uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (i < n && io[i] == 0xffffffffu) io[i] = 0;
+}
+// cpu.rs:475-500: out[k*count + idx] = (sum_i in[i*count + idx])[k]
+__global__ void sum_extelem_kernel(uint32_t* out, const uint32_t* in, uint64_t count, uint32_t to_add) {
+  uint64_t idx = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (idx >= count) return;
+  FpExt s = fe_zero();
+  for (uint32_t i = 0; i < to_add; i++) s = fe_add(s, ld_fe(in + (i * count + idx) * 4));
+#pragma unroll
+  for (int k = 0; k < 4; k++) out[k * count + idx] = s.c[k];
+}
+// cpu.rs:524-553 (FRI_FOLD = 16, rev_i = bit_rev over 4 bits)
+__global__ void fri_fold_kernel(uint32_t* out, const uint32_t* in, FpExt mix, uint64_t count) {
+  uint64_t idx = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (idx >= count) return;
+  FpExt tot = fe_zero(), cur = fe_one();
+#pragma unroll
+  for (uint32_t i = 0; i < 16; i++) {
+    uint64_t rev_idx = uint64_t(bitrev_n(i, 4)) * count + idx;
+    FpExt f;
+#pragma unroll
+    for (int k = 0; k < 4; k++) f.c[k] = in[k * count * 16 + rev_idx];
+    tot = fe_add(tot, fe_mul(cur, f));
+    cur = fe_mul(cur, mix);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) out[k * count + idx] = tot.c[k];
+}
+// cpu.rs:583-596
+__global__ void gather_kernel(uint32_t* dst, const uint32_t* src, uint64_t idx, uint64_t size, uint64_t stride) {
+  uint64_t g = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (g < size) dst[g] = src[g * stride + idx];
+}
+// cpu.rs:598-615: one lane per cycle walks its CSR slice
+__global__ void scatter_kernel(uint32_t* into, const uint32_t* index, const uint32_t* offsets,
+                               const uint32_t* values, uint64_t cycles) {
+  uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (c >= cycles) return;
+  for (uint32_t i = index[c]; i < index[c + 1]; i++) into[offsets[i]] = values[i];
+}
+// cpu.rs:617-635
+__global__ void copy_slice_kernel(uint32_t* into, const uint32_t* from, uint64_t rows, uint64_t cols,
+                                  uint64_t from_offset, uint64_t from_stride, uint64_t into_offset,
+                                  uint64_t into_stride) {
+  uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (i >= rows * cols) return;
+  uint64_t r = i / cols, c = i % cols;
+  into[into_offset + r * into_stride + c] = from[from_offset + r * from_stride + c];
+}
+
+// ---- mix_poly_coeffs (cpu.rs:410-455) ---------------------------------------------
+// out[combo*count + idx] += sum_{i: combos[i]==combo} mix_start*mix^i * in[i*count + idx]
+// One lane per idx streams all input rows (coalesced) and keeps one FpExt
+// accumulator per combo in VGPRs; combo ids are wave-uniform.
+constexpr int kMaxCombos = 8;
+template <int NC>
+__global__ __launch_bounds__(kThreads) void mix_kernel(uint32_t* out, const uint32_t* __restrict__ in,
+                                                      const uint32_t* __restrict__ combos,
+                                                      const uint32_t* __restrict__ pows,  // input_size FpExt
+                                                      uint32_t input_size, uint64_t count, uint32_t used_mask) {
+  uint64_t idx = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (idx >= count) return;
+  FpExt acc[NC];
+#pragma unroll
+  for (int k = 0; k < NC; k++) acc[k] = fe_zero();
+  for (uint32_t i = 0; i < input_size; i++) {
+    uint32_t cid = combos[i];
+    FpExt mp = ld_fe(pows + 4 * i);
+    FpExt t = fe_mul_fp(mp, in[uint64_t(i) * count + idx]);
+#pragma unroll
+    for (int k = 0; k < NC; k++)
+      if (cid == uint32_t(k)) acc[k] = fe_add(acc[k], t);
+  }
+#pragma unroll
+  for (int k = 0; k < NC; k++) {
+    if (used_mask & (1u << k)) {
+      uint32_t* o = out + (uint64_t(k) * count + idx) * 4;
+      st_fe(o, fe_add(ld_fe(o), acc[k]));
+    }
+  }
+}
+
+// ---- batch_evaluate_any (cpu.rs:362-393) -----------------------------------------
+// out[k] = sum_i coeffs[which[k]][i] * x_k^i. Grid (eval, chunk): each lane sums
+// 16 coefficients against precomputed x^0..x^15 (Fp x FpExt: 4 modmul/coeff);
+// lanes combine by a Horner tree with x^16, x^32, ... (8 levels); the chunk
+// partial is scaled by x^(chunk_start) and written; a second kernel adds chunks.
+constexpr int kEvPer = 16;
+constexpr int kEvChunk = kThreads * kEvPer;  // 4096 coefficients per workgroup
+
+__global__ __launch_bounds__(kThreads) void eval_any_kernel(const uint32_t* __restrict__ coeffs, uint32_t log_n,
+                                                           const uint32_t* __restrict__ which,
+                                                           const uint32_t* __restrict__ xs, uint32_t* partial,
+                                                           uint32_t nchunks) {
+  __shared__ FpExt xp[kEvPer + 1];  // x^0..x^16
+  __shared__ FpExt red[kThreads];
+  __shared__ FpExt ypow[9];         // x^(16 * 2^l)
+  const uint32_t k = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
+  const FpExt x = ld_fe(xs + 4 * k);
+  if (tid == 0) {
+    FpExt cur = fe_one();
+    for (int i = 0; i <= kEvPer; i++) {
+      xp[i] = cur;
+      cur = fe_mul(cur, x);
+    }
+    FpExt y = xp[kEvPer];
+    for (int l = 0; l < 9; l++) {
+      ypow[l] = y;
+      y = fe_mul(y, y);
+    }
+  }
+  __syncthreads();
+  const uint64_t n = uint64_t(1) << log_n;
+  const uint32_t* poly = coeffs + uint64_t(which[k]) * n;
+  const uint64_t start = uint64_t(chunk) * kEvChunk + uint64_t(tid) * kEvPer;
+  FpExt acc = fe_zero();
+  if (start < n) {
+    const uint4* src = reinterpret_cast<const uint4*>(poly + start);
+    uint32_t c[kEvPer];
+#pragma unroll
+    for (int q = 0; q < kEvPer / 4; q++) {
+      uint4 v = src[q];
+      c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = 0; i < kEvPer; i++) acc = fe_add(acc, fe_mul_fp(xp[i], c[i]));
+  }
+  red[tid] = acc;
+  __syncthreads();
+  // tree: level l combines lanes (2m, 2m+1) as a + b * x^(16*2^l)
+  for (int l = 0, w = kThreads / 2; w >= 1; l++, w >>= 1) {
+    FpExt v = fe_zero();
+    if (tid < (uint32_t)w) v = fe_add(red[2 * tid], fe_mul(red[2 * tid + 1], ypow[l]));
+    __syncthreads();
+    if (tid < (uint32_t)w) red[tid] = v;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    FpExt scale = fe_pow(x, uint64_t(chunk) * kEvChunk);
+    st_fe(partial + (uint64_t(k) * nchunks + chunk) * 4, fe_mul(red[0], scale));
+  }
+}
+
+__global__ void eval_any_reduce(const uint32_t* partial, uint32_t nchunks, uint32_t* out, uint32_t evals) {
+  uint32_t k = blockIdx.x * kThreads + threadIdx.x;
+  if (k >= evals) return;
+  FpExt s = fe_zero();
+  for (uint32_t c = 0; c < nchunks; c++) s = fe_add(s, ld_fe(partial + (uint64_t(k) * nchunks + c) * 4));
+  st_fe(out + uint64_t(k) * 4, s);
+}
+
+// ---- prefix products (cpu.rs:637-642), serial by definition --------------------------
+__global__ void prefix_products_kernel(uint32_t* io, uint64_t n) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  FpExt prev = ld_fe(io);
+  for (uint64_t i = 1; i < n; i++) {
+    prev = fe_mul(ld_fe(io + 4 * i), prev);
+    st_fe(io + 4 * i, prev);
+  }
+}
+
+// ---- synthetic division (core/poly.rs:81-89) -----------------------------------------
+// p(x) = q(x) (x - z) + r. Going down from the top, cur_i = z*cur_{i+1} + p_i and
+// p_i <- cur_{i+1}. A lane owning 16 coefficients maps an incoming carry c to
+// Z*c + L (Z = z^16, L = its local sum), an affine map; composing maps is
+// associative, so the row is solved as a two-level scan:
+//   div_local  : each lane computes L
+//   div_block  : each 256-lane workgroup scans its maps (Hillis-Steele in LDS),
+//                keeps per-lane "maps of the lanes above me" and its block map
+//   div_top    : one workgroup per row scans the block maps from the top and
+//                produces each block's carry-in and the remainder cur_0
+//   div_apply  : each lane rewrites its 16 quotients from its carry-in
+// All rows of one division round run in the same launches (grid.y = row).
+constexpr int kDivPer = 16;
+
+struct DivRow {
+  uint32_t* p;     // row base (FpExt AoS)
+  FpExt z;
+};
+
+__global__ __launch_bounds__(kThreads) void div_local_kernel(const DivRow* rows, uint32_t nlanes, uint32_t* lanev) {
+  const DivRow r = rows[blockIdx.y];
+  uint32_t lane = blockIdx.x * kThreads + threadIdx.x;
+  if (lane >= nlanes) return;
+  const uint32_t* p = r.p + uint64_t(lane) * kDivPer * 4;
+  FpExt cur = fe_zero();
+#pragma unroll
+  for (int i = kDivPer - 1; i >= 0; i--) cur = fe_add(fe_mul(r.z, cur), ld_fe(p + 4 * i));
+  st_fe(lanev + (uint64_t(blockIdx.y) * nlanes + lane) * 4, cur);
+}
+
+// in: lanev = L per lane. out: lanev = v_{t+1}, lanem = m_{t+1} (maps of lanes above
+// t inside the block), blockv/blockm = whole-block map.
+__global__ __launch_bounds__(kThreads) void div_block_kernel(const DivRow* rows, uint32_t nlanes, uint32_t* lanev,
+                                                            uint32_t* lanem, uint32_t* blockv, uint32_t* blockm) {
+  __shared__ FpExt vals[kThreads + 1];
+  __shared__ FpExt mul[kThreads + 1];
+  const uint32_t row = blockIdx.y, tid = threadIdx.x, nblocks = gridDim.x;
+  const uint32_t lane = blockIdx.x * kThreads + tid;
+  const FpExt Z = fe_pow(rows[row].z, kDivPer);
+  uint32_t* lv = lanev + (uint64_t(row) * nlanes) * 4;
+  vals[tid] = lane < nlanes ? ld_fe(lv + uint64_t(lane) * 4) : fe_zero();
+  mul[tid] = lane < nlanes ? Z : fe_one();
+  if (tid == 0) {
+    vals[kThreads] = fe_zero();
+    mul[kThreads] = fe_one();
+  }
+  __syncthreads();
+  for (uint32_t off = 1; off < kThreads; off <<= 1) {
+    FpExt v = vals[tid], m = mul[tid];
+    if (tid + off < kThreads) {
+      v = fe_add(v, fe_mul(m, vals[tid + off]));
+      m = fe_mul(m, mul[tid + off]);
+    }
+    __syncthreads();
+    vals[tid] = v;
+    mul[tid] = m;
+    __syncthreads();
+  }
+  if (lane < nlanes) {
+    st_fe(lv + uint64_t(lane) * 4, vals[tid + 1]);
+    st_fe(lanem + (uint64_t(row) * nlanes + lane) * 4, mul[tid + 1]);
+  }
+  if (tid == 0) {
+    st_fe(blockv + (uint64_t(row) * nblocks + blockIdx.x) * 4, vals[0]);
+    st_fe(blockm + (uint64_t(row) * nblocks + blockIdx.x) * 4, mul[0]);
+  }
+}
+
+// blockv <- carry into the top lane of each block; rem[row] = cur_0.
+__global__ __launch_bounds__(kThreads) void div_top_kernel(uint32_t nblocks, uint32_t* blockv, const uint32_t* blockm,
+                                                          uint32_t* rem) {
+  __shared__ FpExt vals[kThreads + 1];
+  __shared__ FpExt mul[kThreads + 1];
+  const uint32_t row = blockIdx.x, tid = threadIdx.x;
+  uint32_t* bv = blockv + uint64_t(row) * nblocks * 4;
+  const uint32_t* bm = blockm + uint64_t(row) * nblocks * 4;
+  FpExt carry = fe_zero();
+  uint32_t nseg = (nblocks + kThreads - 1) / kThreads;
+  for (int seg = int(nseg) - 1; seg >= 0; seg--) {
+    uint32_t b = uint32_t(seg) * kThreads + tid;
+    vals[tid] = b < nblocks ? ld_fe(bv + uint64_t(b) * 4) : fe_zero();
+    mul[tid] = b < nblocks ? ld_fe(bm + uint64_t(b) * 4) : fe_one();
+    if (tid == 0) {
+      vals[kThreads] = fe_zero();
+      mul[kThreads] = fe_one();
+    }
+    __syncthreads();
+    for (uint32_t off = 1; off < kThreads; off <<= 1) {
+      FpExt v = vals[tid], m = mul[tid];
+      if (tid + off < kThreads) {
+        v = fe_add(v, fe_mul(m, vals[tid + off]));
+        m = fe_mul(m, mul[tid + off]);
+      }
+      __syncthreads();
+      vals[tid] = v;
+      mul[tid] = m;
+      __syncthreads();
+    }
+    FpExt cin = fe_add(vals[tid + 1], fe_mul(mul[tid + 1], carry));
+    FpExt total = fe_add(vals[0], fe_mul(mul[0], carry));
+    __syncthreads();
+    if (b < nblocks) st_fe(bv + uint64_t(b) * 4, cin);
+    carry = total;
+  }
+  if (tid == 0) st_fe(rem + 4 * row, carry);
+}
+
+__global__ __launch_bounds__(kThreads) void div_apply_kernel(const DivRow* rows, uint32_t nlanes, const uint32_t* lanev,
+                                                            const uint32_t* lanem, const uint32_t* blockv) {
+  const DivRow r = rows[blockIdx.y];
+  const uint32_t lane = blockIdx.x * kThreads + threadIdx.x;
+  if (lane >= nlanes) return;
+  const uint64_t li = uint64_t(blockIdx.y) * nlanes + lane;
+  FpExt bc = ld_fe(blockv + (uint64_t(blockIdx.y) * gridDim.x + blockIdx.x) * 4);
+  FpExt cur = fe_add(ld_fe(lanev + li * 4), fe_mul(ld_fe(lanem + li * 4), bc));
+  uint32_t* p = r.p + uint64_t(lane) * kDivPer * 4;
+#pragma unroll
+  for (int i = kDivPer - 1; i >= 0; i--) {
+    FpExt pi = ld_fe(p + 4 * i);
+    st_fe(p + 4 * i, cur);
+    cur = fe_add(fe_mul(r.z, cur), pi);
+  }
+}
+
+// rows whose length is not a multiple of 16: one lane per row, serial
+__global__ void div_serial_kernel(const DivRow* rows, uint64_t n, uint32_t* rem, uint32_t nrows) {
+  uint32_t row = blockIdx.x * kThreads + threadIdx.x;
+  if (row >= nrows) return;
+  const DivRow r = rows[row];
+  FpExt cur = fe_zero();
+  for (uint64_t i = n; i-- > 0;) {
+    FpExt pi = ld_fe(r.p + 4 * i);
+    st_fe(r.p + 4 * i, cur);
+    cur = fe_add(fe_mul(r.z, cur), pi);
+  }
+  st_fe(rem + 4 * row, cur);
+}
+
+// combos_prepare tail (hal/mod.rs:212-233): combos[r*cycles + i] -= deltas[r*width + i]
+__global__ void combos_sub_kernel(uint32_t* combos, const uint32_t* deltas, uint32_t rows, uint32_t width,
+                                  uint64_t cycles) {
+  uint32_t t = blockIdx.x * kThreads + threadIdx.x;
+  if (t >= rows * width) return;
+  uint32_t r = t / width, i = t % width;
+  if (i >= cycles) return;
+  uint32_t* p = combos + (uint64_t(r) * cycles + i) * 4;
+  st_fe(p, fe_sub(ld_fe(p), ld_fe(deltas + uint64_t(t) * 4)));
+}
+
+// Query openings: dst[i] = bases[base_id[i]][offsets[i]]
+__global__ void gather_words_kernel(uint32_t* dst, const uint32_t* const* bases, const uint32_t* base_id,
+                                    const uint64_t* offsets, uint64_t n) {
+  uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (i < n) dst[i] = bases[base_id[i]][offsets[i]];
+}
+
+}  // namespace
+
+void eltwise_add(hipStream_t s, uint32_t* out, const uint32_t* a, const uint32_t* b, size_t n) {
+  if (!n) return;
+  hipLaunchKernelGGL(add_kernel, dim3(div_up(n, kThreads)), dim3(kThreads), 0, s, out, a, b, uint64_t(n));
+  HIP_OK(hipGetLastError());
+}
+void eltwise_copy(hipStream_t s, uint32_t* out, const uint32_t* in, size_t n) {
+  if (!n || out == in) return;
+  HIP_OK(hipMemcpyAsync(out, in, n * 4, hipMemcpyDeviceToDevice, s));
+}
+void eltwise_zeroize(hipStream_t s, uint32_t* io, size_t n) {
+  if (!n) return;
+  hipLaunchKernelGGL(zeroize_kernel, dim3(div_up(n, kThreads)), dim3(kThreads), 0, s, io, uint64_t(n));
+  HIP_OK(hipGetLastError());
+}
+void eltwise_sum_extelem(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count, size_t to_add) {
+  if (!count) return;
+  hipLaunchKernelGGL(sum_extelem_kernel, dim3(div_up(count, kThreads)), dim3(kThreads), 0, s, out, in,
+                     uint64_t(count), uint32_t(to_add));
+  HIP_OK(hipGetLastError());
+}
+void fri_fold(hipStream_t s, uint32_t* out, const uint32_t* in, FpExt mix, size_t count) {
+  if (!count) return;
+  hipLaunchKernelGGL(fri_fold_kernel, dim3(div_up(count, kThreads)), dim3(kThreads), 0, s, out, in, mix,
+                     uint64_t(count));
+  HIP_OK(hipGetLastError());
+}
+void gather_sample(hipStream_t s, uint32_t* dst, const uint32_t* src, size_t idx, size_t size, size_t stride) {
+  if (!size) return;
+  hipLaunchKernelGGL(gather_kernel, dim3(div_up(size, kThreads)), dim3(kThreads), 0, s, dst, src, uint64_t(idx),
+                     uint64_t(size), uint64_t(stride));
+  HIP_OK(hipGetLastError());
+}
+void scatter(hipStream_t s, uint32_t* into, const uint32_t* index, const uint32_t* offsets, const uint32_t* values,
+             size_t cycles) {
+  if (!cycles) return;
+  hipLaunchKernelGGL(scatter_kernel, dim3(div_up(cycles, kThreads)), dim3(kThreads), 0, s, into, index, offsets,
+                     values, uint64_t(cycles));
+  HIP_OK(hipGetLastError());
+}
+void copy_elem_slice(hipStream_t s, uint32_t* into, const uint32_t* from, size_t rows, size_t cols,
+                     size_t from_offset, size_t from_stride, size_t into_offset, size_t into_stride) {
+  if (!rows || !cols) return;
+  hipLaunchKernelGGL(copy_slice_kernel, dim3(div_up(rows * cols, kThreads)), dim3(kThreads), 0, s, into, from,
+                     uint64_t(rows), uint64_t(cols), uint64_t(from_offset), uint64_t(from_stride),
+                     uint64_t(into_offset), uint64_t(into_stride));
+  HIP_OK(hipGetLastError());
+}
+void prefix_products(hipStream_t s, uint32_t* io, size_t n) {
+  if (n < 2) return;
+  hipLaunchKernelGGL(prefix_products_kernel, dim3(1), dim3(64), 0, s, io, uint64_t(n));
+  HIP_OK(hipGetLastError());
+}
+
+void mix_poly_coeffs(hipStream_t s, uint32_t* out, const uint32_t* in, const uint32_t* combos_dev,
+                     const std::vector<uint32_t>& combos_host, FpExt mix_start, FpExt mix, size_t input_size,
+                     size_t count) {
+  if (!count || !input_size) return;
+  uint32_t used = 0, maxc = 0;
+  for (uint32_t c : combos_host) {
+    R0_REQUIRE(c < 32, "mix_poly_coeffs: combo id too large");
+    used |= 1u << c;
+    maxc = std::max(maxc, c);
+  }
+  std::vector<uint32_t> pows(input_size * 4);
+  FpExt cur = mix_start;
+  for (size_t i = 0; i < input_size; i++) {
+    for (int k = 0; k < 4; k++) pows[4 * i + k] = cur.c[k];
+    cur = fe_mul(cur, mix);
+  }
+  uint32_t* dpows = static_cast<uint32_t*>(scratch(pows.size() * 4, 1));
+  upload_async(dpows, pows.data(), pows.size() * 4);
+  dim3 grid(div_up(count, kThreads));
+  if (maxc < 2) hipLaunchKernelGGL(mix_kernel<2>, grid, dim3(kThreads), 0, s, out, in, combos_dev, dpows, uint32_t(input_size), uint64_t(count), used);
+  else if (maxc < 4) hipLaunchKernelGGL(mix_kernel<4>, grid, dim3(kThreads), 0, s, out, in, combos_dev, dpows, uint32_t(input_size), uint64_t(count), used);
+  else if (maxc < kMaxCombos) hipLaunchKernelGGL(mix_kernel<kMaxCombos>, grid, dim3(kThreads), 0, s, out, in, combos_dev, dpows, uint32_t(input_size), uint64_t(count), used);
+  else R0_REQUIRE(false, "mix_poly_coeffs: more than 8 combos");
+  HIP_OK(hipGetLastError());
+}
+
+void batch_evaluate_any(hipStream_t s, const uint32_t* coeffs, size_t poly_count, uint32_t log_n,
+                        const uint32_t* which, const uint32_t* xs, uint32_t* out, size_t eval_count) {
+  if (!eval_count) return;
+  (void)poly_count;
+  uint64_t n = uint64_t(1) << log_n;
+  uint32_t nchunks = uint32_t((n + kEvChunk - 1) / kEvChunk);
+  R0_REQUIRE(n % kEvPer == 0, "batch_evaluate_any: poly size must be a multiple of 16");
+  R0_REQUIRE(eval_count < 65536, "batch_evaluate_any: too many evaluations");
+  uint32_t* partial = static_cast<uint32_t*>(scratch(size_t(eval_count) * nchunks * 16, 2));
+  hipLaunchKernelGGL(eval_any_kernel, dim3(nchunks, unsigned(eval_count)), dim3(kThreads), 0, s, coeffs, log_n,
+                     which, xs, partial, nchunks);
+  HIP_OK(hipGetLastError());
+  hipLaunchKernelGGL(eval_any_reduce, dim3(div_up(eval_count, kThreads)), dim3(kThreads), 0, s, partial, nchunks,
+                     out, uint32_t(eval_count));
+  HIP_OK(hipGetLastError());
+}
+
+void poly_divide_rows(hipStream_t s, uint32_t* io, size_t n, const std::vector<std::vector<FpExt>>& zs,
+                      uint32_t* rem_dev) {
+  size_t rows = zs.size();
+  size_t maxz = 0;
+  for (auto& v : zs) maxz = std::max(maxz, v.size());
+  if (!rows || !maxz || !n) return;
+  // round k divides every row that has a k-th z (the rows' z lists run in order)
+  for (size_t k = 0; k < maxz; k++) {
+    std::vector<DivRow> rs;
+    std::vector<uint32_t> ids;
+    for (size_t r = 0; r < rows; r++)
+      if (k < zs[r].size()) {
+        rs.push_back(DivRow{io + uint64_t(r) * n * 4, zs[r][k]});
+        ids.push_back(uint32_t(r));
+      }
+    uint32_t nr = uint32_t(rs.size());
+    DivRow* drows = static_cast<DivRow*>(scratch(rs.size() * sizeof(DivRow), 3 + int(k % 2) * 100));
+    upload_async(drows, rs.data(), rs.size() * sizeof(DivRow));
+    uint32_t* rem = static_cast<uint32_t*>(scratch(size_t(nr) * 16, 4));
+    if (n % kDivPer != 0) {
+      hipLaunchKernelGGL(div_serial_kernel, dim3(div_up(nr, kThreads)), dim3(kThreads), 0, s, drows, uint64_t(n),
+                         rem, nr);
+      HIP_OK(hipGetLastError());
+    } else {
+      uint32_t nlanes = uint32_t(n / kDivPer);
+      uint32_t nblocks = div_up(nlanes, kThreads);
+      uint32_t* lanev = static_cast<uint32_t*>(scratch(size_t(nr) * nlanes * 16, 5));
+      uint32_t* lanem = static_cast<uint32_t*>(scratch(size_t(nr) * nlanes * 16, 6));
+      uint32_t* blockv = static_cast<uint32_t*>(scratch(size_t(nr) * nblocks * 16, 7));
+      uint32_t* blockm = static_cast<uint32_t*>(scratch(size_t(nr) * nblocks * 16, 8));
+      hipLaunchKernelGGL(div_local_kernel, dim3(nblocks, nr), dim3(kThreads), 0, s, drows, nlanes, lanev);
+      HIP_OK(hipGetLastError());
+      hipLaunchKernelGGL(div_block_kernel, dim3(nblocks, nr), dim3(kThreads), 0, s, drows, nlanes, lanev, lanem,
+                         blockv, blockm);
+      HIP_OK(hipGetLastError());
+      hipLaunchKernelGGL(div_top_kernel, dim3(nr), dim3(kThreads), 0, s, nblocks, blockv, blockm, rem);
+      HIP_OK(hipGetLastError());
+      hipLaunchKernelGGL(div_apply_kernel, dim3(nblocks, nr), dim3(kThreads), 0, s, drows, nlanes, lanev, lanem,
+                         blockv);
+      HIP_OK(hipGetLastError());
+    }
+    for (uint32_t t = 0; t < nr; t++)
+      HIP_OK(hipMemcpyAsync(rem_dev + (uint64_t(ids[t]) * maxz + k) * 4, rem + 4 * t, 16, hipMemcpyDeviceToDevice, s));
+  }
+}
+
+void combos_sub(hipStream_t s, uint32_t* combos, const uint32_t* deltas, size_t rows, size_t width,
+                size_t cycles) {
+  if (!rows || !width) return;
+  hipLaunchKernelGGL(combos_sub_kernel, dim3(div_up(rows * width, kThreads)), dim3(kThreads), 0, s, combos, deltas,
+                     uint32_t(rows), uint32_t(width), uint64_t(cycles));
+  HIP_OK(hipGetLastError());
+}
+
+void gather_words(hipStream_t s, uint32_t* dst, const uint32_t* const* bases, const uint32_t* base_id,
+                  const uint64_t* offsets, size_t n) {
+  if (!n) return;
+  hipLaunchKernelGGL(gather_words_kernel, dim3(div_up(n, kThreads)), dim3(kThreads), 0, s, dst, bases, base_id,
+                     offsets, uint64_t(n));
+  HIP_OK(hipGetLastError());
+}
+
+}  // namespace r0

@@ -1,0 +1,34 @@
+// Interface between the host driver and the generated per-circuit eval_check
+// kernels (risc0_amd/csrc/gen/eval_check_<circuit>.hip, emitted at build time by
+// tools/gen_eval_check.py from risc0_amd/circuits/<circuit>.poly.ir).
+#pragma once
+#include "runtime.h"
+
+namespace r0 {
+
+struct EvalCheckArgs {
+  const uint32_t* const* args;  // poly_fp argument buffers, circuit order
+  size_t nargs;
+  const uint32_t* poly_mix;     // poly_mix powers + folded products (FpExt AoS, Montgomery)
+  uint32_t* acc;                // scratch: domain x FpExt
+  uint32_t* check;              // out: 4 x domain
+  const uint32_t* vinv;         // 4 values: inv((3 w^c)^N - 1) for c = 0..3
+  uint32_t* mat_fp;             // scratch: mat_fp x domain words
+  uint32_t* mat_ext;            // scratch: mat_ext x domain FpExt
+  uint32_t domain;
+};
+
+struct EvalCheckInfo {
+  const int* combos;  // for each folded product: count, then indices into the powers
+  int ncombos;
+  int npm;            // number of poly_mix powers the kernels index directly
+  int nargs;
+  int mat_fp, mat_ext, kernels;
+};
+
+void eval_check_rv32im(hipStream_t s, const EvalCheckArgs& e);
+void eval_check_rv32im_info(EvalCheckInfo* info);
+void eval_check_recursion(hipStream_t s, const EvalCheckArgs& e);
+void eval_check_recursion_info(EvalCheckInfo* info);
+
+}  // namespace r0

@@ -1,0 +1,214 @@
+// Merkle leaf and node hashing on CDNA4: Poseidon2 and SHA-256 row hashes
+// (hash_rows) and pair compressions (hash_fold), and a fused tree builder.
+//
+//   hash_rows : risc0/zkp/src/hal/cpu.rs:555-567 -> HashFn::hash_elem_slice of one
+//               row of a column-major matrix (poseidon2/mod.rs:221-245 unpadded
+//               sponge; sha/cpu.rs:56-77 unpadded SHA-256 over LE word bytes)
+//   hash_fold : cpu.rs:569-581 -> HashFn::hash_pair (poseidon2/mod.rs:47-59;
+//               sha/mod.rs:96-98 single compression from the IV)
+// One lane hashes one row: consecutive lanes read consecutive rows of each
+// column, so every column read is a fully coalesced 256-byte wave access; the
+// 24-cell state lives in VGPRs. Poseidon2 is integer-VALU bound (~1.4k modmul per
+// permutation), not HBM bound.
+#include "poseidon2.h"
+#include "runtime.h"
+
+namespace r0 {
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ void store_digest(uint32_t* out, const uint32_t* d) {
+  uint4* o = reinterpret_cast<uint4*>(out);
+  o[0] = make_uint4(d[0], d[1], d[2], d[3]);
+  o[1] = make_uint4(d[4], d[5], d[6], d[7]);
+}
+
+__global__ __launch_bounds__(kThreads) void p2_rows_kernel(uint32_t* out, const uint32_t* __restrict__ m,
+                                                         uint64_t rows, uint32_t cols) {
+  uint64_t row = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (row >= rows) return;
+  uint32_t c[24];
+#pragma unroll
+  for (int i = 0; i < 24; i++) c[i] = 0;
+  uint32_t col = 0;
+  // full blocks of 16 columns
+  for (; col + 16 <= cols; col += 16) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) c[i] = m[uint64_t(col + i) * rows + row];
+    poseidon2_mix(c);
+  }
+  if (col < cols || cols == 0) {
+    uint32_t rem = cols - col;
+#pragma unroll
+    for (int i = 0; i < 16; i++) c[i] = (uint32_t)i < rem ? m[uint64_t(col + i) * rows + row] : 0u;
+    poseidon2_mix(c);
+  }
+  store_digest(out + row * 8, c);
+}
+
+__global__ __launch_bounds__(kThreads) void p2_fold_kernel(uint32_t* io, uint64_t in_off, uint64_t out_off,
+                                                         uint64_t n) {
+  uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const uint4* src = reinterpret_cast<const uint4*>(io + (in_off + 2 * i) * 8);
+  uint32_t c[24];
+  uint4 a = src[0], b = src[1], d = src[2], e = src[3];
+  c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w; c[4] = b.x; c[5] = b.y; c[6] = b.z; c[7] = b.w;
+  c[8] = d.x; c[9] = d.y; c[10] = d.z; c[11] = d.w; c[12] = e.x; c[13] = e.y; c[14] = e.z; c[15] = e.w;
+#pragma unroll
+  for (int k = 16; k < 24; k++) c[k] = 0;
+  poseidon2_mix(c);
+  store_digest(io + (out_off + i) * 8, c);
+}
+
+// ---- SHA-256 ------------------------------------------------------------------
+__constant__ static const uint32_t kK256[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_rotateright32(x, n); }
+
+// FIPS 180-4 compression; w[] holds the 16 big-endian message words.
+__device__ __forceinline__ void sha_compress(uint32_t* s, uint32_t* w) {
+  uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+#pragma unroll
+  for (int i = 0; i < 64; i++) {
+    uint32_t wi;
+    if (i < 16) {
+      wi = w[i];
+    } else {
+      uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
+      uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
+      uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+      wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
+      w[i & 15] = wi;
+    }
+    uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+    uint32_t ch = (e & f) ^ (~e & g);
+    uint32_t t1 = h + S1 + ch + kK256[i] + wi;
+    uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+  }
+  s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
+}
+
+__device__ __forceinline__ void sha_init(uint32_t* s) {
+  s[0] = 0x6a09e667; s[1] = 0xbb67ae85; s[2] = 0x3c6ef372; s[3] = 0xa54ff53a;
+  s[4] = 0x510e527f; s[5] = 0x9b05688c; s[6] = 0x1f83d9ab; s[7] = 0x5be0cd19;
+}
+
+// Digest words are the big-endian digest bytes in memory order: bswap each state word.
+__global__ __launch_bounds__(kThreads) void sha_rows_kernel(uint32_t* out, const uint32_t* __restrict__ m,
+                                                          uint64_t rows, uint32_t cols) {
+  uint64_t row = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (row >= rows) return;
+  uint32_t s[8], w[16];
+  sha_init(s);
+  for (uint32_t col = 0; col < cols; col += 16) {
+#pragma unroll
+    for (int i = 0; i < 16; i++)
+      w[i] = (col + i < cols) ? __builtin_bswap32(m[uint64_t(col + i) * rows + row]) : 0u;
+    sha_compress(s, w);
+  }
+  uint32_t d[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) d[i] = __builtin_bswap32(s[i]);
+  store_digest(out + row * 8, d);
+}
+
+__global__ __launch_bounds__(kThreads) void sha_fold_kernel(uint32_t* io, uint64_t in_off, uint64_t out_off,
+                                                          uint64_t n) {
+  uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t* src = io + (in_off + 2 * i) * 8;
+  uint32_t s[8], w[16];
+  sha_init(s);
+#pragma unroll
+  for (int k = 0; k < 16; k++) w[k] = __builtin_bswap32(src[k]);
+  sha_compress(s, w);
+  uint32_t d[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) d[k] = __builtin_bswap32(s[k]);
+  store_digest(io + (out_off + i) * 8, d);
+}
+
+// Top of a tree inside one workgroup: layers with <= 512 nodes, all hashed by
+// 256 lanes with a workgroup barrier between layers (same-CU visibility).
+template <int SUITE>
+__global__ __launch_bounds__(kThreads) void fold_top_kernel(uint32_t* io, uint32_t top_layer_size) {
+  for (uint32_t out = top_layer_size; out >= 1; out >>= 1) {
+    for (uint32_t i = threadIdx.x; i < out; i += kThreads) {
+      const uint32_t* src = io + (uint64_t(2 * out) + 2 * i) * 8;
+      uint32_t d[8];
+      if (SUITE == 0) {
+        uint32_t c[24];
+#pragma unroll
+        for (int k = 0; k < 16; k++) c[k] = src[k];
+#pragma unroll
+        for (int k = 16; k < 24; k++) c[k] = 0;
+        poseidon2_mix(c);
+#pragma unroll
+        for (int k = 0; k < 8; k++) d[k] = c[k];
+      } else {
+        uint32_t s[8], w[16];
+        sha_init(s);
+#pragma unroll
+        for (int k = 0; k < 16; k++) w[k] = __builtin_bswap32(src[k]);
+        sha_compress(s, w);
+#pragma unroll
+        for (int k = 0; k < 8; k++) d[k] = __builtin_bswap32(s[k]);
+      }
+      store_digest(io + (uint64_t(out) + i) * 8, d);
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+void hash_rows(hipStream_t s, int suite, uint32_t* out, const uint32_t* matrix, size_t rows, size_t cols) {
+  if (rows == 0) return;
+  R0_REQUIRE(cols < (1ull << 31), "hash_rows: too many columns");
+  if (suite == 0)
+    hipLaunchKernelGGL(p2_rows_kernel, dim3(div_up(rows, kThreads)), dim3(kThreads), 0, s, out, matrix,
+                       uint64_t(rows), uint32_t(cols));
+  else
+    hipLaunchKernelGGL(sha_rows_kernel, dim3(div_up(rows, kThreads)), dim3(kThreads), 0, s, out, matrix,
+                       uint64_t(rows), uint32_t(cols));
+  HIP_OK(hipGetLastError());
+}
+
+void hash_fold(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t output_size) {
+  if (output_size == 0) return;
+  R0_REQUIRE(input_size == 2 * output_size, "hash_fold: input_size != 2*output_size");
+  if (suite == 0)
+    hipLaunchKernelGGL(p2_fold_kernel, dim3(div_up(output_size, kThreads)), dim3(kThreads), 0, s, io,
+                       uint64_t(input_size), uint64_t(output_size), uint64_t(output_size));
+  else
+    hipLaunchKernelGGL(sha_fold_kernel, dim3(div_up(output_size, kThreads)), dim3(kThreads), 0, s, io,
+                       uint64_t(input_size), uint64_t(output_size), uint64_t(output_size));
+  HIP_OK(hipGetLastError());
+}
+
+// MerkleTreeProver::new (risc0/zkp/src/prove/merkle.rs:54-81): leaves, then every layer.
+void merkle_tree(hipStream_t s, int suite, uint32_t* nodes, const uint32_t* matrix, size_t rows, size_t cols) {
+  hash_rows(s, suite, nodes + rows * 8, matrix, rows, cols);
+  size_t layer = rows / 2;
+  for (; layer > 512; layer /= 2) hash_fold(s, suite, nodes, 2 * layer, layer);
+  if (layer >= 1) {
+    if (suite == 0) hipLaunchKernelGGL(fold_top_kernel<0>, dim3(1), dim3(kThreads), 0, s, nodes, uint32_t(layer));
+    else hipLaunchKernelGGL(fold_top_kernel<1>, dim3(1), dim3(kThreads), 0, s, nodes, uint32_t(layer));
+    HIP_OK(hipGetLastError());
+  }
+}
+
+}  // namespace r0

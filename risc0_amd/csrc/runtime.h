@@ -1,0 +1,87 @@
+// Host-side runtime shared by the C ABI (api.cpp), the segment prover
+// (prover.cpp) and the kernel launchers: error plumbing, the per-process HIP
+// stream, cached constant tables in HBM, and the launcher declarations.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <functional>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "bb31.h"
+
+#define HIP_OK(expr)                                                                          \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess)                                                                     \
+      throw std::runtime_error(std::string(#expr) + " failed: " + hipGetErrorString(e_) +     \
+                               " (" + __FILE__ + ":" + std::to_string(__LINE__) + ")");      \
+  } while (0)
+
+#define R0_REQUIRE(cond, msg)                                             \
+  do {                                                                    \
+    if (!(cond)) throw std::runtime_error(std::string("r0hip: ") + (msg)); \
+  } while (0)
+
+namespace r0 {
+
+// Per-process stream on the current device (created by r0hip_init / lazily).
+hipStream_t stream();
+void ensure_init();
+
+// Constant tables kept resident in HBM for the life of the process, keyed by a
+// string; `gen` runs on the host once per key.
+const uint32_t* dev_table(const std::string& key, const std::function<std::vector<uint32_t>()>& gen);
+
+// Scratch buffer reused across calls (grown on demand; stream-ordered use only).
+void* scratch(size_t bytes, int slot = 0);
+
+// Stream-ordered host->device upload through a pinned bump arena, so the caller's
+// host data may die immediately. The arena is recycled by stage_reset() (call only
+// when the stream is idle).
+void upload_async(void* d_dst, const void* h_src, size_t bytes);
+void stage_reset();
+
+inline unsigned div_up(size_t a, size_t b) { return unsigned((a + b - 1) / b); }
+
+// ---- launchers (all asynchronous on `s`) -----------------------------------
+// NTT family (ntt.hip). Sizes are log2 of the per-polynomial length.
+void ntt_evaluate(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count, uint32_t log_out,
+                  uint32_t expand_bits);
+void ntt_interpolate(hipStream_t s, uint32_t* io, size_t count, uint32_t log_n, bool zk_shift);
+void bit_reverse(hipStream_t s, uint32_t* io, size_t count, uint32_t log_n);
+void zk_shift(hipStream_t s, uint32_t* io, size_t count, uint32_t log_n);
+
+// Hashes (poseidon2.hip / sha256.hip). suite: 0 = poseidon2, 1 = sha-256.
+void hash_rows(hipStream_t s, int suite, uint32_t* out, const uint32_t* matrix, size_t rows, size_t cols);
+void hash_fold(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t output_size);
+// Full merkle tree: nodes[rows..2rows) = leaves, hashes every layer up to the root.
+void merkle_tree(hipStream_t s, int suite, uint32_t* nodes, const uint32_t* matrix, size_t rows, size_t cols);
+
+// Element-wise and polynomial kernels (eltwise.hip).
+void eltwise_add(hipStream_t s, uint32_t* out, const uint32_t* a, const uint32_t* b, size_t n);
+void eltwise_copy(hipStream_t s, uint32_t* out, const uint32_t* in, size_t n);
+void eltwise_zeroize(hipStream_t s, uint32_t* io, size_t n);
+void eltwise_sum_extelem(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count, size_t to_add);
+void fri_fold(hipStream_t s, uint32_t* out, const uint32_t* in, FpExt mix, size_t count);
+void gather_sample(hipStream_t s, uint32_t* dst, const uint32_t* src, size_t idx, size_t size, size_t stride);
+void mix_poly_coeffs(hipStream_t s, uint32_t* out, const uint32_t* in, const uint32_t* combos_dev,
+                     const std::vector<uint32_t>& combos_host, FpExt mix_start, FpExt mix,
+                     size_t input_size, size_t count);
+void batch_evaluate_any(hipStream_t s, const uint32_t* coeffs, size_t poly_count, uint32_t log_n,
+                        const uint32_t* which, const uint32_t* xs, uint32_t* out, size_t eval_count);
+void scatter(hipStream_t s, uint32_t* into, const uint32_t* index, const uint32_t* offsets,
+             const uint32_t* values, size_t cycles);
+void copy_elem_slice(hipStream_t s, uint32_t* into, const uint32_t* from, size_t rows, size_t cols,
+                     size_t from_offset, size_t from_stride, size_t into_offset, size_t into_stride);
+void prefix_products(hipStream_t s, uint32_t* io, size_t n);
+// In-place synthetic division of `nrows` FpExt polys of length n (row r at io + r*n*4)
+// by (x - z_k) for each of its z's, in order. zs/zbegin: flattened per-row lists.
+// The remainders (must be zero) are written to rem_dev[row*maxz + k].
+void poly_divide_rows(hipStream_t s, uint32_t* io, size_t n, const std::vector<std::vector<FpExt>>& zs,
+                      uint32_t* rem_dev);
+
+}  // namespace r0

@@ -1,0 +1,329 @@
+"""Python mirror of the risc0_zkp `Hal` trait over the r0hip C ABI.
+
+`HipHal` exposes the same method names and argument meanings as
+risc0/zkp/src/hal/mod.rs:55-258 (buffers are device allocations of u32 words:
+Elem = 1 word, ExtElem = 4, Digest = 8), so the parity tests read like the
+reference's DualHal tests (risc0/zkp/src/hal/mod.rs:319-616). It is a thin
+ctypes layer: every operation runs in libr0hip.so on the GPU. There is no CPU
+fallback; a missing library or device raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libr0hip.so")
+
+POSEIDON2, SHA256 = 0, 1
+SUITES = {"poseidon2": POSEIDON2, "sha-256": SHA256}
+
+_lib = None
+u32p = C.POINTER(C.c_uint32)
+
+
+class R0HipError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libr0hip.so (built by __graft_entry__.build()); raise if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise R0HipError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB_PATH)
+        for name in dir(L):
+            pass
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+def _declare(L):
+    sz = C.c_size_t
+    vp = C.c_void_p
+    sig = {
+        "r0hip_init": [C.c_int],
+        "r0hip_device_info": [C.c_char_p, sz, C.POINTER(C.c_uint64)],
+        "r0hip_alloc": [C.POINTER(vp), sz],
+        "r0hip_free": [vp],
+        "r0hip_memset32": [vp, C.c_uint32, sz],
+        "r0hip_memcpy_h2d": [vp, vp, sz],
+        "r0hip_memcpy_d2h": [vp, vp, sz],
+        "r0hip_memcpy_d2d": [vp, vp, sz],
+        "r0hip_synchronize": [],
+        "r0hip_batch_expand_into_evaluate_ntt": [vp, vp, sz, C.c_uint32, C.c_uint32],
+        "r0hip_batch_interpolate_ntt": [vp, sz, C.c_uint32],
+        "r0hip_zk_shift": [vp, sz, C.c_uint32],
+        "r0hip_batch_bit_reverse": [vp, sz, C.c_uint32],
+        "r0hip_batch_evaluate_any": [vp, vp, sz, C.c_uint32, vp, vp, sz],
+        "r0hip_mix_poly_coeffs": [vp, vp, u32p, u32p, u32p, sz, sz],
+        "r0hip_fri_fold": [vp, vp, u32p, sz],
+        "r0hip_combos_prepare": [vp, u32p, sz, sz, u32p, u32p, sz, u32p],
+        "r0hip_poly_divide": [vp, sz, u32p, u32p],
+        "r0hip_combos_divide": [vp, sz, u32p, u32p, sz, C.POINTER(C.c_int64)],
+        "r0hip_eltwise_add_elem": [vp, vp, vp, sz],
+        "r0hip_eltwise_copy_elem": [vp, vp, sz],
+        "r0hip_eltwise_zeroize_elem": [vp, sz],
+        "r0hip_eltwise_sum_extelem": [vp, vp, sz, sz],
+        "r0hip_eltwise_copy_elem_slice": [vp, vp, sz, sz, sz, sz, sz, sz],
+        "r0hip_gather_sample": [vp, vp, sz, sz, sz],
+        "r0hip_scatter": [vp, vp, vp, vp, sz],
+        "r0hip_prefix_products": [vp, sz],
+        "r0hip_hash_rows": [C.c_int, vp, vp, sz, sz],
+        "r0hip_hash_fold": [C.c_int, vp, sz, sz],
+        "r0hip_eval_check": [C.c_char_p, vp, C.POINTER(vp), vp, vp, u32p, C.c_uint32],
+        "r0hip_prove_segment": [C.c_char_p, C.c_int, C.c_uint32, vp, vp, vp, vp, C.c_int, C.c_uint32, u32p, sz,
+                                C.POINTER(sz), u32p],
+        "r0hip_last_profile": [C.c_char_p, sz],
+    }
+    for name, args in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = C.c_void_p
+    L.r0hip_free_error.argtypes = [C.c_void_p]
+    L.r0hip_free_error.restype = None
+
+
+def check(err):
+    if err:
+        msg = C.cast(err, C.c_char_p).value.decode()
+        lib().r0hip_free_error(err)
+        raise R0HipError(msg)
+
+
+def exported_symbols():
+    """Every r0hip_* entry point declared in include/r0hip.h."""
+    hdr = os.path.join(os.path.dirname(_HERE), "include", "r0hip.h")
+    import re
+    return sorted(set(re.findall(r"\b(r0hip_\w+)\s*\(", open(hdr).read())))
+
+
+def _h(a):
+    a = np.ascontiguousarray(a, dtype=np.uint32)
+    return a, a.ctypes.data_as(u32p)
+
+
+class Buffer:
+    """A device allocation of `size` elements of `words` u32 each (hal/mod.rs:39-53)."""
+
+    def __init__(self, hal, name, size, words=1, ptr=None, owner=True):
+        self.hal, self.name, self.size, self.words = hal, name, size, words
+        self._owner = owner
+        if ptr is None:
+            p = C.c_void_p()
+            check(lib().r0hip_alloc(C.byref(p), max(1, size * words) * 4))
+            ptr = p.value
+        self.ptr = ptr
+
+    @property
+    def nwords(self):
+        return self.size * self.words
+
+    def slice(self, offset, size):
+        return Buffer(self.hal, self.name, size, self.words, self.ptr + offset * self.words * 4, owner=False)
+
+    def to_numpy(self):
+        out = np.empty(self.nwords, dtype=np.uint32)
+        if self.nwords:
+            check(lib().r0hip_memcpy_d2h(out.ctypes.data, self.ptr, self.nwords * 4))
+        return out
+
+    def copy_from(self, arr):
+        a = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1)
+        assert a.size == self.nwords, (a.size, self.nwords)
+        if a.size:
+            check(lib().r0hip_memcpy_h2d(self.ptr, a.ctypes.data, a.size * 4))
+
+    def free(self):
+        if self._owner and self.ptr:
+            check(lib().r0hip_free(self.ptr))
+        self.ptr = 0
+
+    def __del__(self):
+        try:
+            if self._owner and self.ptr and _lib is not None:
+                _lib.r0hip_free(self.ptr)
+        except Exception:
+            pass
+
+
+def _lg(n):
+    l = int(n).bit_length() - 1
+    assert 1 << l == n, f"{n} is not a power of two"
+    return l
+
+
+class HipHal:
+    """risc0_zkp::hal::Hal on MI355X (one instance per process/device)."""
+
+    EXT_SIZE = 4
+    CHECK_SIZE = 16
+
+    def __init__(self, hashfn="poseidon2", device=0):
+        self.suite = SUITES[hashfn] if isinstance(hashfn, str) else int(hashfn)
+        check(lib().r0hip_init(device))
+
+    # ---- allocation (hal/mod.rs:67-100) ----
+    def alloc_elem(self, name, size):
+        return Buffer(self, name, size, 1)
+
+    def alloc_extelem(self, name, size):
+        return Buffer(self, name, size, 4)
+
+    def alloc_digest(self, name, size):
+        return Buffer(self, name, size, 8)
+
+    def alloc_u32(self, name, size):
+        return Buffer(self, name, size, 1)
+
+    def alloc_elem_init(self, name, size, value):
+        b = self.alloc_elem(name, size)
+        check(lib().r0hip_memset32(b.ptr, value, size))
+        return b
+
+    def alloc_extelem_zeroed(self, name, size):
+        b = self.alloc_extelem(name, size)
+        check(lib().r0hip_memset32(b.ptr, 0, size * 4))
+        return b
+
+    def copy_from_elem(self, name, arr):
+        a = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1)
+        b = self.alloc_elem(name, a.size)
+        b.copy_from(a)
+        return b
+
+    copy_from_u32 = copy_from_elem
+
+    def copy_from_extelem(self, name, arr):
+        a = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1)
+        b = self.alloc_extelem(name, a.size // 4)
+        b.copy_from(a)
+        return b
+
+    def copy_from_digest(self, name, arr):
+        a = np.ascontiguousarray(arr, dtype=np.uint32).reshape(-1)
+        b = self.alloc_digest(name, a.size // 8)
+        b.copy_from(a)
+        return b
+
+    def has_unified_memory(self):
+        return False
+
+    # ---- HAL ops ----
+    def batch_expand_into_evaluate_ntt(self, output, input, count, expand_bits):
+        out_size = output.size // count
+        check(lib().r0hip_batch_expand_into_evaluate_ntt(output.ptr, input.ptr, count, _lg(out_size), expand_bits))
+
+    def batch_interpolate_ntt(self, io, count):
+        check(lib().r0hip_batch_interpolate_ntt(io.ptr, count, _lg(io.size // count)))
+
+    def batch_bit_reverse(self, io, count):
+        check(lib().r0hip_batch_bit_reverse(io.ptr, count, _lg(io.size // count)))
+
+    def zk_shift(self, io, count):
+        check(lib().r0hip_zk_shift(io.ptr, count, _lg(io.size // count)))
+
+    def batch_evaluate_any(self, coeffs, poly_count, which, xs, out):
+        check(lib().r0hip_batch_evaluate_any(out.ptr, coeffs.ptr, poly_count, _lg(coeffs.size // poly_count),
+                                             which.ptr, xs.ptr, which.size))
+
+    def mix_poly_coeffs(self, out, mix_start, mix, input, combos, input_size, count):
+        cb, cp = _h(combos)
+        ms, msp = _h(mix_start)
+        mx, mxp = _h(mix)
+        check(lib().r0hip_mix_poly_coeffs(out.ptr, input.ptr, cp, msp, mxp, input_size, count))
+
+    def eltwise_add_elem(self, output, input1, input2):
+        assert output.size == input1.size == input2.size
+        check(lib().r0hip_eltwise_add_elem(output.ptr, input1.ptr, input2.ptr, output.size))
+
+    def eltwise_sum_extelem(self, output, input):
+        count = output.size // 4
+        check(lib().r0hip_eltwise_sum_extelem(output.ptr, input.ptr, input.size // count, count))
+
+    def eltwise_copy_elem(self, output, input):
+        assert output.size == input.size
+        check(lib().r0hip_eltwise_copy_elem(output.ptr, input.ptr, output.size))
+
+    def eltwise_copy_elem_slice(self, into, frm, from_rows, from_cols, from_offset, from_stride, into_offset,
+                                into_stride):
+        src = self.copy_from_elem("from", frm)
+        check(lib().r0hip_eltwise_copy_elem_slice(into.ptr, src.ptr, from_rows, from_cols, from_offset, from_stride,
+                                                  into_offset, into_stride))
+
+    def eltwise_zeroize_elem(self, elems):
+        check(lib().r0hip_eltwise_zeroize_elem(elems.ptr, elems.size))
+
+    def fri_fold(self, output, input, mix):
+        m, mp = _h(mix)
+        check(lib().r0hip_fri_fold(output.ptr, input.ptr, mp, output.size // 4))
+
+    def hash_rows(self, output, matrix):
+        rows = output.size
+        check(lib().r0hip_hash_rows(self.suite, output.ptr, matrix.ptr, rows, matrix.size // rows))
+
+    def hash_fold(self, io, input_size, output_size):
+        check(lib().r0hip_hash_fold(self.suite, io.ptr, input_size, output_size))
+
+    def gather_sample(self, dst, src, idx, size, stride):
+        check(lib().r0hip_gather_sample(dst.ptr, src.ptr, idx, size, stride))
+
+    def scatter(self, into, index, offsets, values):
+        index = np.asarray(index, dtype=np.uint32)
+        if index.size == 0:
+            return
+        di, dof, dv = (self.copy_from_u32("index", index), self.copy_from_u32("offsets", offsets),
+                       self.copy_from_elem("values", values))
+        check(lib().r0hip_scatter(into.ptr, di.ptr, dof.ptr, dv.ptr, index.size - 1))
+
+    def prefix_products(self, io):
+        check(lib().r0hip_prefix_products(io.ptr, io.size))
+
+    def combos_prepare(self, combos, coeff_u, combo_count, cycles, reg_sizes, reg_combo_ids, mix):
+        u, up = _h(coeff_u)
+        rs, rsp = _h(reg_sizes)
+        rc, rcp = _h(reg_combo_ids)
+        m, mp = _h(mix)
+        check(lib().r0hip_combos_prepare(combos.ptr, up, combo_count, cycles, rsp, rcp, rs.size, mp))
+
+    def combos_divide(self, combos, chunk_pows, chunk_begin, cycles):
+        pw, pwp = _h(chunk_pows)
+        bg, bgp = _h(chunk_begin)
+        bad = C.c_int64(0)
+        check(lib().r0hip_combos_divide(combos.ptr, bg.size - 1, pwp, bgp, cycles, C.byref(bad)))
+        return bad.value
+
+    def eval_check(self, circuit, check_buf, groups, mix, glob, poly_mix, po2):
+        arr = (C.c_void_p * len(groups))(*[g.ptr for g in groups])
+        pm, pmp = _h(poly_mix)
+        check(lib().r0hip_eval_check(circuit.encode(), check_buf.ptr, arr, mix.ptr, glob.ptr, pmp, po2))
+
+    def synchronize(self):
+        check(lib().r0hip_synchronize())
+
+
+def prove_segment(hal, circuit, po2, code, data, accum, glob, version=None, seal_cap=1 << 24):
+    """Prove one segment from device-resident witness groups; returns (seal, mix)."""
+    from json import load
+    with open(os.path.join(_HERE, "circuits", circuit + ".taps.json")) as f:
+        mix_size = load(f)["mix_size"]
+    seal = np.zeros(seal_cap, dtype=np.uint32)
+    n = C.c_size_t(0)
+    mix = np.zeros(mix_size, dtype=np.uint32)
+    check(lib().r0hip_prove_segment(circuit.encode(), hal.suite, po2, code.ptr, data.ptr, accum.ptr, glob.ptr,
+                                    int(version is not None), version or 0, seal.ctypes.data_as(u32p), seal_cap,
+                                    C.byref(n), mix.ctypes.data_as(u32p)))
+    return seal[: n.value].copy(), mix
+
+
+def last_profile():
+    buf = C.create_string_buffer(4096)
+    check(lib().r0hip_last_profile(buf, 4096))
+    out = {}
+    for kv in buf.value.decode().split(";"):
+        if "=" in kv:
+            k, v = kv.split("=")
+            out[k] = float(v)
+    return out

@@ -1,0 +1,377 @@
+#!/usr/bin/env python3
+"""Emit the gfx950 eval_check kernels for a circuit from its constraint program
+(risc0_amd/circuits/<circuit>.poly.ir, see tools/gen_poly_ir.py).
+
+  check[k*D + cycle] = (poly_fp(cycle) * inv((3*w_D^cycle)^N - 1))[k]
+  — risc0/circuit/rv32im/src/prove/hal/cpu.rs:145-207 (rv32im),
+    risc0/circuit/recursion-sys/kernels/cxx/ffi.cpp:220-247 (recursion).
+
+MI355X design. One lane per evaluation point, all values in VGPRs. The ~20k-op
+program is too large for one kernel (register spills, and LLVM compile time grows
+super-linearly: 2.6k ops ~ 100 s with spills, 1.4k ops ~ 3 s without), so it is
+scheduled as a short sequence of kernels, each below a cost budget:
+  1. linear split: poly_fp = sum_i expr_i * prod(factors_i); accumulate nodes
+     (ACC + T*pm[k], ACC + T*U*pm[k]) are split into their summands until every
+     term's dependency cone fits the budget or is not an accumulation;
+  2. materialisation: for terms still over budget, the largest sub-expression that
+     fits is computed by an earlier kernel and stored per point in HBM (4 B per
+     Fp, 16 B per FpExt), becoming a leaf for its consumers;
+  3. packing: items are packed into kernels in dependency order; each kernel adds
+     its terms into an FpExt accumulator; the last one applies the vanishing-
+     polynomial inverse (4 distinct values on the 4N domain, from the host) and
+     writes the 4 SoA planes.
+Trace taps are reloaded by every kernel that needs them (coalesced per column).
+Products of several poly_mix powers are folded into host-computed constants.
+
+Usage: gen_eval_check.py CIRCUIT OUTDIR [BUDGET]
+Writes OUTDIR/eval_check_<circuit>_k<i>.hip (one per kernel, compiled in parallel)
+and OUTDIR/eval_check_<circuit>.hip (launcher).
+"""
+import os
+import sys
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+P = 15 * 2**27 + 1
+
+
+def load(circuit):
+    prog = []
+    with open(os.path.join(ROOT, "risc0_amd", "circuits", circuit + ".poly.ir")) as f:
+        for line in f:
+            if line.startswith("#") or not line.strip():
+                continue
+            t = line.split()
+            prog.append((t[0],) + tuple(int(x) for x in t[1:]))
+    return prog
+
+
+def deps(ins):
+    op = ins[0]
+    if op in "+-*a":
+        return [ins[2], ins[3]]
+    if op == "b":
+        return [ins[2], ins[3], ins[4]]
+    return []
+
+
+def enc(x):
+    return (x % P) * 2**32 % P
+
+
+class Program:
+    def __init__(self, circuit):
+        self.circuit = circuit
+        self.prog = load(circuit)
+        self.byid = {ins[1]: ins for ins in self.prog if ins[0] != "r"}
+        self.order = {ins[1]: n for n, ins in enumerate(self.prog) if ins[0] != "r"}
+        self.res = [ins for ins in self.prog if ins[0] == "r"][0][1]
+        t = {}
+        for ins in self.prog:
+            op = ins[0]
+            if op in ("c", "l", "g"):
+                t[ins[1]] = "f"
+            elif op in ("e", "a", "b"):
+                t[ins[1]] = "e"
+            elif op in "+-*":
+                t[ins[1]] = "e" if "e" in (t[ins[2]], t[ins[3]]) else "f"
+        self.types = t
+        self.mat = set()
+
+    def cost(self, v):
+        ins = self.byid[v]
+        op = ins[0]
+        ty = self.types
+        if op in "clge":
+            return 0
+        if op in "+-":
+            return 4 if ty[v] == "e" else 1
+        if op == "*":
+            a, b = ty[ins[2]], ty[ins[3]]
+            return 16 if (a, b) == ("e", "e") else (4 if "e" in (a, b) else 1)
+        if op == "a":
+            return 8 if ty[ins[3]] == "f" else 20
+        return 9 if ty[ins[3]] == "f" and ty[ins[4]] == "f" else 24
+
+    def cone(self, roots):
+        seen = set()
+        rs = set(roots)
+        stack = list(roots)
+        while stack:
+            v = stack.pop()
+            if v in seen:
+                continue
+            seen.add(v)
+            if v in self.mat and v not in rs:
+                continue
+            stack.extend(deps(self.byid[v]))
+        return seen
+
+    def cone_cost(self, roots):
+        rs = set(roots)
+        return sum(self.cost(v) for v in self.cone(roots) if not (v in self.mat and v not in rs))
+
+
+def term_roots(t):
+    return [t[0]] + [x[1] for x in t[1] if x[0] == "v"]
+
+
+def schedule(pg, budget):
+    byid = pg.byid
+    # 1. linear split
+    terms = [(pg.res, [])]
+    while True:
+        best, bestc = None, -1
+        for i, t in enumerate(terms):
+            if byid[t[0]][0] in "ab":
+                c = pg.cone_cost(term_roots(t))
+                if c > bestc:
+                    best, bestc = i, c
+        if best is None or bestc <= budget:
+            break
+        e, f = terms[best]
+        ins = byid[e]
+        if ins[0] == "a":
+            new = [(ins[2], f), (ins[3], f + [("pm", ins[4])])]
+        else:
+            T, U = ins[3], ins[4]
+            if byid[U][0] in "ab" and byid[T][0] not in "ab":
+                T, U = U, T
+            new = [(ins[2], f), (T, f + [("v", U), ("pm", ins[5])])]
+        terms[best:best + 1] = new
+
+    # 2. materialise sub-expressions of over-budget items
+    def fix(roots):
+        while pg.cone_cost(roots) > budget:
+            best, bestc = None, -1
+            for v in pg.cone(roots):
+                if v in roots or v in pg.mat or byid[v][0] in "clge":
+                    continue
+                c = pg.cone_cost([v])
+                if bestc < c <= budget:
+                    best, bestc = v, c
+            if best is None:
+                raise RuntimeError("cannot materialise below budget")
+            pg.mat.add(best)
+
+    for t in terms:
+        fix(term_roots(t))
+
+    level = {}
+
+    def lev(v):
+        if v not in level:
+            level[v] = 1 + max([lev(u) for u in pg.cone([v]) if u != v and u in pg.mat] + [-1])
+        return level[v]
+
+    items = []
+    for v in pg.mat:
+        items.append((lev(v), pg.order[v], "mat", v))
+    for n, t in enumerate(terms):
+        rs = term_roots(t)
+        l = 1 + max([lev(u) for u in pg.cone(rs) if u in pg.mat and u not in rs] + [-1])
+        items.append((l, 10**9 + n, "term", t))
+    items.sort(key=lambda x: (x[0], x[1]))
+    # 3. pack in order; a kernel only reads values produced by earlier kernels
+    kernels = []
+    cur, cur_roots = [], []
+    done = set()
+    for it in items:
+        roots = [it[3]] if it[2] == "mat" else term_roots(it[3])
+        need = [u for u in pg.cone(roots) if u in pg.mat and u not in roots]
+        ok = all(u in done for u in need)
+        if cur and (not ok or pg.cone_cost(cur_roots + roots) > budget):
+            kernels.append(cur)
+            done.update(x[3] for x in cur if x[2] == "mat")
+            cur, cur_roots = [], []
+        cur.append(it)
+        cur_roots += roots
+    if cur:
+        kernels.append(cur)
+    return terms, kernels
+
+
+def emit(circuit, outdir, budget):
+    pg = Program(circuit)
+    terms, kernels = schedule(pg, budget)
+    prog, types = pg.prog, pg.types
+    nargs = 1 + max(ins[2] for ins in prog if ins[0] in ("l", "g"))
+    npm = max([ins[4] for ins in prog if ins[0] == "a"] + [ins[5] for ins in prog if ins[0] == "b"]) + 1
+    mat = sorted(pg.mat, key=lambda v: pg.order[v])
+    slot = {}
+    nf = ne = 0
+    for v in mat:
+        if types[v] == "f":
+            slot[v] = ("f", nf)
+            nf += 1
+        else:
+            slot[v] = ("e", ne)
+            ne += 1
+    combo_index = {}
+    os.makedirs(outdir, exist_ok=True)
+
+    common = [
+        '#include "bb31.h"',
+        '#include "evalcheck.h"',
+        "namespace r0 {",
+        f"namespace ec_{circuit} {{",
+        "struct Args {",
+        f"  const uint32_t* a[{nargs}];",
+        "  const uint32_t* pm;   // poly_mix powers then folded products, FpExt AoS",
+        "  uint32_t* acc;        // FpExt AoS accumulator per point",
+        "  uint32_t* check;      // 4 SoA planes",
+        "  const uint32_t* vinv; // inv((3x)^N - 1) for cycle & 3",
+        "  uint32_t* mf;         // materialised Fp values, [slot][domain]",
+        "  uint32_t* me;         // materialised FpExt values, [slot][domain] AoS",
+        "  uint32_t domain;",
+        "};",
+        f"constexpr int NPM = {npm};",
+        "__device__ __forceinline__ FpExt pmx(const uint32_t* pm, int k) {",
+        "  return FpExt{{pm[4 * k], pm[4 * k + 1], pm[4 * k + 2], pm[4 * k + 3]}};",
+        "}",
+        "__device__ __forceinline__ FpExt eadd(FpExt a, FpExt b) { return fe_add(a, b); }",
+        "__device__ __forceinline__ FpExt eadd(FpExt a, uint32_t b) { a.c[0] = fp_add(a.c[0], b); return a; }",
+        "__device__ __forceinline__ FpExt eadd(uint32_t a, FpExt b) { b.c[0] = fp_add(a, b.c[0]); return b; }",
+        "__device__ __forceinline__ FpExt esub(FpExt a, FpExt b) { return fe_sub(a, b); }",
+        "__device__ __forceinline__ FpExt esub(FpExt a, uint32_t b) { a.c[0] = fp_sub(a.c[0], b); return a; }",
+        "__device__ __forceinline__ FpExt esub(uint32_t a, FpExt b) { return fe_sub(fe_from_fp(a), b); }",
+        "__device__ __forceinline__ FpExt emul(FpExt a, FpExt b) { return fe_mul(a, b); }",
+        "__device__ __forceinline__ FpExt emul(FpExt a, uint32_t b) { return fe_mul_fp(a, b); }",
+        "__device__ __forceinline__ FpExt emul(uint32_t a, FpExt b) { return fe_mul_fp(b, a); }",
+        "__device__ __forceinline__ uint32_t emul(uint32_t a, uint32_t b) { return fp_mul(a, b); }",
+    ]
+    common_text = "\n".join(common) + "\n"
+
+    stats = []
+    for ki, items in enumerate(kernels):
+        roots = []
+        for it in items:
+            roots += [it[3]] if it[2] == "mat" else term_roots(it[3])
+        need = pg.cone(roots)
+        produced = set(it[3] for it in items if it[2] == "mat")
+        first, last = ki == 0, ki == len(kernels) - 1
+        L = []
+        w = L.append
+        w(f"// GENERATED by tools/gen_eval_check.py from risc0_amd/circuits/{circuit}.poly.ir — do not edit.")
+        w(common_text)
+        w(f"__global__ __launch_bounds__(256) void k{ki}(Args A) {{")
+        w("  const uint32_t cycle = blockIdx.x * 256u + threadIdx.x;")
+        w("  if (cycle >= A.domain) return;")
+        w("  const uint32_t mask = A.domain - 1;")
+        for ins in prog:
+            op, i = ins[0], ins[1]
+            if i not in need or op == "r":
+                continue
+            if i in pg.mat and i not in produced:
+                kind, s = slot[i]
+                if kind == "f":
+                    w(f"  const uint32_t v{i} = A.mf[uint64_t({s}u) * A.domain + cycle];")
+                else:
+                    w(f"  FpExt v{i}; {{ uint4 t = reinterpret_cast<const uint4*>(A.me)[uint64_t({s}u) * A.domain + cycle];"
+                      f" v{i} = FpExt{{{{t.x, t.y, t.z, t.w}}}}; }}")
+                continue
+            if op == "c":
+                w(f"  const uint32_t v{i} = {enc(ins[2])}u;")
+            elif op == "e":
+                w(f"  const FpExt v{i} = FpExt{{{{{', '.join(str(enc(x)) + 'u' for x in ins[2:6])}}}}};")
+            elif op == "l":
+                w(f"  const uint32_t v{i} = A.a[{ins[2]}][{ins[3]}u * A.domain + ((cycle - {4 * ins[4]}u) & mask)];")
+            elif op == "g":
+                w(f"  const uint32_t v{i} = A.a[{ins[2]}][{ins[3]}];")
+            elif op == "a":
+                w(f"  const FpExt v{i} = eadd(v{ins[2]}, emul(v{ins[3]}, pmx(A.pm, {ins[4]})));")
+            elif op == "b":
+                w(f"  const FpExt v{i} = eadd(v{ins[2]}, emul(emul(v{ins[3]}, v{ins[4]}), pmx(A.pm, {ins[5]})));")
+            else:
+                a, b = ins[2], ins[3]
+                if types[a] == "f" and types[b] == "f":
+                    fn = {"+": "fp_add", "-": "fp_sub", "*": "fp_mul"}[op]
+                    w(f"  const uint32_t v{i} = {fn}(v{a}, v{b});")
+                else:
+                    fn = {"+": "eadd", "-": "esub", "*": "emul"}[op]
+                    w(f"  const FpExt v{i} = {fn}(v{a}, v{b});")
+            if i in produced:
+                kind, s = slot[i]
+                if kind == "f":
+                    w(f"  A.mf[uint64_t({s}u) * A.domain + cycle] = v{i};")
+                else:
+                    w(f"  reinterpret_cast<uint4*>(A.me)[uint64_t({s}u) * A.domain + cycle] ="
+                      f" make_uint4(v{i}.c[0], v{i}.c[1], v{i}.c[2], v{i}.c[3]);")
+        mine = [it[3] for it in items if it[2] == "term"]
+        if mine or last:
+            w("  FpExt s = fe_zero();")
+            for e, f in mine:
+                vals = [x[1] for x in f if x[0] == "v"]
+                pms = tuple(sorted(x[1] for x in f if x[0] == "pm"))
+                expr = f"v{e}"
+                for v in vals:
+                    expr = f"emul({expr}, v{v})"
+                if len(pms) == 1:
+                    expr = f"emul({expr}, pmx(A.pm, {pms[0]}))"
+                elif len(pms) > 1:
+                    if pms not in combo_index:
+                        combo_index[pms] = len(combo_index)
+                    expr = f"emul({expr}, pmx(A.pm, NPM + {combo_index[pms]}))"
+                w(f"  s = eadd(s, {expr});")
+            w("  uint4* accp = reinterpret_cast<uint4*>(A.acc) + cycle;")
+            if not first:
+                w("  { uint4 p = *accp; s = fe_add(s, FpExt{{p.x, p.y, p.z, p.w}}); }")
+            if last:
+                w("  s = fe_mul_fp(s, A.vinv[cycle & 3]);")
+                w("  #pragma unroll")
+                w("  for (int k = 0; k < 4; k++) A.check[uint64_t(k) * A.domain + cycle] = s.c[k];")
+            else:
+                w("  *accp = make_uint4(s.c[0], s.c[1], s.c[2], s.c[3]);")
+        elif not first:
+            pass
+        if first and not mine and not last:
+            # keep the accumulator defined for later kernels
+            w("  reinterpret_cast<uint4*>(A.acc)[cycle] = make_uint4(0u, 0u, 0u, 0u);")
+        w("}")
+        w(f"void launch_k{ki}(hipStream_t s, const Args& A) {{")
+        w(f"  hipLaunchKernelGGL(k{ki}, dim3(div_up(A.domain, 256)), dim3(256), 0, s, A);")
+        w("  HIP_OK(hipGetLastError());")
+        w("}")
+        w(f"}}  // namespace ec_{circuit}")
+        w("}  // namespace r0")
+        with open(os.path.join(outdir, f"eval_check_{circuit}_k{ki}.hip"), "w") as f:
+            f.write("\n".join(L) + "\n")
+        stats.append(pg.cone_cost(roots))
+    # accumulator initialisation: kernels after the first add into acc; if the first
+    # kernel has no terms it zeroes it (above).
+    flat = []
+    for pms, j in sorted(combo_index.items(), key=lambda kv: kv[1]):
+        flat += [len(pms)] + list(pms)
+    L = []
+    w = L.append
+    w(f"// GENERATED by tools/gen_eval_check.py — {circuit}: {len(prog)} IR ops, {len(terms)} terms,")
+    w(f"// {len(kernels)} kernels, {nf} Fp + {ne} FpExt materialised values per point.")
+    w(common_text)
+    for ki in range(len(kernels)):
+        w(f"void launch_k{ki}(hipStream_t s, const Args& A);")
+    w(f"const int kPmCombos[] = {{{', '.join(str(x) for x in flat) or '0'}}};")
+    w(f"}}  // namespace ec_{circuit}")
+    w(f"void eval_check_{circuit}_info(EvalCheckInfo* info) {{")
+    w(f"  info->combos = ec_{circuit}::kPmCombos; info->ncombos = {len(combo_index)}; info->npm = ec_{circuit}::NPM;")
+    w(f"  info->nargs = {nargs}; info->mat_fp = {nf}; info->mat_ext = {ne}; info->kernels = {len(kernels)};")
+    w("}")
+    w(f"void eval_check_{circuit}(hipStream_t s, const EvalCheckArgs& e) {{")
+    w(f"  using namespace ec_{circuit};")
+    w(f"  R0_REQUIRE(e.nargs == {nargs}, \"eval_check_{circuit}: wrong argument count\");")
+    w("  Args A;")
+    w(f"  for (int i = 0; i < {nargs}; i++) A.a[i] = e.args[i];")
+    w("  A.pm = e.poly_mix; A.acc = e.acc; A.check = e.check; A.vinv = e.vinv; A.domain = e.domain;")
+    w("  A.mf = e.mat_fp; A.me = e.mat_ext;")
+    for ki in range(len(kernels)):
+        w(f"  launch_k{ki}(s, A);")
+    w("}")
+    w("}  // namespace r0")
+    with open(os.path.join(outdir, f"eval_check_{circuit}.hip"), "w") as f:
+        f.write("\n".join(L) + "\n")
+    tot = sum(stats)
+    base = pg.cone_cost([pg.res])
+    print(f"{circuit}: {len(terms)} terms, {len(kernels)} kernels, mat {nf} Fp + {ne} FpExt, "
+          f"work {tot} vs {base} ({tot / base:.2f}x), per-kernel cost {stats}")
+
+
+if __name__ == "__main__":
+    emit(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 4000)
