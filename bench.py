@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""Benchmark: RISC-V cycles proved per second at segment po2=20 (BASELINE.json metric).
+
+A step proves one rv32im segment of 2^po2 cycles on one GPU: from the witness
+groups already resident in HBM (code 1 / data 211 / accum 103 columns, synthetic,
+seeded per segment) to the seal (Vec<u32>) on the host, through the whole STARK
+prover (commit code/data/accum, eval_check, DEEP-ALI, FRI, query openings).
+Multi-GPU: one process per GPU (torch.distributed.run), whole segments sharded per
+rank, no data-path collective (gloo only for the barrier and the max-time reduce).
+
+Prints ONE JSON line (rank 0). Extra diagnostics go to stderr.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+P = 15 * 2**27 + 1
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--po2", type=int, default=20)
+    ap.add_argument("--circuit", default="rv32im")
+    ap.add_argument("--hashfn", default="poseidon2")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-po2", type=int, default=16, help="segment size of the bounded CPU baseline sample")
+    return ap.parse_args()
+
+
+def synthetic_witness(rng, circuit, po2):
+    """Uniform canonical BabyBear words, seed 0x5249534330 + segment."""
+    n = 1 << po2
+    gs = circuit["group_sizes"]
+    draw = lambda k: rng.integers(0, P, size=k, dtype=np.uint64).astype(np.uint32)
+    return draw(gs[1] * n), draw(gs[2] * n), draw(gs[0] * n), draw(circuit["output_size"])
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", init_method="env://")
+    import risc0_amd as r
+    with open(os.path.join(ROOT, "risc0_amd", "circuits", args.circuit + ".taps.json")) as f:
+        circ = json.load(f)
+    hal = r.HipHal(args.hashfn, device=local_rank)
+    version = 2 if args.circuit == "rv32im" else None
+
+    # inputs resident in HBM before the timed region: one witness set per rank
+    rng = np.random.default_rng(0x5249534330 + rank)
+    code, data, accum, glob = synthetic_witness(rng, circ, args.po2)
+    dc, dd, da, dg = (hal.copy_from_elem(k, v) for k, v in
+                      (("code", code), ("data", data), ("accum", accum), ("global", glob)))
+    del code, data, accum
+
+    def step():
+        return r.prove_segment(hal, args.circuit, args.po2, dc, dd, da, dg, version=version)
+
+    for _ in range(args.warmup):
+        step()
+    r.lib()  # noqa
+    hal.synchronize()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    phase_tot = {}
+    for _ in range(args.steps):
+        seal, _mix = step()
+        for k, v in r.last_profile().items():
+            phase_tot[k] = phase_tot.get(k, 0.0) + v
+    hal.synchronize()
+    t = time.perf_counter() - t0
+    if dist:
+        import torch
+        tt = torch.tensor([t], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t = float(tt[0])
+        dist.barrier()
+    cycles_total = world * args.steps * (1 << args.po2)
+    value = cycles_total / t
+    ms_per_step = 1000.0 * t / args.steps
+
+    # kernel-level timing of the dominant kernel + roofline (rank 0)
+    roofline = None
+    cpu = None
+    if rank == 0:
+        kt = kernel_roofline(r, hal, args, circ, dc, dd, da, dg, version)
+        roofline = kt
+        phases = {k: round(v / args.steps, 3) for k, v in phase_tot.items()}
+        print(json.dumps({"phases_ms": phases, "seal_words": int(seal.size)}), file=sys.stderr)
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(args, circ)
+
+    if rank == 0:
+        line = {
+            "metric": "RISC-V cycles proved/sec at segment po2=20",
+            "value": round(value, 1),
+            "unit": "cycles/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32 (BabyBear Montgomery, exact modular integer)",
+            "data": "synthetic (uniform BabyBear witness, seeded per segment)",
+            "config": {"workload": f"{args.circuit} segment po2={args.po2}, {args.hashfn} hashfn, "
+                                   "witness resident in HBM -> seal on host",
+                       "circuit": args.circuit, "po2": args.po2, "hashfn": args.hashfn,
+                       "segments_per_gpu": args.steps, "parallelism": f"segment-per-gpu x{world}"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+
+
+def kernel_roofline(r, hal, args, circ, dc, dd, da, dg, version):
+    """Time the dominant kernel with HIP events on the library stream (r0hip_kernel_times)."""
+    try:
+        r.set_kernel_timing(True)
+        r.prove_segment(hal, args.circuit, args.po2, dc, dd, da, dg, version=version)
+        times = r.kernel_times()
+        r.set_kernel_timing(False)
+    except AttributeError:
+        return None
+    if not times:
+        return None
+    name, (ms, calls, alg_bytes) = max(times.items(), key=lambda kv: kv[1][0])
+    print(json.dumps({"kernel_times_ms": {k: [round(v[0], 3), v[1]] for k, v in times.items()}}), file=sys.stderr)
+    avg_s = ms / 1000.0 / calls
+    per_launch = alg_bytes / calls
+    achieved = per_launch / avg_s / 1e9
+    return {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": 8000.0, "unit": "GB/s",
+            "frac": round(achieved / 8000.0, 4), "traffic": None, "alg_bytes_per_launch": int(per_launch),
+            "avg_launch_ms": round(avg_s * 1000, 4)}
+
+
+def cpu_baseline(args, circ):
+    """The CPU oracle (C++ restatement of CpuHal + Prover) on a bounded sample."""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        if oracle.ref_lib() is None:
+            return None
+        po2 = args.cpu_po2
+        rng = np.random.default_rng(0x5249534330)
+        code, data, accum, glob = synthetic_witness(rng, circ, po2)
+        suite = oracle.POSEIDON2 if args.hashfn == "poseidon2" else oracle.SHA256
+        t0 = time.perf_counter()
+        oracle.prove_segment(args.circuit, suite, po2, code, data, accum, glob,
+                             version=2 if args.circuit == "rv32im" else None)
+        t = time.perf_counter() - t0
+        return {"value": round((1 << po2) / t, 1), "unit": "cycles/s", "cores": int(oracle.num_threads()),
+                "kind": "port",
+                "sample": f"one {args.circuit} segment at po2={po2} ({args.hashfn}), {t:.1f} s; "
+                          "eval_check uses the reference's compiled C++ poly_fp"}
+    except Exception as e:  # the baseline is reported, never required
+        print(f"cpu baseline failed: {e}", file=sys.stderr)
+        return None
+
+
+if __name__ == "__main__":
+    main()

@@ -111,6 +111,10 @@ const char* r0hip_prove_segment(const char* circuit, int suite, uint32_t po2, co
                                 const uint32_t* d_data, const uint32_t* d_accum, uint32_t* d_global,
                                 int write_version, uint32_t version, uint32_t* h_seal, size_t seal_cap,
                                 size_t* seal_len, uint32_t* h_mix_out);
+/* kernel-level timing with HIP events on the library stream: enable, run, then read
+ * "name=total_ms:calls:alg_bytes;..." (alg_bytes = algorithmic HBM bytes) */
+const char* r0hip_set_kernel_timing(int on);
+const char* r0hip_kernel_times(char* buf, size_t cap);
 /* per-phase device timings (ms) of the last r0hip_prove_segment, as "name=ms;..." */
 const char* r0hip_last_profile(char* buf, size_t cap);
 

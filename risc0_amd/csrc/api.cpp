@@ -274,6 +274,20 @@ const char* r0hip_prove_segment(const char* circuit, int suite, uint32_t po2, co
   });
 }
 
+const char* r0hip_set_kernel_timing(int on) {
+  return wrap([&] { ktimer_enable(on != 0); });
+}
+
+const char* r0hip_kernel_times(char* buf, size_t cap) {
+  return wrap([&] {
+    std::string p = ktimer_report();
+    if (buf && cap) {
+      strncpy(buf, p.c_str(), cap - 1);
+      buf[cap - 1] = 0;
+    }
+  });
+}
+
 const char* r0hip_last_profile(char* buf, size_t cap) {
   return wrap([&] {
     std::string p = last_profile();

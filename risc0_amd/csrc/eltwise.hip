@@ -364,12 +364,14 @@ void eltwise_zeroize(hipStream_t s, uint32_t* io, size_t n) {
 }
 void eltwise_sum_extelem(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count, size_t to_add) {
   if (!count) return;
+  KScope ks("eltwise_sum_extelem", double(count) * 16 * (to_add + 1));
   hipLaunchKernelGGL(sum_extelem_kernel, dim3(div_up(count, kThreads)), dim3(kThreads), 0, s, out, in,
                      uint64_t(count), uint32_t(to_add));
   HIP_OK(hipGetLastError());
 }
 void fri_fold(hipStream_t s, uint32_t* out, const uint32_t* in, FpExt mix, size_t count) {
   if (!count) return;
+  KScope ks("fri_fold", double(count) * (16 * 16 + 16));
   hipLaunchKernelGGL(fri_fold_kernel, dim3(div_up(count, kThreads)), dim3(kThreads), 0, s, out, in, mix,
                      uint64_t(count));
   HIP_OK(hipGetLastError());
@@ -406,6 +408,9 @@ void mix_poly_coeffs(hipStream_t s, uint32_t* out, const uint32_t* in, const uin
                      size_t count) {
   if (!count || !input_size) return;
   uint32_t used = 0, maxc = 0;
+  for (uint32_t c : combos_host) used |= 1u << (c & 31);
+  KScope ks("mix_poly_coeffs", double(count) * (input_size * 4 + 32.0 * __builtin_popcount(used)));
+  used = 0;
   for (uint32_t c : combos_host) {
     R0_REQUIRE(c < 32, "mix_poly_coeffs: combo id too large");
     used |= 1u << c;
@@ -433,6 +438,7 @@ void batch_evaluate_any(hipStream_t s, const uint32_t* coeffs, size_t poly_count
   (void)poly_count;
   uint64_t n = uint64_t(1) << log_n;
   uint32_t nchunks = uint32_t((n + kEvChunk - 1) / kEvChunk);
+  KScope ks("batch_evaluate_any", double(std::min<size_t>(poly_count, eval_count)) * n * 4);
   R0_REQUIRE(n % kEvPer == 0, "batch_evaluate_any: poly size must be a multiple of 16");
   R0_REQUIRE(eval_count < 65536, "batch_evaluate_any: too many evaluations");
   uint32_t* partial = static_cast<uint32_t*>(scratch(size_t(eval_count) * nchunks * 16, 2));
@@ -450,6 +456,9 @@ void poly_divide_rows(hipStream_t s, uint32_t* io, size_t n, const std::vector<s
   size_t maxz = 0;
   for (auto& v : zs) maxz = std::max(maxz, v.size());
   if (!rows || !maxz || !n) return;
+  size_t ndiv = 0;
+  for (auto& v : zs) ndiv += v.size();
+  KScope ks("poly_divide", double(ndiv) * n * 32);
   // round k divides every row that has a k-th z (the rows' z lists run in order)
   for (size_t k = 0; k < maxz; k++) {
     std::vector<DivRow> rs;

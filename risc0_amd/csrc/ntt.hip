@@ -302,6 +302,7 @@ void fill_pass(PassArgs& p, bool inv, uint32_t L, uint32_t a, uint32_t b, size_t
 void ntt_evaluate(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count, uint32_t L,
                   uint32_t eb) {
   if (count == 0) return;
+  KScope ks("ntt_evaluate", double(count) * 4 * ((size_t(1) << L) + (size_t(1) << (L - eb))));
   R0_REQUIRE(in != out || eb == 0, "expand_into_evaluate needs distinct buffers");
   if (L == 0) {
     HIP_OK(hipMemcpyAsync(out, in, count * 4, hipMemcpyDeviceToDevice, s));
@@ -322,6 +323,7 @@ void ntt_evaluate(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count
 
 void ntt_interpolate(hipStream_t s, uint32_t* io, size_t count, uint32_t L, bool zk) {
   if (count == 0 || L == 0) return;  // size-1 transform (and 3^0 shift) is the identity
+  KScope ks("ntt_interpolate", double(count) * 8 * (size_t(1) << L));
   auto pl = plan(L);
   for (size_t i = pl.size(); i-- > 0;) {
     PassArgs p{};
@@ -358,6 +360,7 @@ void ntt_interpolate(hipStream_t s, uint32_t* io, size_t count, uint32_t L, bool
 
 void bit_reverse(hipStream_t s, uint32_t* io, size_t count, uint32_t L) {
   if (count == 0 || L < 2) return;
+  KScope ks("bit_reverse", double(count) * 8 * (size_t(1) << L));
   uint32_t k = L / 2 < 5 ? L / 2 : 5;
   uint64_t nwg = uint64_t(count) << (L - 2 * k);
   R0_REQUIRE(nwg < (1ull << 31), "bit_reverse grid too large");
@@ -368,6 +371,7 @@ void bit_reverse(hipStream_t s, uint32_t* io, size_t count, uint32_t L) {
 void zk_shift(hipStream_t s, uint32_t* io, size_t count, uint32_t L) {
   uint64_t n = uint64_t(count) << L;
   if (n == 0) return;
+  KScope ks("zk_shift", double(n) * 8);
   uint32_t h = L / 2;
   const uint32_t* A = dev_table("zkA" + std::to_string(L), [=] {
     std::vector<uint32_t> t(size_t(1) << h);

@@ -227,6 +227,9 @@ void run_eval_check(const CircuitDef& c, uint32_t* check, const uint32_t* const*
   e.mat_ext = static_cast<uint32_t*>(scratch(size_t(info.mat_ext) * domain * 16 + 16, 24));
   e.check = check;
   e.domain = uint32_t(domain);
+  double bytes = 16.0 * domain;
+  for (int g = 0; g < 3; g++) bytes += 4.0 * domain * c.group_sizes[g];
+  KScope ks("eval_check", bytes);
   c.eval_check(s, e);
 }
 

@@ -4,7 +4,9 @@
 
 #include <algorithm>
 #include <cstring>
+#include <cstdio>
 #include <map>
+#include <tuple>
 #include <mutex>
 #include <unordered_map>
 
@@ -127,6 +129,68 @@ void stage_reset() {
   for (auto* p : g_stage_old) (void)hipHostFree(p);
   g_stage_old.clear();
   g_stage.used = 0;
+}
+
+// ---- kernel timing -----------------------------------------------------------
+namespace {
+struct KRec {
+  std::string name;
+  double bytes;
+  hipEvent_t a, b;
+};
+bool g_kt_on = false;
+std::vector<KRec> g_kt;
+}  // namespace
+
+void ktimer_enable(bool on) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_kt_on = on;
+}
+
+KScope::KScope(const char* name, double bytes) {
+  if (!g_kt_on) return;
+  KRec r{name, bytes, nullptr, nullptr};
+  HIP_OK(hipEventCreate(&r.a));
+  HIP_OK(hipEventCreate(&r.b));
+  HIP_OK(hipEventRecord(r.a, stream()));
+  std::lock_guard<std::mutex> lk(g_mu);
+  idx = int(g_kt.size());
+  g_kt.push_back(r);
+}
+
+KScope::~KScope() {
+  if (idx < 0) return;
+  hipEvent_t b;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    b = g_kt[idx].b;
+  }
+  (void)hipEventRecord(b, stream());
+}
+
+std::string ktimer_report() {
+  HIP_OK(hipStreamSynchronize(stream()));
+  std::lock_guard<std::mutex> lk(g_mu);
+  std::map<std::string, std::tuple<double, int, double>> agg;
+  for (auto& r : g_kt) {
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, r.a, r.b));
+    auto& t = agg[r.name];
+    std::get<0>(t) += ms;
+    std::get<1>(t) += 1;
+    std::get<2>(t) += r.bytes;
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  g_kt.clear();
+  std::string out;
+  for (auto& kv : agg) {
+    char buf[256];
+    snprintf(buf, sizeof(buf), "%s=%.6f:%d:%.0f;", kv.first.c_str(), std::get<0>(kv.second), std::get<1>(kv.second),
+             std::get<2>(kv.second));
+    out += buf;
+  }
+  return out;
 }
 
 // ---- pooled device buffers ---------------------------------------------------

@@ -45,6 +45,16 @@ void* scratch(size_t bytes, int slot = 0);
 void upload_async(void* d_dst, const void* h_src, size_t bytes);
 void stage_reset();
 
+// Optional kernel-level timing (HIP events on the library stream around each
+// launcher), with the launcher's algorithmic HBM bytes for roofline reporting.
+struct KScope {
+  KScope(const char* name, double alg_bytes);
+  ~KScope();
+  int idx = -1;
+};
+void ktimer_enable(bool on);
+std::string ktimer_report();  // "name=total_ms:calls:alg_bytes;..." (synchronises)
+
 inline unsigned div_up(size_t a, size_t b) { return unsigned((a + b - 1) / b); }
 
 // ---- launchers (all asynchronous on `s`) -----------------------------------

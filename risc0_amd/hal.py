@@ -77,6 +77,8 @@ def _declare(L):
         "r0hip_prove_segment": [C.c_char_p, C.c_int, C.c_uint32, vp, vp, vp, vp, C.c_int, C.c_uint32, u32p, sz,
                                 C.POINTER(sz), u32p],
         "r0hip_last_profile": [C.c_char_p, sz],
+        "r0hip_set_kernel_timing": [C.c_int],
+        "r0hip_kernel_times": [C.c_char_p, sz],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -326,4 +328,21 @@ def last_profile():
         if "=" in kv:
             k, v = kv.split("=")
             out[k] = float(v)
+    return out
+
+
+def set_kernel_timing(on):
+    check(lib().r0hip_set_kernel_timing(int(bool(on))))
+
+
+def kernel_times():
+    """{kernel: (total_ms, calls, algorithmic_bytes)} since timing was enabled."""
+    buf = C.create_string_buffer(16384)
+    check(lib().r0hip_kernel_times(buf, 16384))
+    out = {}
+    for kv in buf.value.decode().split(";"):
+        if "=" in kv:
+            k, v = kv.split("=")
+            ms, calls, b = v.split(":")
+            out[k] = (float(ms), int(calls), float(b))
     return out
