@@ -15,7 +15,7 @@
 // each pass is a local size-2^b DIT after one twiddle multiply per element (and
 // the transpose of that for the inverse). Pass 0 (a = 0) reads contiguous rows;
 // upper passes read 2^c adjacent columns per workgroup so every global access is
-// a >=64-byte contiguous run. A po2=20 evaluate (L = 22) is two passes: one read
+// a >=64-byte contiguous run. A po2=20 evaluate (L = 22) is two passes (13 + 9 bits): one read
 // of the coefficients and one read+write of the 4x domain through HBM.
 #include "runtime.h"
 
@@ -41,12 +41,110 @@ struct PassArgs {
   uint32_t sc_split;
 };
 
-__device__ __forceinline__ uint64_t elem_index(const PassArgs& p, uint64_t g_hi, uint32_t low, uint32_t t) {
-  // g_hi: index over (poly, hi) for a > 0; element = g_hi*2^(a+b) + t*2^a + low
-  return (g_hi << (p.a + p.b)) + (uint64_t(t) << p.a) + low;
+// LDS placement. Row passes (a == 0) keep each row contiguous with one pad word
+// per 8 so strided butterfly reads spread over the banks; column passes store
+// [t][j] with the 2^c (= 32) adjacent columns of a row in consecutive words.
+template <bool COLS>
+__device__ __forceinline__ uint32_t lidx(uint32_t j, uint32_t t, uint32_t b, uint32_t c) {
+  if (COLS) return (t << c) + j;
+  return j * ((1u << b) + (1u << b >> 3)) + t + (t >> 3);
 }
 
-template <bool INV, bool EXPAND, bool LAST>
+// One stage group of 1..3 radix-2 stages [s0, s0+NST) done in registers: each lane
+// owns blocks of 2^NST elements t_base + m*h (h = 2^(s0-1)), so the group costs one
+// LDS read and one write per element instead of NST.
+template <bool INV, bool COLS, int NST>
+__device__ __forceinline__ void stage_group(uint32_t* lds, const uint32_t* __restrict__ tw, uint32_t s0,
+                                            uint32_t b, uint32_t c) {
+  constexpr uint32_t M = 1u << NST;
+  const uint32_t h = 1u << (s0 - 1);
+  const uint32_t nrb = 1u << (b - NST);  // blocks per column/row
+  const uint32_t nblk = nrb << c;
+  for (uint32_t blk = threadIdx.x; blk < nblk; blk += kThreads) {
+    uint32_t j, r;
+    if (COLS) {
+      j = blk & ((1u << c) - 1);
+      r = blk >> c;
+    } else {
+      j = blk / nrb;
+      r = blk & (nrb - 1);
+    }
+    const uint32_t k = r & (h - 1);
+    const uint32_t tb = ((r >> (s0 - 1)) << (s0 - 1 + NST)) | k;
+    uint32_t v[M];
+#pragma unroll
+    for (uint32_t m = 0; m < M; m++) v[m] = lds[lidx<COLS>(j, tb + m * h, b, c)];
+    if (!INV) {
+#pragma unroll
+      for (uint32_t st = 0; st < NST; st++) {
+        const uint32_t half = 1u << st, hs = h << st;
+#pragma unroll
+        for (uint32_t m = 0; m < M; m++) {
+          if (m & half) continue;
+          uint32_t w = tw[hs + k + (m & (half - 1)) * h];
+          uint32_t x = v[m], y = fp_mul(v[m + half], w);
+          v[m] = fp_add(x, y);
+          v[m + half] = fp_sub(x, y);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int st = NST - 1; st >= 0; st--) {
+        const uint32_t half = 1u << st, hs = h << st;
+#pragma unroll
+        for (uint32_t m = 0; m < M; m++) {
+          if (m & half) continue;
+          uint32_t w = tw[hs + k + (m & (half - 1)) * h];
+          uint32_t x = v[m], y = v[m + half];
+          v[m] = fp_add(x, y);
+          v[m + half] = fp_mul(fp_sub(x, y), w);
+        }
+      }
+    }
+#pragma unroll
+    for (uint32_t m = 0; m < M; m++) lds[lidx<COLS>(j, tb + m * h, b, c)] = v[m];
+  }
+  __syncthreads();
+}
+
+template <bool INV, bool COLS>
+__device__ __forceinline__ void stages(uint32_t* lds, const uint32_t* __restrict__ tw, uint32_t first,
+                                       uint32_t last, uint32_t b, uint32_t c) {
+  // stages [first, last] inclusive, ascending for DIT, descending for DIF
+  if (!INV) {
+    uint32_t s = first;
+    while (s <= last) {
+      uint32_t n = last - s + 1;
+      if (n >= 3) {
+        stage_group<INV, COLS, 3>(lds, tw, s, b, c);
+        s += 3;
+      } else if (n == 2) {
+        stage_group<INV, COLS, 2>(lds, tw, s, b, c);
+        s += 2;
+      } else {
+        stage_group<INV, COLS, 1>(lds, tw, s, b, c);
+        s += 1;
+      }
+    }
+  } else {
+    int s = int(last);
+    while (s >= int(first)) {
+      int n = s - int(first) + 1;
+      if (n >= 3) {
+        stage_group<INV, COLS, 3>(lds, tw, uint32_t(s - 2), b, c);
+        s -= 3;
+      } else if (n == 2) {
+        stage_group<INV, COLS, 2>(lds, tw, uint32_t(s - 1), b, c);
+        s -= 2;
+      } else {
+        stage_group<INV, COLS, 1>(lds, tw, uint32_t(s), b, c);
+        s -= 1;
+      }
+    }
+  }
+}
+
+template <bool INV, bool EXPAND, bool LAST, bool COLS>
 __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t tid = threadIdx.x;
@@ -54,23 +152,20 @@ __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
   const uint32_t C = 1u << p.c;
   const uint32_t total = nb << p.c;
   const uint32_t bmask = nb - 1;
-
-  // Workgroup -> (g_hi, low0) for a > 0, or first row group for a == 0.
-  uint64_t wg = blockIdx.x;
+  const uint64_t wg = blockIdx.x;
   uint64_t g_hi = 0;
   uint32_t low0 = 0;
-  if (p.a > 0) {
+  if (COLS) {
     uint32_t lowblocks = 1u << (p.a - p.c);
     low0 = uint32_t(wg % lowblocks) << p.c;
     g_hi = wg / lowblocks;
   }
-
-  // ---- load (with forward twiddle pre-scale) --------------------------------
+  // ---- load (forward column passes pre-scale by w_{2^(a+b)}^{low * rev_b(t)}) ----
   for (uint32_t idx = tid; idx < total; idx += kThreads) {
     uint32_t t, j;
     uint64_t e;
     bool ok = true;
-    if (p.a == 0) {
+    if (!COLS) {
       t = idx & bmask;
       j = idx >> p.b;
       uint64_t g = (wg << p.c) + j;
@@ -79,75 +174,39 @@ __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
     } else {
       j = idx & (C - 1);
       t = idx >> p.c;
-      e = elem_index(p, g_hi, low0 + j, t);
+      e = (g_hi << (p.a + p.b)) + (uint64_t(t) << p.a) + low0 + j;
     }
     uint32_t v = 0;
     if (ok) {
       if (EXPAND) v = p.in[e >> p.eb];
       else v = p.out[e];
-      if (!INV && p.a > 0) {
+      if (!INV && COLS) {
         uint32_t ex = (low0 + j) * bitrev_n(t, p.b);
         v = fp_mul(v, fp_mul(p.sc_hi[ex >> p.sc_split], p.sc_lo[ex & ((1u << p.sc_split) - 1)]));
       }
     }
-    lds[(j << p.b) + t] = v;
+    lds[lidx<COLS>(j, t, p.b, p.c)] = v;
   }
   __syncthreads();
-
-  // ---- butterflies -----------------------------------------------------------
-  const uint32_t nbf = total >> 1;  // butterflies per stage
-  const uint32_t hb = p.b - 1;
-  if (!INV) {
-    for (uint32_t s = 1 + (EXPAND ? p.eb : 0); s <= p.b; s++) {
-      const uint32_t h = 1u << (s - 1);
-      for (uint32_t q = tid; q < nbf; q += kThreads) {
-        uint32_t j = q >> hb, r = q & ((1u << hb) - 1);
-        uint32_t k = r & (h - 1);
-        uint32_t t0 = ((r >> (s - 1)) << s) | k;
-        uint32_t* base = lds + (j << p.b);
-        uint32_t u = base[t0];
-        uint32_t v = fp_mul(base[t0 + h], p.local_tw[h + k]);
-        base[t0] = fp_add(u, v);
-        base[t0 + h] = fp_sub(u, v);
-      }
-      __syncthreads();
-    }
-  } else {
-    for (uint32_t s = p.b; s >= 1; s--) {
-      const uint32_t h = 1u << (s - 1);
-      for (uint32_t q = tid; q < nbf; q += kThreads) {
-        uint32_t j = q >> hb, r = q & ((1u << hb) - 1);
-        uint32_t k = r & (h - 1);
-        uint32_t t0 = ((r >> (s - 1)) << s) | k;
-        uint32_t* base = lds + (j << p.b);
-        uint32_t u = base[t0];
-        uint32_t v = base[t0 + h];
-        base[t0] = fp_add(u, v);
-        base[t0 + h] = fp_mul(fp_sub(u, v), p.local_tw[h + k]);
-      }
-      __syncthreads();
-    }
-  }
-
-  // ---- store (with inverse twiddle post-scale / normalisation) --------------
+  if (!INV) stages<false, COLS>(lds, p.local_tw, 1 + (EXPAND ? p.eb : 0), p.b, p.b, p.c);
+  else stages<true, COLS>(lds, p.local_tw, 1, p.b, p.b, p.c);
+  // ---- store (inverse column passes post-scale; last inverse pass normalises) ----
   for (uint32_t idx = tid; idx < total; idx += kThreads) {
     uint32_t t, j;
     uint64_t e;
-    bool ok = true;
-    if (p.a == 0) {
+    if (!COLS) {
       t = idx & bmask;
       j = idx >> p.b;
       uint64_t g = (wg << p.c) + j;
-      ok = g < p.groups;
+      if (g >= p.groups) continue;
       e = (g << p.b) + t;
     } else {
       j = idx & (C - 1);
       t = idx >> p.c;
-      e = elem_index(p, g_hi, low0 + j, t);
+      e = (g_hi << (p.a + p.b)) + (uint64_t(t) << p.a) + low0 + j;
     }
-    if (!ok) continue;
-    uint32_t v = lds[(j << p.b) + t];
-    if (INV && p.a > 0) {
+    uint32_t v = lds[lidx<COLS>(j, t, p.b, p.c)];
+    if (INV && COLS) {
       uint32_t ex = (low0 + j) * bitrev_n(t, p.b);
       v = fp_mul(v, fp_mul(p.sc_hi[ex >> p.sc_split], p.sc_lo[ex & ((1u << p.sc_split) - 1)]));
     }
@@ -248,15 +307,16 @@ void scale_tables(bool inv, uint32_t m, const uint32_t** lo, const uint32_t** hi
   });
 }
 
-// Pass plan over index bits: first pass (a = 0) takes up to 12 bits; the rest are
-// split evenly into passes of at most 10 bits.
+// Pass plan over index bits: the row pass (a = 0) takes up to 13 bits (32 KiB rows
+// in LDS); the remaining bits go to column passes of at most 9 bits over 32
+// adjacent columns (128-byte global segments, 64 KiB of LDS per workgroup).
 std::vector<std::pair<uint32_t, uint32_t>> plan(uint32_t L) {
   std::vector<std::pair<uint32_t, uint32_t>> v;
-  uint32_t first = L < 12 ? L : 12;
+  uint32_t first = L < 13 ? L : 13;
   v.push_back({0, first});
   uint32_t rest = L - first;
   if (rest) {
-    uint32_t np = (rest + 9) / 10;
+    uint32_t np = (rest + 8) / 9;
     uint32_t a = first;
     for (uint32_t i = 0; i < np; i++) {
       uint32_t b = rest / np + (i < rest % np ? 1 : 0);
@@ -267,15 +327,14 @@ std::vector<std::pair<uint32_t, uint32_t>> plan(uint32_t L) {
   return v;
 }
 
-template <bool INV, bool EXPAND, bool LAST>
+template <bool INV, bool EXPAND, bool LAST, bool COLS>
 void launch_pass(hipStream_t s, PassArgs p) {
-  uint32_t nb = p.b;
-  size_t lds = size_t(4) << (nb + p.c);
+  size_t lds = COLS ? (size_t(4) << (p.b + p.c)) : size_t(4) * ((size_t(1) << p.b) + (size_t(1) << p.b >> 3)) << p.c;
   uint64_t nwg;
-  if (p.a == 0) nwg = (p.groups + (uint64_t(1) << p.c) - 1) >> p.c;
-  else nwg = p.groups >> p.c;  // groups = count * 2^(L-b) ; each wg 2^c adjacent lows
+  if (!COLS) nwg = (p.groups + (uint64_t(1) << p.c) - 1) >> p.c;
+  else nwg = p.groups >> p.c;  // groups = count * 2^(L-b); each wg takes 2^c adjacent columns
   R0_REQUIRE(nwg < (1ull << 31), "ntt grid too large");
-  hipLaunchKernelGGL((ntt_pass_kernel<INV, EXPAND, LAST>), dim3(unsigned(nwg)), dim3(kThreads), lds, s, p);
+  hipLaunchKernelGGL((ntt_pass_kernel<INV, EXPAND, LAST, COLS>), dim3(unsigned(nwg)), dim3(kThreads), lds, s, p);
   HIP_OK(hipGetLastError());
 }
 
@@ -285,11 +344,10 @@ void fill_pass(PassArgs& p, bool inv, uint32_t L, uint32_t a, uint32_t b, size_t
   p.b = b;
   p.groups = uint64_t(count) << (L - b);
   if (a == 0) {
-    // rows per workgroup so a workgroup holds >= 1024 elements (<= 4096)
-    uint32_t c = b >= 10 ? 0 : 10 - b;
-    p.c = c;
+    // rows per workgroup so a workgroup holds >= 2048 elements
+    p.c = b >= 11 ? 0 : 11 - b;
   } else {
-    p.c = a < 4 ? a : 4;
+    p.c = a < 5 ? a : 5;
   }
   p.local_tw = local_tw_table(inv, b);
   p.sc_lo = p.sc_hi = nullptr;
@@ -316,8 +374,8 @@ void ntt_evaluate(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count
     p.in = in;
     p.eb = eb;
     fill_pass(p, false, L, pl[i].first, pl[i].second, count);
-    if (i == 0) launch_pass<false, true, false>(s, p);
-    else launch_pass<false, false, false>(s, p);
+    if (i == 0) launch_pass<false, true, false, false>(s, p);
+    else launch_pass<false, false, false, true>(s, p);
   }
 }
 
@@ -351,9 +409,9 @@ void ntt_interpolate(hipStream_t s, uint32_t* io, size_t count, uint32_t L, bool
           return t;
         });
       }
-      launch_pass<true, false, true>(s, p);
+      launch_pass<true, false, true, false>(s, p);
     } else {
-      launch_pass<true, false, false>(s, p);
+      launch_pass<true, false, false, true>(s, p);
     }
   }
 }

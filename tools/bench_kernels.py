@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Micro-benchmarks of individual HAL ops at prover shapes (po2=20 rv32im data group),
+timed with the library's HIP-event kernel timer. Run under rocprofv3 for per-kernel splits."""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import risc0_amd as r  # noqa: E402
+
+P = 15 * 2**27 + 1
+
+
+def main():
+    which = sys.argv[1:] or ["ntt", "hash"]
+    hal = r.HipHal("poseidon2")
+    rng = np.random.default_rng(1)
+    cols, po2 = 211, 20
+    n = 1 << po2
+    inp = hal.copy_from_elem("in", rng.integers(0, P, cols * n, dtype=np.uint64).astype(np.uint32))
+    out = hal.alloc_elem("out", cols * 4 * n)
+    reps = 5
+    r.set_kernel_timing(True)
+    for _ in range(reps):
+        if "ntt" in which:
+            hal.batch_expand_into_evaluate_ntt(out, inp, cols, 2)
+            hal.batch_interpolate_ntt(inp, cols)
+        if "hash" in which:
+            d = hal.alloc_digest("d", 4 * n)
+            hal.hash_rows(d, out)
+    hal.synchronize()
+    for k, (ms, calls, b) in sorted(r.kernel_times().items()):
+        print(f"{k:28s} {ms / calls:9.3f} ms/launch  {b / calls / 1e9:7.3f} GB alg  {b / (ms / 1e3) / 1e9:8.1f} GB/s")
+
+
+if __name__ == "__main__":
+    main()
