@@ -44,6 +44,11 @@ R0_HD uint32_t mont_reduce(uint64_t t) {
 }
 R0_HD uint32_t fp_mul(uint32_t a, uint32_t b) { return mont_reduce(uint64_t(a) * b); }
 
+// Congruent fold of any 64-bit value below 2^60 + 2^32: hi * (2^32 mod p) + lo —
+// one v_mad_u64_u32; lets sums of several Montgomery products stay unreduced.
+constexpr uint32_t kFoldC = uint32_t((uint64_t(1) << 32) % kP);  // 268435454
+R0_HD uint64_t fold64(uint64_t x) { return uint64_t(uint32_t(x >> 32)) * kFoldC + uint32_t(x); }
+
 constexpr uint32_t mont_mul_c(uint32_t a, uint32_t b) {
   // constexpr twin of fp_mul for compile-time constants
   return (uint32_t((uint64_t(a) * b + uint64_t(uint32_t(uint64_t(a) * b) * kNegPinv) * kP) >> 32) >= kP)
@@ -86,19 +91,17 @@ R0_HD FpExt fe_mul_fp(FpExt a, uint32_t b) {
 }
 
 R0_HD FpExt fe_mul(FpExt a, FpExt b) {
-  // Extension multiply (equal to baby_bear.rs:744-757) with lazy reduction: two
-  // 62-bit products summed stay below p*2^32 (2p^2 < p*2^32), so each pair needs a
-  // single REDC. Results are canonical, hence bit-identical to the reference.
-  uint32_t r0 = fp_add(fp_mul(a.c[0], b.c[0]),
-                       fp_mul(kNBeta, fp_add(mont_reduce(uint64_t(a.c[1]) * b.c[3] + uint64_t(a.c[2]) * b.c[2]),
-                                             fp_mul(a.c[3], b.c[1]))));
-  uint32_t r1 = fp_add(mont_reduce(uint64_t(a.c[0]) * b.c[1] + uint64_t(a.c[1]) * b.c[0]),
-                       fp_mul(kNBeta, mont_reduce(uint64_t(a.c[2]) * b.c[3] + uint64_t(a.c[3]) * b.c[2])));
-  uint32_t r2 = fp_add(mont_reduce(uint64_t(a.c[0]) * b.c[2] + uint64_t(a.c[1]) * b.c[1]),
-                       fp_add(fp_mul(a.c[2], b.c[0]), fp_mul(kNBeta, fp_mul(a.c[3], b.c[3]))));
-  uint32_t r3 = fp_add(mont_reduce(uint64_t(a.c[0]) * b.c[3] + uint64_t(a.c[1]) * b.c[2]),
-                       mont_reduce(uint64_t(a.c[2]) * b.c[1] + uint64_t(a.c[3]) * b.c[0]));
-  return FpExt{{r0, r1, r2, r3}};
+  // Extension multiply (equal to baby_bear.rs:744-757) with lazy reduction: x^4 =
+  // NBETA is applied to b's upper limbs first, then each output limb is a sum of
+  // four 62-bit products (< 2^64), folded below p * 2^32 and reduced once.
+  // Results are canonical, hence bit-identical to the reference.
+  const uint32_t n1 = fp_mul(kNBeta, b.c[1]), n2 = fp_mul(kNBeta, b.c[2]), n3 = fp_mul(kNBeta, b.c[3]);
+  const uint64_t a0 = a.c[0], a1 = a.c[1], a2 = a.c[2], a3 = a.c[3];
+  uint64_t s0 = a0 * b.c[0] + a1 * n3 + a2 * n2 + a3 * n1;
+  uint64_t s1 = a0 * b.c[1] + a1 * b.c[0] + a2 * n3 + a3 * n2;
+  uint64_t s2 = a0 * b.c[2] + a1 * b.c[1] + a2 * b.c[0] + a3 * n3;
+  uint64_t s3 = a0 * b.c[3] + a1 * b.c[2] + a2 * b.c[1] + a3 * b.c[0];
+  return FpExt{{mont_reduce(fold64(s0)), mont_reduce(fold64(s1)), mont_reduce(fold64(s2)), mont_reduce(fold64(s3))}};
 }
 R0_HD FpExt fe_pow(FpExt x, uint64_t n) {
   FpExt tot = fe_one();

@@ -10,6 +10,7 @@ struct EvalCheckArgs {
   const uint32_t* const* args;  // poly_fp argument buffers, circuit order
   size_t nargs;
   const uint32_t* poly_mix;     // poly_mix powers + folded products (FpExt AoS, Montgomery)
+  const uint32_t* poly_mix_nb;  // the same table times NBETA = -11 (lazy extension products)
   uint32_t* acc;                // scratch: domain x FpExt
   uint32_t* check;              // out: 4 x domain
   const uint32_t* vinv;         // 4 values: inv((3 w^c)^N - 1) for c = 0..3

@@ -221,6 +221,9 @@ void run_eval_check(const CircuitDef& c, uint32_t* check, const uint32_t* const*
   e.args = args.data();
   e.nargs = args.size();
   e.poly_mix = upload(pm, 20);
+  std::vector<FpExt> pmn(pm.size());
+  for (size_t i = 0; i < pm.size(); i++) pmn[i] = fe_mul_fp(pm[i], kNBeta);
+  e.poly_mix_nb = upload(pmn, 25);
   e.vinv = upload(vinv, 21);
   e.acc = static_cast<uint32_t*>(scratch(domain * 16, 22));
   e.mat_fp = static_cast<uint32_t*>(scratch(size_t(info.mat_fp) * domain * 4 + 16, 23));

@@ -217,6 +217,7 @@ def emit(circuit, outdir, budget):
         "struct Args {",
         f"  const uint32_t* a[{nargs}];",
         "  const uint32_t* pm;   // poly_mix powers then folded products, FpExt AoS",
+        "  const uint32_t* pmn;  // the same times NBETA",
         "  uint32_t* acc;        // FpExt AoS accumulator per point",
         "  uint32_t* check;      // 4 SoA planes",
         "  const uint32_t* vinv; // inv((3x)^N - 1) for cycle & 3",
@@ -225,9 +226,6 @@ def emit(circuit, outdir, budget):
         "  uint32_t domain;",
         "};",
         f"constexpr int NPM = {npm};",
-        "__device__ __forceinline__ FpExt pmx(const uint32_t* pm, int k) {",
-        "  return FpExt{{pm[4 * k], pm[4 * k + 1], pm[4 * k + 2], pm[4 * k + 3]}};",
-        "}",
         "__device__ __forceinline__ FpExt eadd(FpExt a, FpExt b) { return fe_add(a, b); }",
         "__device__ __forceinline__ FpExt eadd(FpExt a, uint32_t b) { a.c[0] = fp_add(a.c[0], b); return a; }",
         "__device__ __forceinline__ FpExt eadd(uint32_t a, FpExt b) { b.c[0] = fp_add(a, b.c[0]); return b; }",
@@ -238,19 +236,115 @@ def emit(circuit, outdir, budget):
         "__device__ __forceinline__ FpExt emul(FpExt a, uint32_t b) { return fe_mul_fp(a, b); }",
         "__device__ __forceinline__ FpExt emul(uint32_t a, FpExt b) { return fe_mul_fp(b, a); }",
         "__device__ __forceinline__ uint32_t emul(uint32_t a, uint32_t b) { return fp_mul(a, b); }",
+        "// Lazy FpExt accumulator: four unreduced 64-bit sums of Montgomery products",
+        "// (each < p^2); the generator tracks an upper bound per value and folds",
+        "// (hi * (2^32 mod p) + lo, < 2^60) before a sum could reach 2^64.",
+        "struct Acc { uint64_t c[4]; };",
+        "// a canonical value v enters as v * 2^32 (mod p), so the final REDC returns v",
+        "__device__ __forceinline__ Acc acc_of(FpExt a) {",
+        "  return Acc{{uint64_t(a.c[0]) * kFoldC, uint64_t(a.c[1]) * kFoldC, uint64_t(a.c[2]) * kFoldC,",
+        "              uint64_t(a.c[3]) * kFoldC}};",
+        "}",
+        "__device__ __forceinline__ Acc acc_of(uint32_t a) { return Acc{{uint64_t(a) * kFoldC, 0, 0, 0}}; }",
+        "__device__ __forceinline__ Acc acc_fold(Acc a) {",
+        "#pragma unroll",
+        "  for (int i = 0; i < 4; i++) a.c[i] = fold64(a.c[i]);",
+        "  return a;",
+        "}",
+        "__device__ __forceinline__ FpExt acc_red(Acc a) {",
+        "  return FpExt{{mont_reduce(a.c[0]), mont_reduce(a.c[1]), mont_reduce(a.c[2]), mont_reduce(a.c[3])}};",
+        "}",
+        "__device__ __forceinline__ Acc acc_add(Acc a, Acc b) {",
+        "#pragma unroll",
+        "  for (int i = 0; i < 4; i++) a.c[i] += b.c[i];",
+        "  return a;",
+        "}",
+        "// a += t * pm[k]  (t in Fp)",
+        "__device__ __forceinline__ Acc acc_fp(Acc a, uint32_t t, const uint32_t* pm, int k) {",
+        "#pragma unroll",
+        "  for (int i = 0; i < 4; i++) a.c[i] += uint64_t(t) * pm[4 * k + i];",
+        "  return a;",
+        "}",
+        "// a += t * pm[k]  (t in FpExt; x^4 = NBETA folded into pmn = NBETA * pm)",
+        "__device__ __forceinline__ Acc acc_ext(Acc a, FpExt t, const uint32_t* pm, const uint32_t* pmn, int k) {",
+        "  const uint32_t* q = pm + 4 * k;",
+        "  const uint32_t* n = pmn + 4 * k;",
+        "  a.c[0] += uint64_t(t.c[0]) * q[0] + uint64_t(t.c[1]) * n[3] + uint64_t(t.c[2]) * n[2] + uint64_t(t.c[3]) * n[1];",
+        "  a.c[1] += uint64_t(t.c[0]) * q[1] + uint64_t(t.c[1]) * q[0] + uint64_t(t.c[2]) * n[3] + uint64_t(t.c[3]) * n[2];",
+        "  a.c[2] += uint64_t(t.c[0]) * q[2] + uint64_t(t.c[1]) * q[1] + uint64_t(t.c[2]) * q[0] + uint64_t(t.c[3]) * n[3];",
+        "  a.c[3] += uint64_t(t.c[0]) * q[3] + uint64_t(t.c[1]) * q[2] + uint64_t(t.c[2]) * q[1] + uint64_t(t.c[3]) * q[0];",
+        "  return a;",
+        "}",
     ]
     common_text = "\n".join(common) + "\n"
 
     stats = []
+    PROD = (P - 1) ** 2
+    LIM = 2**64
+    RED = P * 2**32
+    CANON = (P - 1) * (2**32 % P)  # bound of acc_of(canonical)
+
+    def fold_bound(bd):
+        return (bd >> 32) * (2**32 % P) + 2**32 - 1
+
     for ki, items in enumerate(kernels):
         roots = []
         for it in items:
             roots += [it[3]] if it[2] == "mat" else term_roots(it[3])
         need = pg.cone(roots)
         produced = set(it[3] for it in items if it[2] == "mat")
+        loaded = set(v for v in need if v in pg.mat and v not in produced)
         first, last = ki == 0, ki == len(kernels) - 1
+        mine = [it[3] for it in items if it[2] == "term"]
+        # accumulate ops computed here stay lazy (Acc a<i>); canonical v<i> only where needed
+        lazy = set(v for v in need if v not in loaded and pg.byid[v][0] in "ab")
+        canon = set(produced & lazy)
+        for v in need:
+            if v in loaded:
+                continue
+            ins = pg.byid[v]
+            ds = deps(ins)
+            for n, d in enumerate(ds):
+                if d in lazy and not (ins[0] in "ab" and n == 0):
+                    canon.add(d)
+        for e, f in mine:
+            if f and e in lazy:
+                canon.add(e)
+            for x in f:
+                if x[0] == "v" and x[1] in lazy:
+                    canon.add(x[1])
+        bound = {}
         L = []
         w = L.append
+
+        def acc_src(x):
+            """(expression, bound) of an Acc holding value x."""
+            if x in lazy:
+                return f"a{x}", bound[x]
+            return f"acc_of(v{x})", CANON
+
+        def room(expr, bd, k):
+            """fold expr first if adding k more products could overflow 64 bits."""
+            if bd + k * PROD >= LIM:
+                return f"acc_fold({expr})", fold_bound(bd)
+            return expr, bd
+
+        def reduced(expr, bd):
+            if bd >= RED:
+                return f"acc_red(acc_fold({expr}))"
+            return f"acc_red({expr})"
+
+        def pmidx(k):
+            return str(k)
+
+        def add_prod(expr, bd, t, tty, k):
+            """Acc expression for expr + t * pm[k]; t canonical of type tty."""
+            n = 1 if tty == "f" else 4
+            expr, bd = room(expr, bd, n)
+            if tty == "f":
+                return f"acc_fp({expr}, {t}, A.pm, {k})", bd + PROD
+            return f"acc_ext({expr}, {t}, A.pm, A.pmn, {k})", bd + 4 * PROD
+
         w(f"// GENERATED by tools/gen_eval_check.py from risc0_amd/circuits/{circuit}.poly.ir — do not edit.")
         w(common_text)
         w(f"__global__ __launch_bounds__(256) void k{ki}(Args A) {{")
@@ -261,12 +355,12 @@ def emit(circuit, outdir, budget):
             op, i = ins[0], ins[1]
             if i not in need or op == "r":
                 continue
-            if i in pg.mat and i not in produced:
-                kind, s = slot[i]
+            if i in loaded:
+                kind, s_ = slot[i]
                 if kind == "f":
-                    w(f"  const uint32_t v{i} = A.mf[uint64_t({s}u) * A.domain + cycle];")
+                    w(f"  const uint32_t v{i} = A.mf[uint64_t({s_}u) * A.domain + cycle];")
                 else:
-                    w(f"  FpExt v{i}; {{ uint4 t = reinterpret_cast<const uint4*>(A.me)[uint64_t({s}u) * A.domain + cycle];"
+                    w(f"  FpExt v{i}; {{ uint4 t = reinterpret_cast<const uint4*>(A.me)[uint64_t({s_}u) * A.domain + cycle];"
                       f" v{i} = FpExt{{{{t.x, t.y, t.z, t.w}}}}; }}")
                 continue
             if op == "c":
@@ -277,10 +371,19 @@ def emit(circuit, outdir, budget):
                 w(f"  const uint32_t v{i} = A.a[{ins[2]}][{ins[3]}u * A.domain + ((cycle - {4 * ins[4]}u) & mask)];")
             elif op == "g":
                 w(f"  const uint32_t v{i} = A.a[{ins[2]}][{ins[3]}];")
-            elif op == "a":
-                w(f"  const FpExt v{i} = eadd(v{ins[2]}, emul(v{ins[3]}, pmx(A.pm, {ins[4]})));")
-            elif op == "b":
-                w(f"  const FpExt v{i} = eadd(v{ins[2]}, emul(emul(v{ins[3]}, v{ins[4]}), pmx(A.pm, {ins[5]})));")
+            elif op in "ab":
+                src, bd = acc_src(ins[2])
+                if op == "a":
+                    t, tty, k = f"v{ins[3]}", types[ins[3]], ins[4]
+                else:
+                    T, U, k = ins[3], ins[4], ins[5]
+                    t = f"emul(v{T}, v{U})"
+                    tty = "e" if "e" in (types[T], types[U]) else "f"
+                expr, bd = add_prod(src, bd, t, tty, k)
+                w(f"  const Acc a{i} = {expr};")
+                bound[i] = bd
+                if i in canon:
+                    w(f"  const FpExt v{i} = {reduced(f'a{i}', bd)};")
             else:
                 a, b = ins[2], ins[3]
                 if types[a] == "f" and types[b] == "f":
@@ -290,39 +393,64 @@ def emit(circuit, outdir, budget):
                     fn = {"+": "eadd", "-": "esub", "*": "emul"}[op]
                     w(f"  const FpExt v{i} = {fn}(v{a}, v{b});")
             if i in produced:
-                kind, s = slot[i]
+                kind, s_ = slot[i]
                 if kind == "f":
-                    w(f"  A.mf[uint64_t({s}u) * A.domain + cycle] = v{i};")
+                    w(f"  A.mf[uint64_t({s_}u) * A.domain + cycle] = v{i};")
                 else:
-                    w(f"  reinterpret_cast<uint4*>(A.me)[uint64_t({s}u) * A.domain + cycle] ="
+                    w(f"  reinterpret_cast<uint4*>(A.me)[uint64_t({s_}u) * A.domain + cycle] ="
                       f" make_uint4(v{i}.c[0], v{i}.c[1], v{i}.c[2], v{i}.c[3]);")
-        mine = [it[3] for it in items if it[2] == "term"]
         if mine or last:
-            w("  FpExt s = fe_zero();")
+            w("  uint4* accp = reinterpret_cast<uint4*>(A.acc) + cycle;")
+            if first:
+                w("  Acc s0 = Acc{{0, 0, 0, 0}};")
+                sb = 0
+            else:
+                w("  Acc s0; { uint4 p = *accp; s0 = acc_of(FpExt{{p.x, p.y, p.z, p.w}}); }")
+                sb = CANON
+            sn = 0
             for e, f in mine:
                 vals = [x[1] for x in f if x[0] == "v"]
                 pms = tuple(sorted(x[1] for x in f if x[0] == "pm"))
+                if not vals and not pms:
+                    src, bd = acc_src(e)
+                    cur, sb2 = f"s{sn}", sb
+                    if sb2 + bd >= LIM:
+                        cur, sb2 = f"acc_fold({cur})", fold_bound(sb2)
+                    if sb2 + bd >= LIM:
+                        src, bd = f"acc_fold({src})", fold_bound(bd)
+                    w(f"  const Acc s{sn + 1} = acc_add({cur}, {src});")
+                    sb = sb2 + bd
+                    sn += 1
+                    continue
                 expr = f"v{e}"
+                ety = types[e]
                 for v in vals:
                     expr = f"emul({expr}, v{v})"
+                    if types[v] == "e":
+                        ety = "e"
+                if not pms:
+                    src = f"acc_of({expr})"
+                    cur, sb2 = room(f"s{sn}", sb, 1)
+                    w(f"  const Acc s{sn + 1} = acc_add({cur}, {src});")
+                    sb = sb2 + CANON
+                    sn += 1
+                    continue
                 if len(pms) == 1:
-                    expr = f"emul({expr}, pmx(A.pm, {pms[0]}))"
-                elif len(pms) > 1:
+                    k = pms[0]
+                else:
                     if pms not in combo_index:
                         combo_index[pms] = len(combo_index)
-                    expr = f"emul({expr}, pmx(A.pm, NPM + {combo_index[pms]}))"
-                w(f"  s = eadd(s, {expr});")
-            w("  uint4* accp = reinterpret_cast<uint4*>(A.acc) + cycle;")
-            if not first:
-                w("  { uint4 p = *accp; s = fe_add(s, FpExt{{p.x, p.y, p.z, p.w}}); }")
+                    k = f"NPM + {combo_index[pms]}"
+                e2, sb = add_prod(f"s{sn}", sb, expr, ety, k)
+                w(f"  const Acc s{sn + 1} = {e2};")
+                sn += 1
+            w(f"  FpExt s = {reduced(f's{sn}', sb)};")
             if last:
                 w("  s = fe_mul_fp(s, A.vinv[cycle & 3]);")
                 w("  #pragma unroll")
                 w("  for (int k = 0; k < 4; k++) A.check[uint64_t(k) * A.domain + cycle] = s.c[k];")
             else:
                 w("  *accp = make_uint4(s.c[0], s.c[1], s.c[2], s.c[3]);")
-        elif not first:
-            pass
         if first and not mine and not last:
             # keep the accumulator defined for later kernels
             w("  reinterpret_cast<uint4*>(A.acc)[cycle] = make_uint4(0u, 0u, 0u, 0u);")
@@ -359,7 +487,7 @@ def emit(circuit, outdir, budget):
     w(f"  R0_REQUIRE(e.nargs == {nargs}, \"eval_check_{circuit}: wrong argument count\");")
     w("  Args A;")
     w(f"  for (int i = 0; i < {nargs}; i++) A.a[i] = e.args[i];")
-    w("  A.pm = e.poly_mix; A.acc = e.acc; A.check = e.check; A.vinv = e.vinv; A.domain = e.domain;")
+    w("  A.pm = e.poly_mix; A.pmn = e.poly_mix_nb; A.acc = e.acc; A.check = e.check; A.vinv = e.vinv; A.domain = e.domain;")
     w("  A.mf = e.mat_fp; A.me = e.mat_ext;")
     for ki in range(len(kernels)):
         w(f"  launch_k{ki}(s, A);")
