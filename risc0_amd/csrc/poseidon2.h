@@ -19,6 +19,7 @@ static const uint32_t kP2Partial[21] = P2_PARTIAL_RC_MONT;
 static const uint32_t kP2Diag[24] = P2_DIAG_MONT;
 #endif
 
+// ---- reference formulation (mod.rs:102-216 step by step, every value canonical) ----
 R0_HD uint32_t p2_sbox(uint32_t x) {
   uint32_t x2 = fp_mul(x, x);
   uint32_t x4 = fp_mul(x2, x2);
@@ -45,44 +46,118 @@ R0_HD void p2_m4(uint32_t* x) {
 
 // M_EXT: mod.rs:150-173
 R0_HD void p2_m_ext(uint32_t* c) {
-#pragma unroll
   for (int i = 0; i < 6; i++) p2_m4(c + 4 * i);
   uint32_t s[4];
-#pragma unroll
   for (int j = 0; j < 4; j++) {
     s[j] = fp_add(fp_add(fp_add(c[j], c[4 + j]), fp_add(c[8 + j], c[12 + j])), fp_add(c[16 + j], c[20 + j]));
   }
-#pragma unroll
   for (int i = 0; i < 24; i++) c[i] = fp_add(c[i], s[i & 3]);
 }
 
 // M_INT = 1 + diag: mod.rs:129-135
 R0_HD void p2_m_int(uint32_t* c) {
   uint32_t sum = 0;
-#pragma unroll
   for (int i = 0; i < 24; i++) sum = fp_add(sum, c[i]);
-#pragma unroll
   for (int i = 0; i < 24; i++) c[i] = fp_add(sum, fp_mul(kP2Diag[i], c[i]));
 }
 
 R0_HD void p2_full_round(uint32_t* c, int r) {
-#pragma unroll
   for (int i = 0; i < 24; i++) c[i] = p2_sbox(fp_add(c[i], kP2Full[r * 24 + i]));
   p2_m_ext(c);
 }
 
-// mod.rs:193-216
-R0_HD void poseidon2_mix(uint32_t* c) {
+R0_HD void poseidon2_mix_simple(uint32_t* c) {
   p2_m_ext(c);
-#pragma unroll
   for (int r = 0; r < 4; r++) p2_full_round(c, r);
-#pragma unroll
   for (int r = 0; r < 21; r++) {
     c[0] = p2_sbox(fp_add(c[0], kP2Partial[r]));
     p2_m_int(c);
   }
-#pragma unroll
   for (int r = 4; r < 8; r++) p2_full_round(c, r);
+}
+
+// ---- VALU-lean formulation (same permutation, ~30% fewer instructions) ----------
+// Poseidon2 is integer-VALU bound on CDNA4 (one v_* per 4 cycles per SIMD), so the
+// count of instructions is the cost. Bounds (p < 2^31):
+//  * sbox: x^2 canonical, then three REDCs without the final umin: each product has
+//    one factor < p and one < 2p, so t < 2p^2 < p*2^32 and the result is < 2p;
+//  * M_EXT runs in 64-bit on those lazy (< 2p) cells: every output is a combination
+//    with coefficient sum <= 112, so y < 224p < 2^39, and one Barrett step
+//    (q = ((y >> 7) * 273) >> 32 is floor(y/p) or one less) plus a umin gives the
+//    canonical cell — the next round constant is added in 64-bit before it;
+//  * M_INT: c_i*d_i + S = REDC(c_i*d_i + S*2^32) and S*2^32 is congruent to
+//    fold64(sum c_i * (2^32 mod p)) < 2^60, so multiply, add and reduce are one
+//    v_mad_u64_u32 plus one REDC (t < p^2 + 2^60 < p*2^32).
+R0_HD uint32_t p2_red39(uint64_t y) {
+  uint32_t q = uint32_t((uint64_t(uint32_t(y >> 7)) * 273u) >> 32);
+  uint32_t r = uint32_t(y) - q * kP;  // in [0, 2p)
+  return umin(r, r - kP);
+}
+R0_HD uint32_t mont_lazy(uint64_t t) {  // t < p*2^32 -> t*2^-32 mod p in [0, 2p)
+  uint32_t m = uint32_t(t) * kNegPinv;
+  return uint32_t((t + uint64_t(m) * kP) >> 32);
+}
+R0_HD uint32_t p2_sbox_lazy(uint32_t x) {  // x canonical -> x^7 in [0, 2p)
+  uint32_t x2 = fp_mul(x, x);
+  uint32_t x4 = mont_lazy(uint64_t(x2) * x2);
+  uint32_t x6 = mont_lazy(uint64_t(x4) * x2);
+  return mont_lazy(uint64_t(x6) * x);
+}
+// y = M_EXT * x over the integers (x < 2p)
+R0_HD void p2_m_ext64(const uint32_t* x, uint64_t* y) {
+#pragma unroll
+  for (int b = 0; b < 6; b++) {
+    const uint32_t* v = x + 4 * b;
+    uint64_t t0 = uint64_t(v[0]) + v[1];
+    uint64_t t1 = uint64_t(v[2]) + v[3];
+    uint64_t t2 = (uint64_t(v[1]) << 1) + t1;
+    uint64_t t3 = (uint64_t(v[3]) << 1) + t0;
+    uint64_t t4 = (t1 << 2) + t3;
+    uint64_t t5 = (t0 << 2) + t2;
+    y[4 * b] = t3 + t5;
+    y[4 * b + 1] = t5;
+    y[4 * b + 2] = t2 + t4;
+    y[4 * b + 3] = t4;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    uint64_t s = ((y[j] + y[4 + j]) + (y[8 + j] + y[12 + j])) + (y[16 + j] + y[20 + j]);
+#pragma unroll
+    for (int b = 0; b < 6; b++) y[4 * b + j] += s;
+  }
+}
+
+R0_HD void poseidon2_mix(uint32_t* c) {
+  uint64_t y[24];
+  uint32_t x[24];
+  p2_m_ext64(c, y);
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+#pragma unroll
+    for (int i = 0; i < 24; i++) x[i] = p2_sbox_lazy(p2_red39(y[i] + kP2Full[r * 24 + i]));
+    p2_m_ext64(x, y);
+  }
+#pragma unroll
+  for (int i = 0; i < 24; i++) c[i] = p2_red39(y[i]);
+#pragma unroll
+  for (int r = 0; r < 21; r++) {
+    c[0] = p2_sbox_lazy(fp_add(c[0], kP2Partial[r]));
+    c[0] = umin(c[0], c[0] - kP);
+    uint64_t sf = 0;
+#pragma unroll
+    for (int i = 0; i < 24; i++) sf += uint64_t(c[i]) * kFoldC;
+    sf = fold64(sf);
+#pragma unroll
+    for (int i = 0; i < 24; i++) c[i] = mont_reduce(uint64_t(c[i]) * kP2Diag[i] + sf);
+  }
+#pragma unroll
+  for (int r = 4; r < 8; r++) {
+#pragma unroll
+    for (int i = 0; i < 24; i++) x[i] = p2_sbox_lazy(fp_add(c[i], kP2Full[r * 24 + i]));
+    p2_m_ext64(x, y);
+#pragma unroll
+    for (int i = 0; i < 24; i++) c[i] = p2_red39(y[i]);
+  }
 }
 
 }  // namespace r0
