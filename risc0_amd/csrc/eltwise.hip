@@ -438,7 +438,9 @@ void batch_evaluate_any(hipStream_t s, const uint32_t* coeffs, size_t poly_count
   (void)poly_count;
   uint64_t n = uint64_t(1) << log_n;
   uint32_t nchunks = uint32_t((n + kEvChunk - 1) / kEvChunk);
-  KScope ks("batch_evaluate_any", double(std::min<size_t>(poly_count, eval_count)) * n * 4);
+  // per coefficient: FpExt power step (16) + FpExt x Fp term (4)
+  KScope ks("batch_evaluate_any", double(std::min<size_t>(poly_count, eval_count)) * n * 4,
+            double(eval_count) * n * 20);
   R0_REQUIRE(n % kEvPer == 0, "batch_evaluate_any: poly size must be a multiple of 16");
   R0_REQUIRE(eval_count < 65536, "batch_evaluate_any: too many evaluations");
   uint32_t* partial = static_cast<uint32_t*>(scratch(size_t(eval_count) * nchunks * 16, 2));

@@ -25,6 +25,7 @@ struct EvalCheckInfo {
   int npm;            // number of poly_mix powers the kernels index directly
   int nargs;
   int mat_fp, mat_ext, kernels;
+  double modmuls_per_point;  // field multiplications of the restated poly_fp (+4 for the 1/Z scale)
 };
 
 void eval_check_rv32im(hipStream_t s, const EvalCheckArgs& e);

@@ -17,6 +17,7 @@ namespace r0 {
 namespace {
 
 constexpr int kThreads = 256;
+constexpr double kP2Modmuls = 8 * 24 * 4 + 21 * 4 + 21 * 24;
 
 __device__ __forceinline__ void store_digest(uint32_t* out, const uint32_t* d) {
   uint4* o = reinterpret_cast<uint4*>(out);
@@ -178,7 +179,10 @@ __global__ __launch_bounds__(kThreads) void fold_top_kernel(uint32_t* io, uint32
 void hash_rows(hipStream_t s, int suite, uint32_t* out, const uint32_t* matrix, size_t rows, size_t cols) {
   if (rows == 0) return;
   R0_REQUIRE(cols < (1ull << 31), "hash_rows: too many columns");
-  KScope ks(suite == 0 ? "hash_rows_poseidon2" : "hash_rows_sha256", double(rows) * (cols * 4 + 32));
+  // Poseidon2 permutation = 1356 modmul (8x24 S-boxes x4, 21 partial S-boxes x4, 21x24 diagonal)
+  const double perms = double(rows) * (cols ? (cols + 15) / 16 : 1);
+  KScope ks(suite == 0 ? "hash_rows_poseidon2" : "hash_rows_sha256", double(rows) * (cols * 4 + 32),
+            suite == 0 ? perms * kP2Modmuls : 0);
   if (suite == 0)
     hipLaunchKernelGGL(p2_rows_kernel, dim3(div_up(rows, kThreads)), dim3(kThreads), 0, s, out, matrix,
                        uint64_t(rows), uint32_t(cols));
@@ -203,7 +207,8 @@ void hash_fold(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t
 // MerkleTreeProver::new (risc0/zkp/src/prove/merkle.rs:54-81): leaves, then every layer.
 void merkle_tree(hipStream_t s, int suite, uint32_t* nodes, const uint32_t* matrix, size_t rows, size_t cols) {
   hash_rows(s, suite, nodes + rows * 8, matrix, rows, cols);
-  KScope ks(suite == 0 ? "merkle_fold_poseidon2" : "merkle_fold_sha256", double(rows) * 32 * 1.5);
+  KScope ks(suite == 0 ? "merkle_fold_poseidon2" : "merkle_fold_sha256", double(rows) * 32 * 1.5,
+            suite == 0 ? double(rows - 1) * kP2Modmuls : 0);
   size_t layer = rows / 2;
   for (; layer > 512; layer /= 2) hash_fold(s, suite, nodes, 2 * layer, layer);
   if (layer >= 1) {

@@ -360,7 +360,8 @@ void fill_pass(PassArgs& p, bool inv, uint32_t L, uint32_t a, uint32_t b, size_t
 void ntt_evaluate(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count, uint32_t L,
                   uint32_t eb) {
   if (count == 0) return;
-  KScope ks("ntt_evaluate", double(count) * 4 * ((size_t(1) << L) + (size_t(1) << (L - eb))));
+  KScope ks("ntt_evaluate", double(count) * 4 * ((size_t(1) << L) + (size_t(1) << (L - eb))),
+            double(count) * double(size_t(1) << L) / 2 * (L - eb));  // one modmul per butterfly
   R0_REQUIRE(in != out || eb == 0, "expand_into_evaluate needs distinct buffers");
   if (L == 0) {
     HIP_OK(hipMemcpyAsync(out, in, count * 4, hipMemcpyDeviceToDevice, s));
@@ -381,7 +382,7 @@ void ntt_evaluate(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count
 
 void ntt_interpolate(hipStream_t s, uint32_t* io, size_t count, uint32_t L, bool zk) {
   if (count == 0 || L == 0) return;  // size-1 transform (and 3^0 shift) is the identity
-  KScope ks("ntt_interpolate", double(count) * 8 * (size_t(1) << L));
+  KScope ks("ntt_interpolate", double(count) * 8 * (size_t(1) << L), double(count) * double(size_t(1) << L) / 2 * L);
   auto pl = plan(L);
   for (size_t i = pl.size(); i-- > 0;) {
     PassArgs p{};

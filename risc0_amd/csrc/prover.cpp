@@ -232,7 +232,7 @@ void run_eval_check(const CircuitDef& c, uint32_t* check, const uint32_t* const*
   e.domain = uint32_t(domain);
   double bytes = 16.0 * domain;
   for (int g = 0; g < 3; g++) bytes += 4.0 * domain * c.group_sizes[g];
-  KScope ks("eval_check", bytes);
+  KScope ks("eval_check", bytes, double(domain) * info.modmuls_per_point);
   c.eval_check(s, e);
 }
 

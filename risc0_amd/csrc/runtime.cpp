@@ -135,7 +135,7 @@ void stage_reset() {
 namespace {
 struct KRec {
   std::string name;
-  double bytes;
+  double bytes, mm;
   hipEvent_t a, b;
 };
 bool g_kt_on = false;
@@ -147,9 +147,9 @@ void ktimer_enable(bool on) {
   g_kt_on = on;
 }
 
-KScope::KScope(const char* name, double bytes) {
+KScope::KScope(const char* name, double bytes, double mm) {
   if (!g_kt_on) return;
-  KRec r{name, bytes, nullptr, nullptr};
+  KRec r{name, bytes, mm, nullptr, nullptr};
   HIP_OK(hipEventCreate(&r.a));
   HIP_OK(hipEventCreate(&r.b));
   HIP_OK(hipEventRecord(r.a, stream()));
@@ -171,7 +171,7 @@ KScope::~KScope() {
 std::string ktimer_report() {
   HIP_OK(hipStreamSynchronize(stream()));
   std::lock_guard<std::mutex> lk(g_mu);
-  std::map<std::string, std::tuple<double, int, double>> agg;
+  std::map<std::string, std::tuple<double, int, double, double>> agg;
   for (auto& r : g_kt) {
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, r.a, r.b));
@@ -179,6 +179,7 @@ std::string ktimer_report() {
     std::get<0>(t) += ms;
     std::get<1>(t) += 1;
     std::get<2>(t) += r.bytes;
+    std::get<3>(t) += r.mm;
     (void)hipEventDestroy(r.a);
     (void)hipEventDestroy(r.b);
   }
@@ -186,8 +187,8 @@ std::string ktimer_report() {
   std::string out;
   for (auto& kv : agg) {
     char buf[256];
-    snprintf(buf, sizeof(buf), "%s=%.6f:%d:%.0f;", kv.first.c_str(), std::get<0>(kv.second), std::get<1>(kv.second),
-             std::get<2>(kv.second));
+    snprintf(buf, sizeof(buf), "%s=%.6f:%d:%.0f:%.0f;", kv.first.c_str(), std::get<0>(kv.second),
+             std::get<1>(kv.second), std::get<2>(kv.second), std::get<3>(kv.second));
     out += buf;
   }
   return out;

@@ -46,14 +46,15 @@ void upload_async(void* d_dst, const void* h_src, size_t bytes);
 void stage_reset();
 
 // Optional kernel-level timing (HIP events on the library stream around each
-// launcher), with the launcher's algorithmic HBM bytes for roofline reporting.
+// launcher), with the launcher's algorithmic HBM bytes and modmul-equivalent count
+// (field multiplications of the restated algorithm) for roofline reporting.
 struct KScope {
-  KScope(const char* name, double alg_bytes);
+  KScope(const char* name, double alg_bytes, double alg_modmuls = 0);
   ~KScope();
   int idx = -1;
 };
 void ktimer_enable(bool on);
-std::string ktimer_report();  // "name=total_ms:calls:alg_bytes;..." (synchronises)
+std::string ktimer_report();  // "name=total_ms:calls:alg_bytes:alg_modmuls;..." (synchronises)
 
 inline unsigned div_up(size_t a, size_t b) { return unsigned((a + b - 1) / b); }
 

@@ -33,8 +33,6 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise R0HipError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
         L = C.CDLL(LIB_PATH)
-        for name in dir(L):
-            pass
         _declare(L)
         _lib = L
     return _lib
@@ -336,13 +334,13 @@ def set_kernel_timing(on):
 
 
 def kernel_times():
-    """{kernel: (total_ms, calls, algorithmic_bytes)} since timing was enabled."""
+    """{kernel: (total_ms, calls, algorithmic_bytes, modmul_equivalents)} since timing was enabled."""
     buf = C.create_string_buffer(16384)
     check(lib().r0hip_kernel_times(buf, 16384))
     out = {}
     for kv in buf.value.decode().split(";"):
         if "=" in kv:
             k, v = kv.split("=")
-            ms, calls, b = v.split(":")
-            out[k] = (float(ms), int(calls), float(b))
+            ms, calls, b, mm = v.split(":")
+            out[k] = (float(ms), int(calls), float(b), float(mm))
     return out

@@ -326,3 +326,29 @@ def test_prove_segment_seal_identical(hal, hal_sha, oracle, circuit, suite, po2)
     assert np.array_equal(mix, ref_mix)
     assert seal.size == ref_seal.size
     assert np.array_equal(seal, ref_seal)
+
+
+# ---- golden fixtures (tests/golden, from the reference's compiled poly_fp; no oracle/_ref needed) ----
+import test_golden as G  # noqa: E402
+
+
+@pytest.mark.parametrize("case", G.INDEX["eval_check"], ids=lambda c: f"{c['circuit']}-po2{c['po2']}")
+def test_eval_check_golden(hal, oracle, case):
+    groups, mix, glob, pm = G.eval_inputs(oracle, case["circuit"], case["po2"], case["seed"])
+    out = hal.alloc_elem("check", 4 * (4 << case["po2"]))
+    hal.eval_check(case["circuit"], out, [dev(hal, g) for g in groups], dev(hal, mix), dev(hal, glob), pm,
+                   case["po2"])
+    assert np.array_equal(out.to_numpy(), np.load(G.os.path.join(G.GOLD, case["file"])))
+
+
+@pytest.mark.parametrize("case", G.INDEX["seals"], ids=lambda c: f"{c['circuit']}-{c['suite']}-po2{c['po2']}")
+def test_prove_segment_seal_golden(hal, hal_sha, oracle, case):
+    import risc0_amd as r
+    circuit, po2 = case["circuit"], case["po2"]
+    h = hal if case["suite"] == "poseidon2" else hal_sha
+    code, data, accum, glob = G.seal_inputs(oracle, circuit, po2)
+    seal, mix = r.prove_segment(h, circuit, po2, dev(h, code), dev(h, data), dev(h, accum), dev(h, glob),
+                                version=2 if circuit == "rv32im" else None)
+    assert seal.size == case["seal_words"]
+    assert G.digest(seal) == case["seal_sha256"]
+    assert [int(x) for x in mix] == case["mix"]

@@ -111,6 +111,25 @@ class Program:
         return sum(self.cost(v) for v in self.cone(roots) if not (v in self.mat and v not in rs))
 
 
+def modmuls(pg):
+    """Field multiplications of the program as written (Fp x Fp = 1, FpExt x Fp = 4,
+    FpExt x FpExt = 16; accumulate ops count their products) — the algorithmic op count
+    the VALU roofline is quoted in."""
+    ty = pg.types
+    n = 0
+    for ins in pg.prog:
+        op = ins[0]
+        if op == "*":
+            a, b = ty[ins[2]], ty[ins[3]]
+            n += 16 if (a, b) == ("e", "e") else (4 if "e" in (a, b) else 1)
+        elif op == "a":
+            n += 16 if ty[ins[3]] == "e" else 4
+        elif op == "b":
+            fe = "e" in (ty[ins[3]], ty[ins[4]])
+            n += (4 if fe else 1) + (16 if fe else 4)
+    return n
+
+
 def term_roots(t):
     return [t[0]] + [x[1] for x in t[1] if x[0] == "v"]
 
@@ -481,6 +500,7 @@ def emit(circuit, outdir, budget):
     w(f"void eval_check_{circuit}_info(EvalCheckInfo* info) {{")
     w(f"  info->combos = ec_{circuit}::kPmCombos; info->ncombos = {len(combo_index)}; info->npm = ec_{circuit}::NPM;")
     w(f"  info->nargs = {nargs}; info->mat_fp = {nf}; info->mat_ext = {ne}; info->kernels = {len(kernels)};")
+    w(f"  info->modmuls_per_point = {modmuls(pg) + 4};")
     w("}")
     w(f"void eval_check_{circuit}(hipStream_t s, const EvalCheckArgs& e) {{")
     w(f"  using namespace ec_{circuit};")
