@@ -31,49 +31,63 @@ constexpr int kThreads = 256;
 struct PassArgs {
   uint32_t* out;
   const uint32_t* in;       // expand source (first forward pass) or == out
-  const uint32_t* local_tw; // [2^(s-1) + k] = w_{2^s}^k, s = 1..b (fwd or rev roots)
-  const uint32_t* sc_lo;    // w_{2^(a+b)}^e = sc_hi[e >> sc_split] * sc_lo[e & mask]
+  const uint32_t* local_tw; // [2^(s-1) + k] = w_{2^s}^k, s = 1..B (fwd or rev roots)
+  const uint32_t* sc_lo;    // w_{2^(a+B)}^e = sc_hi[e >> sc_split] * sc_lo[e & mask]
   const uint32_t* sc_hi;
-  const uint32_t* post_t;   // last inverse pass: per-t factor (norm * 3^{rev_b(t)*2^(L-b)})
-  const uint32_t* post_hi;  // last inverse pass: per-row factor 3^{rev_{L-b}(row)} (or null)
-  uint64_t groups;          // total groups of 2^b elements over the whole batch
-  uint32_t L, a, b, c, eb;  // eb: expand bits (first forward pass only)
+  const uint32_t* post_t;   // last inverse pass: per-t factor (norm * 3^{rev_B(t)*2^(L-B)})
+  const uint32_t* post_hi;  // last inverse pass: per-row factor 3^{rev_{L-B}(row)} (or null)
+  uint64_t groups;          // total groups of 2^B elements over the whole batch
+  uint32_t L, a, eb;        // eb: expand bits (first forward pass only)
   uint32_t sc_split;
 };
 
-// LDS placement. Row passes (a == 0) keep each row contiguous with one pad word
-// per 8 so strided butterfly reads spread over the banks; column passes store
-// [t][j] with the 2^c (= 32) adjacent columns of a row in consecutive words.
-template <bool COLS>
-__device__ __forceinline__ uint32_t lidx(uint32_t j, uint32_t t, uint32_t b, uint32_t c) {
-  if (COLS) return (t << c) + j;
-  return j * ((1u << b) + (1u << b >> 3)) + t + (t >> 3);
+// Pass shapes are compile-time (B index bits per pass, 2^C rows or columns per
+// workgroup), so every LDS index below is shifts and masks of constants.
+//
+// LDS placement. Row passes (a == 0) keep each row contiguous with one pad word per
+// 8 so strided butterfly reads spread over the banks; column passes store [t][j]
+// with the 2^C (= 32) adjacent columns of a row in consecutive words.
+template <bool COLS, int B, int C>
+__device__ __forceinline__ uint32_t lidx(uint32_t j, uint32_t t) {
+  if (COLS) return (t << C) + j;
+  return j * ((1u << B) + (1u << B >> 3)) + t + (t >> 3);
+}
+template <bool COLS, int B, int C>
+constexpr uint32_t lds_words() {
+  return COLS ? (1u << (B + C)) : ((1u << B) + (1u << B >> 3)) << C;
 }
 
-// One stage group of 1..3 radix-2 stages [s0, s0+NST) done in registers: each lane
-// owns blocks of 2^NST elements t_base + m*h (h = 2^(s0-1)), so the group costs one
-// LDS read and one write per element instead of NST.
-template <bool INV, bool COLS, int NST>
-__device__ __forceinline__ void stage_group(uint32_t* lds, const uint32_t* __restrict__ tw, uint32_t s0,
-                                            uint32_t b, uint32_t c) {
+// One group of NST (1..3) radix-2 stages [s0, s0+NST) in registers: a lane owns blocks
+// of 2^NST elements t_base + m*h (h = 2^(s0-1)), so a group costs one LDS read and
+// write per element instead of NST. Twiddles come from the LDS copy of the table.
+template <bool INV, bool COLS, int B, int C, int NST, int FROM_EB = 0>
+__device__ __forceinline__ void stage_group(uint32_t* lds, const uint32_t* tw, uint32_t s0,
+                                            const uint32_t* csrc = nullptr) {
+  if constexpr (NST > B) return;  // never reached; keeps the shifts below well-formed
   constexpr uint32_t M = 1u << NST;
   const uint32_t h = 1u << (s0 - 1);
-  const uint32_t nrb = 1u << (b - NST);  // blocks per column/row
-  const uint32_t nblk = nrb << c;
-  for (uint32_t blk = threadIdx.x; blk < nblk; blk += kThreads) {
+  constexpr uint32_t nrb = 1u << (B >= NST ? B - NST : 0);  // blocks per column/row
+  constexpr uint32_t nblk = nrb << C;
+#pragma unroll
+  for (uint32_t it = 0; it < (nblk + kThreads - 1) / kThreads; it++) {
+    const uint32_t blk = it * kThreads + threadIdx.x;
+    if (nblk % kThreads != 0 && blk >= nblk) break;
     uint32_t j, r;
     if (COLS) {
-      j = blk & ((1u << c) - 1);
-      r = blk >> c;
+      j = blk & ((1u << C) - 1);
+      r = blk >> C;
     } else {
-      j = blk / nrb;
+      j = blk >> (B >= NST ? B - NST : 0);
       r = blk & (nrb - 1);
     }
     const uint32_t k = r & (h - 1);
     const uint32_t tb = ((r >> (s0 - 1)) << (s0 - 1 + NST)) | k;
     uint32_t v[M];
 #pragma unroll
-    for (uint32_t m = 0; m < M; m++) v[m] = lds[lidx<COLS>(j, tb + m * h, b, c)];
+    for (uint32_t m = 0; m < M; m++) {
+      if (FROM_EB) v[m] = csrc[(j << (B - FROM_EB)) + ((tb + m * h) >> FROM_EB)];  // replicated input
+      else v[m] = lds[lidx<COLS, B, C>(j, tb + m * h)];
+    }
     if (!INV) {
 #pragma unroll
       for (uint32_t st = 0; st < NST; st++) {
@@ -102,119 +116,205 @@ __device__ __forceinline__ void stage_group(uint32_t* lds, const uint32_t* __res
       }
     }
 #pragma unroll
-    for (uint32_t m = 0; m < M; m++) lds[lidx<COLS>(j, tb + m * h, b, c)] = v[m];
+    for (uint32_t m = 0; m < M; m++) lds[lidx<COLS, B, C>(j, tb + m * h)] = v[m];
   }
   __syncthreads();
 }
 
-template <bool INV, bool COLS>
-__device__ __forceinline__ void stages(uint32_t* lds, const uint32_t* __restrict__ tw, uint32_t first,
-                                       uint32_t last, uint32_t b, uint32_t c) {
-  // stages [first, last] inclusive, ascending for DIT, descending for DIF
+// stages [first, B] ascending (DIT) or [1, B] descending (DIF), radix-8 groups first
+template <bool INV, bool COLS, int B, int C, int EB = 0>
+__device__ __forceinline__ void stages(uint32_t* lds, const uint32_t* tw, const uint32_t* csrc = nullptr) {
   if (!INV) {
-    uint32_t s = first;
-    while (s <= last) {
-      uint32_t n = last - s + 1;
+    // DIT stages EB+1 .. B; the first group reads the compact (unreplicated) input
+#pragma unroll
+    for (uint32_t s = EB + 1; s <= uint32_t(B);) {
+      const uint32_t n = uint32_t(B) - s + 1;
+      const bool first = s == EB + 1 && EB > 0;
       if (n >= 3) {
-        stage_group<INV, COLS, 3>(lds, tw, s, b, c);
+        if (first) stage_group<INV, COLS, B, C, 3, EB>(lds, tw, s, csrc);
+        else stage_group<INV, COLS, B, C, 3>(lds, tw, s);
         s += 3;
       } else if (n == 2) {
-        stage_group<INV, COLS, 2>(lds, tw, s, b, c);
+        if (first) stage_group<INV, COLS, B, C, 2, EB>(lds, tw, s, csrc);
+        else stage_group<INV, COLS, B, C, 2>(lds, tw, s);
         s += 2;
       } else {
-        stage_group<INV, COLS, 1>(lds, tw, s, b, c);
+        if (first) stage_group<INV, COLS, B, C, 1, EB>(lds, tw, s, csrc);
+        else stage_group<INV, COLS, B, C, 1>(lds, tw, s);
         s += 1;
       }
     }
   } else {
-    int s = int(last);
-    while (s >= int(first)) {
-      int n = s - int(first) + 1;
-      if (n >= 3) {
-        stage_group<INV, COLS, 3>(lds, tw, uint32_t(s - 2), b, c);
+#pragma unroll
+    for (int s = B; s >= 1;) {
+      if (s >= 3) {
+        stage_group<INV, COLS, B, C, 3>(lds, tw, uint32_t(s - 2));
         s -= 3;
-      } else if (n == 2) {
-        stage_group<INV, COLS, 2>(lds, tw, uint32_t(s - 1), b, c);
+      } else if (s == 2) {
+        stage_group<INV, COLS, B, C, 2>(lds, tw, uint32_t(s - 1));
         s -= 2;
       } else {
-        stage_group<INV, COLS, 1>(lds, tw, uint32_t(s), b, c);
+        stage_group<INV, COLS, B, C, 1>(lds, tw, uint32_t(s));
         s -= 1;
       }
     }
   }
 }
 
-template <bool INV, bool EXPAND, bool LAST, bool COLS>
+
+// Column passes (C = 5, B >= 3): lane (j = tid & 31, t0 = tid >> 5) owns rows
+// t = 8i + t0, so rev_B(t) = rev_3(t0)*2^(B-3) + rev_{B-3}(i) and its twiddles are
+// base * c^k, k = rev_{B-3}(i) < E, with c = w_{2^(a+B)}^(low0+j) and
+// base = c^(rev_3(t0)*2^(B-3)): E running products (8 independent chains) replace
+// two table loads and a multiply per element.
+template <int B>
+struct ColTwiddles {
+  static constexpr uint32_t E = 1u << (B - 3);
+  uint32_t pw[E];
+  __device__ __forceinline__ void init(const PassArgs& p, uint32_t ex, uint32_t t0) {
+    const uint32_t c = fp_mul(p.sc_hi[ex >> p.sc_split], p.sc_lo[ex & ((1u << p.sc_split) - 1)]);
+    constexpr uint32_t S = E < 8 ? E : 8;
+    pw[0] = fp_pow(c, uint64_t(bitrev_n(t0, 3)) << (B - 3));
+#pragma unroll
+    for (uint32_t k = 1; k < S; k++) pw[k] = fp_mul(pw[k - 1], c);
+    uint32_t step = c;
+#pragma unroll
+    for (uint32_t k = 1; k < S; k <<= 1) step = fp_mul(step, step);  // c^S
+#pragma unroll
+    for (uint32_t k = S; k < E; k++) pw[k] = fp_mul(pw[k - S], step);
+  }
+  __device__ __forceinline__ uint32_t at(uint32_t i) const { return pw[bitrev_n(i, B - 3)]; }
+};
+
+template <bool INV, bool EXPAND, bool LAST, bool COLS, int B, int C, int EB>
 __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* tw = lds + lds_words<COLS, B, C>();
   const uint32_t tid = threadIdx.x;
-  const uint32_t nb = 1u << p.b;
-  const uint32_t C = 1u << p.c;
-  const uint32_t total = nb << p.c;
-  const uint32_t bmask = nb - 1;
+  constexpr uint32_t nb = 1u << B;
+  constexpr uint32_t total = nb << C;
   const uint64_t wg = blockIdx.x;
+  // stage twiddles -> LDS (entries 1 .. 2^B - 1)
+#pragma unroll
+  for (uint32_t i = 0; i < (nb + kThreads - 1) / kThreads; i++) {
+    uint32_t q = i * kThreads + tid;
+    if (q < nb) tw[q] = p.local_tw[q];
+  }
   uint64_t g_hi = 0;
   uint32_t low0 = 0;
   if (COLS) {
-    uint32_t lowblocks = 1u << (p.a - p.c);
-    low0 = uint32_t(wg % lowblocks) << p.c;
-    g_hi = wg / lowblocks;
+    const uint32_t lowblocks = 1u << (p.a - C);
+    low0 = uint32_t(wg & (lowblocks - 1)) << C;
+    g_hi = wg >> (p.a - C);
   }
-  // ---- load (forward column passes pre-scale by w_{2^(a+b)}^{low * rev_b(t)}) ----
-  for (uint32_t idx = tid; idx < total; idx += kThreads) {
-    uint32_t t, j;
-    uint64_t e;
-    bool ok = true;
-    if (!COLS) {
-      t = idx & bmask;
-      j = idx >> p.b;
-      uint64_t g = (wg << p.c) + j;
-      ok = g < p.groups;
-      e = (g << p.b) + t;
-    } else {
-      j = idx & (C - 1);
-      t = idx >> p.c;
-      e = (g_hi << (p.a + p.b)) + (uint64_t(t) << p.a) + low0 + j;
+  // ---- load: every global load of the workgroup is issued before the first LDS
+  // write (E words per lane in registers), so each lane has E loads in flight ----
+  uint32_t* compact = tw + nb;  // expand passes: the 2^(B+C-EB) distinct input words
+  if constexpr (!COLS) {
+    // rows [wg*2^C, +2^C): a contiguous run of 2^(B+C-EB) source words (expand: each
+    // stands for 2^EB replicated slots, which the first stage group reads in place)
+    constexpr uint32_t NIN = total >> EB;
+    constexpr uint32_t EIN = (NIN + kThreads - 1) / kThreads;
+    const uint32_t* src = EXPAND ? p.in : p.out;
+    const uint64_t base = wg << (B + C - EB);
+    const uint64_t limit = p.groups << (B - EB);
+    uint32_t r[EIN];
+#pragma unroll
+    for (uint32_t i = 0; i < EIN; i++) {
+      const uint32_t q = i * kThreads + tid;
+      r[i] = 0;
+      if ((NIN % kThreads == 0 || q < NIN) && base + q < limit) r[i] = src[base + q];
     }
-    uint32_t v = 0;
-    if (ok) {
-      if (EXPAND) v = p.in[e >> p.eb];
-      else v = p.out[e];
-      if (!INV && COLS) {
-        uint32_t ex = (low0 + j) * bitrev_n(t, p.b);
+#pragma unroll
+    for (uint32_t i = 0; i < EIN; i++) {
+      const uint32_t q = i * kThreads + tid;
+      if (NIN % kThreads != 0 && q >= NIN) continue;
+      if (EB == 0) lds[lidx<COLS, B, C>(q >> B, q & (nb - 1))] = r[i];
+      else if (EB >= B) {
+#pragma unroll
+        for (uint32_t rep = 0; rep < (1u << EB); rep++) {
+          const uint32_t el = (q << EB) + rep;
+          lds[lidx<COLS, B, C>(el >> B, el & (nb - 1))] = r[i];
+        }
+      } else compact[q] = r[i];
+    }
+  } else if constexpr (B < 3) {
+    // tiny column passes: plain mapping, table twiddles
+    constexpr uint32_t E = (total + kThreads - 1) / kThreads;
+#pragma unroll
+    for (uint32_t i = 0; i < E; i++) {
+      const uint32_t idx = i * kThreads + tid;
+      if (total % kThreads != 0 && idx >= total) continue;
+      const uint32_t j = idx & ((1u << C) - 1), t = idx >> C;
+      uint32_t v = p.out[(g_hi << (p.a + B)) + (uint64_t(t) << p.a) + low0 + j];
+      if (!INV) {
+        const uint32_t ex = (low0 + j) * bitrev_n(t, B);
         v = fp_mul(v, fp_mul(p.sc_hi[ex >> p.sc_split], p.sc_lo[ex & ((1u << p.sc_split) - 1)]));
       }
+      lds[lidx<COLS, B, C>(j, t)] = v;
     }
-    lds[lidx<COLS>(j, t, p.b, p.c)] = v;
+  } else {
+    // 2^C adjacent columns x 2^B rows of stride 2^a. Lane (j, r0) owns the rows t with
+    // rev_B(t) = u = r0*E + i, i < E, so its forward pre-scale factors
+    // w_{2^(a+B)}^{(low0+j)*u} are one running product (c^i) — no table loads.
+    constexpr uint32_t E = total / kThreads;
+    const uint32_t j = tid & ((1u << C) - 1), t0 = tid >> C;
+    uint32_t r[E];
+#pragma unroll
+    for (uint32_t i = 0; i < E; i++)
+      r[i] = p.out[(g_hi << (p.a + B)) + (uint64_t(8 * i + t0) << p.a) + low0 + j];
+    if (!INV) {
+      ColTwiddles<B> tf;
+      tf.init(p, low0 + j, t0);
+#pragma unroll
+      for (uint32_t i = 0; i < E; i++) r[i] = fp_mul(r[i], tf.at(i));
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < E; i++) lds[lidx<COLS, B, C>(j, 8 * i + t0)] = r[i];
   }
   __syncthreads();
-  if (!INV) stages<false, COLS>(lds, p.local_tw, 1 + (EXPAND ? p.eb : 0), p.b, p.b, p.c);
-  else stages<true, COLS>(lds, p.local_tw, 1, p.b, p.b, p.c);
+  if (!INV) stages<false, COLS, B, C, (EB < B ? EB : 0)>(lds, tw, compact);
+  else stages<true, COLS, B, C>(lds, tw);
   // ---- store (inverse column passes post-scale; last inverse pass normalises) ----
+  if constexpr (COLS && B >= 3) {
+    constexpr uint32_t E = total / kThreads;
+    const uint32_t j = tid & ((1u << C) - 1), t0 = tid >> C;
+    ColTwiddles<B> tf;
+    if (INV) tf.init(p, low0 + j, t0);
+#pragma unroll
+    for (uint32_t i = 0; i < E; i++) {
+      const uint32_t t = 8 * i + t0;
+      uint32_t v = lds[lidx<COLS, B, C>(j, t)];
+      if (INV) v = fp_mul(v, tf.at(i));
+      p.out[(g_hi << (p.a + B)) + (uint64_t(t) << p.a) + low0 + j] = v;
+    }
+    return;
+  }
+#pragma unroll 4
   for (uint32_t idx = tid; idx < total; idx += kThreads) {
     uint32_t t, j;
     uint64_t e;
     if (!COLS) {
-      t = idx & bmask;
-      j = idx >> p.b;
-      uint64_t g = (wg << p.c) + j;
+      t = idx & (nb - 1);
+      j = idx >> B;
+      const uint64_t g = (wg << C) + j;
       if (g >= p.groups) continue;
-      e = (g << p.b) + t;
+      e = (g << B) + t;
     } else {
-      j = idx & (C - 1);
-      t = idx >> p.c;
-      e = (g_hi << (p.a + p.b)) + (uint64_t(t) << p.a) + low0 + j;
+      j = idx & ((1u << C) - 1);
+      t = idx >> C;
+      e = (g_hi << (p.a + B)) + (uint64_t(t) << p.a) + low0 + j;
     }
-    uint32_t v = lds[lidx<COLS>(j, t, p.b, p.c)];
+    uint32_t v = lds[lidx<COLS, B, C>(j, t)];
     if (INV && COLS) {
-      uint32_t ex = (low0 + j) * bitrev_n(t, p.b);
+      const uint32_t ex = (low0 + j) * bitrev_n(t, B);
       v = fp_mul(v, fp_mul(p.sc_hi[ex >> p.sc_split], p.sc_lo[ex & ((1u << p.sc_split) - 1)]));
     }
     if (LAST) {
       v = fp_mul(v, p.post_t[t]);
       if (p.post_hi) {
-        uint64_t g = (wg << p.c) + j;
-        uint32_t row = uint32_t(g & ((uint64_t(1) << (p.L - p.b)) - 1));
+        const uint64_t g = (wg << C) + j;
+        const uint32_t row = uint32_t(g & ((uint64_t(1) << (p.L - B)) - 1));
         v = fp_mul(v, p.post_hi[row]);
       }
     }
@@ -327,28 +427,58 @@ std::vector<std::pair<uint32_t, uint32_t>> plan(uint32_t L) {
   return v;
 }
 
-template <bool INV, bool EXPAND, bool LAST, bool COLS>
-void launch_pass(hipStream_t s, PassArgs p) {
-  size_t lds = COLS ? (size_t(4) << (p.b + p.c)) : size_t(4) * ((size_t(1) << p.b) + (size_t(1) << p.b >> 3)) << p.c;
-  uint64_t nwg;
-  if (!COLS) nwg = (p.groups + (uint64_t(1) << p.c) - 1) >> p.c;
-  else nwg = p.groups >> p.c;  // groups = count * 2^(L-b); each wg takes 2^c adjacent columns
+// rows per workgroup of a row pass: enough rows that a workgroup holds >= 2048 words
+constexpr int row_c(int B) { return B >= 11 ? 0 : 11 - B; }
+
+template <bool INV, bool EXPAND, bool LAST, bool COLS, int B, int EB>
+void launch_pass_be(hipStream_t s, const PassArgs& p) {
+  constexpr int C = COLS ? 5 : row_c(B);
+  if (COLS) R0_REQUIRE(p.a >= uint32_t(C), "column pass needs >= 32 columns");
+  const size_t lds =
+      4 * (size_t(lds_words<COLS, B, C>()) + (size_t(1) << B) + (EB > 0 && EB < B ? (size_t(1) << (B + C - EB)) : 0));
+  uint64_t nwg = COLS ? (p.groups >> C) : ((p.groups + (uint64_t(1) << C) - 1) >> C);
   R0_REQUIRE(nwg < (1ull << 31), "ntt grid too large");
-  hipLaunchKernelGGL((ntt_pass_kernel<INV, EXPAND, LAST, COLS>), dim3(unsigned(nwg)), dim3(kThreads), lds, s, p);
+  hipLaunchKernelGGL((ntt_pass_kernel<INV, EXPAND, LAST, COLS, B, C, EB>), dim3(unsigned(nwg)), dim3(kThreads), lds,
+                     s, p);
   HIP_OK(hipGetLastError());
+}
+
+template <bool INV, bool EXPAND, bool LAST, bool COLS, int B>
+void launch_pass_b(hipStream_t s, const PassArgs& p) {
+  if (!EXPAND || p.eb == 0) return launch_pass_be<INV, EXPAND, LAST, COLS, B, 0>(s, p);
+  if constexpr (EXPAND && !COLS) {
+    if (p.eb == 1 && B >= 1) return launch_pass_be<INV, EXPAND, LAST, COLS, B, (B >= 1 ? 1 : 0)>(s, p);
+    if (p.eb == 2 && B >= 2) return launch_pass_be<INV, EXPAND, LAST, COLS, B, (B >= 2 ? 2 : 0)>(s, p);
+    if (p.eb == 3 && B >= 3) return launch_pass_be<INV, EXPAND, LAST, COLS, B, (B >= 3 ? 3 : 0)>(s, p);
+  }
+  R0_REQUIRE(false, "unsupported expand_bits for this NTT pass");
+}
+
+template <bool INV, bool EXPAND, bool LAST, bool COLS>
+void launch_pass(hipStream_t s, const PassArgs& p, uint32_t b) {
+  switch (b) {
+#define R0_CASE(X) \
+  case X: return launch_pass_b<INV, EXPAND, LAST, COLS, X>(s, p);
+    R0_CASE(1) R0_CASE(2) R0_CASE(3) R0_CASE(4) R0_CASE(5) R0_CASE(6) R0_CASE(7) R0_CASE(8) R0_CASE(9)
+#undef R0_CASE
+    default: break;
+  }
+  if (!COLS) {
+    switch (b) {
+      case 10: return launch_pass_b<INV, EXPAND, LAST, false, 10>(s, p);
+      case 11: return launch_pass_b<INV, EXPAND, LAST, false, 11>(s, p);
+      case 12: return launch_pass_b<INV, EXPAND, LAST, false, 12>(s, p);
+      case 13: return launch_pass_b<INV, EXPAND, LAST, false, 13>(s, p);
+      default: break;
+    }
+  }
+  R0_REQUIRE(false, "unsupported NTT pass size");
 }
 
 void fill_pass(PassArgs& p, bool inv, uint32_t L, uint32_t a, uint32_t b, size_t count) {
   p.L = L;
   p.a = a;
-  p.b = b;
   p.groups = uint64_t(count) << (L - b);
-  if (a == 0) {
-    // rows per workgroup so a workgroup holds >= 2048 elements
-    p.c = b >= 11 ? 0 : 11 - b;
-  } else {
-    p.c = a < 5 ? a : 5;
-  }
   p.local_tw = local_tw_table(inv, b);
   p.sc_lo = p.sc_hi = nullptr;
   p.sc_split = 0;
@@ -375,8 +505,8 @@ void ntt_evaluate(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count
     p.in = in;
     p.eb = eb;
     fill_pass(p, false, L, pl[i].first, pl[i].second, count);
-    if (i == 0) launch_pass<false, true, false, false>(s, p);
-    else launch_pass<false, false, false, true>(s, p);
+    if (i == 0) launch_pass<false, true, false, false>(s, p, pl[i].second);
+    else launch_pass<false, false, false, true>(s, p, pl[i].second);
   }
 }
 
@@ -410,9 +540,9 @@ void ntt_interpolate(hipStream_t s, uint32_t* io, size_t count, uint32_t L, bool
           return t;
         });
       }
-      launch_pass<true, false, true, false>(s, p);
+      launch_pass<true, false, true, false>(s, p, b);
     } else {
-      launch_pass<true, false, false, true>(s, p);
+      launch_pass<true, false, false, true>(s, p, pl[i].second);
     }
   }
 }

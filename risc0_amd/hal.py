@@ -13,7 +13,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libr0hip.so")
+# R0HIP_LIB selects an alternative build of the same library (tools/ experiments only)
+LIB_PATH = os.environ.get("R0HIP_LIB") or os.path.join(_HERE, "lib", "libr0hip.so")
 
 POSEIDON2, SHA256 = 0, 1
 SUITES = {"poseidon2": POSEIDON2, "sha-256": SHA256}

@@ -18,6 +18,27 @@ def main():
     which = sys.argv[1:] or ["ntt", "hash"]
     hal = r.HipHal("poseidon2")
     rng = np.random.default_rng(1)
+    if "ec" in which:
+        import json
+        circ = json.load(open(os.path.join(ROOT, "risc0_amd", "circuits", "rv32im.taps.json")))
+        po2 = 20
+        D = 4 << po2
+        gs = circ["group_sizes"]
+        groups = [hal.copy_from_elem("g", rng.integers(0, P, gs[g] * D, dtype=np.uint64).astype(np.uint32))
+                  for g in range(3)]
+        mix = hal.copy_from_elem("mix", rng.integers(0, P, circ["mix_size"], dtype=np.uint64).astype(np.uint32))
+        glob = hal.copy_from_elem("glob", rng.integers(0, P, circ["output_size"], dtype=np.uint64).astype(np.uint32))
+        out = hal.alloc_elem("check", 4 * D)
+        pm = rng.integers(0, P, 4, dtype=np.uint64).astype(np.uint32)
+        hal.eval_check("rv32im", out, groups, mix, glob, pm, po2)
+        hal.synchronize()
+        r.set_kernel_timing(True)
+        for _ in range(3):
+            hal.eval_check("rv32im", out, groups, mix, glob, pm, po2)
+        hal.synchronize()
+        for k, v in sorted(r.kernel_times().items()):
+            print(f"{os.environ.get('R0HIP_LIB', 'default')}: {k} {v[0] / v[1]:.3f} ms/launch")
+        return
     cols, po2 = 211, 20
     n = 1 << po2
     inp = hal.copy_from_elem("in", rng.integers(0, P, cols * n, dtype=np.uint64).astype(np.uint32))
@@ -32,7 +53,7 @@ def main():
             d = hal.alloc_digest("d", 4 * n)
             hal.hash_rows(d, out)
     hal.synchronize()
-    for k, (ms, calls, b) in sorted(r.kernel_times().items()):
+    for k, (ms, calls, b, _mm) in sorted(r.kernel_times().items()):
         print(f"{k:28s} {ms / calls:9.3f} ms/launch  {b / calls / 1e9:7.3f} GB alg  {b / (ms / 1e3) / 1e9:8.1f} GB/s")
 
 

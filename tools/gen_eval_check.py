@@ -209,6 +209,9 @@ def schedule(pg, budget):
     return terms, kernels
 
 
+CHUNK = int(os.environ.get("EC_CHUNK", "0"))
+
+
 def emit(circuit, outdir, budget):
     pg = Program(circuit)
     terms, kernels = schedule(pg, budget)
@@ -336,11 +339,46 @@ def emit(circuit, outdir, budget):
         L = []
         w = L.append
 
+        # Trace taps and materialised values are re-loaded where they are used instead of
+        # being kept live: the program is cut into chunks of CHUNK ops separated by a
+        # compiler memory barrier, and a load is emitted (once) in each chunk that needs
+        # it. Without this LLVM hoists all ~400 loads to the top and the kernels need
+        # 450-512 VGPR+AGPR (one wave per SIMD, exposed load latency).
+        remat = set(v for v in need if v in loaded or pg.byid[v][0] == "l") if CHUNK else set()
+        chunk = {"n": 0, "ops": 0, "have": {}}
+
+        def ref(x):
+            if x not in remat:
+                return f"v{x}"
+            h = chunk["have"]
+            if x not in h:
+                nm = f"v{x}_{chunk['n']}"
+                h[x] = nm
+                if x in loaded:
+                    kind, s_ = slot[x]
+                    if kind == "f":
+                        w(f"  const uint32_t {nm} = A.mf[uint64_t({s_}u) * A.domain + cycle];")
+                    else:
+                        w(f"  FpExt {nm}; {{ uint4 t = reinterpret_cast<const uint4*>(A.me)[uint64_t({s_}u) * A.domain"
+                          f" + cycle]; {nm} = FpExt{{{{t.x, t.y, t.z, t.w}}}}; }}")
+                else:
+                    ins = pg.byid[x]
+                    w(f"  const uint32_t {nm} = A.a[{ins[2]}][{ins[3]}u * A.domain + ((cycle - {4 * ins[4]}u) & mask)];")
+            return h[x]
+
+        def tick():
+            chunk["ops"] += 1
+            if CHUNK and chunk["ops"] >= CHUNK:
+                w("  asm volatile(\"\" ::: \"memory\");")
+                chunk["n"] += 1
+                chunk["ops"] = 0
+                chunk["have"] = {}
+
         def acc_src(x):
             """(expression, bound) of an Acc holding value x."""
             if x in lazy:
                 return f"a{x}", bound[x]
-            return f"acc_of(v{x})", CANON
+            return f"acc_of({ref(x)})", CANON
 
         def room(expr, bd, k):
             """fold expr first if adding k more products could overflow 64 bits."""
@@ -364,15 +402,70 @@ def emit(circuit, outdir, budget):
                 return f"acc_fp({expr}, {t}, A.pm, {k})", bd + PROD
             return f"acc_ext({expr}, {t}, A.pm, A.pmn, {k})", bd + 4 * PROD
 
+        # Each term is added to the running sum right after its last root is computed,
+        # so term values do not stay live to the end of the kernel.
+        acc_state = {"n": 0, "b": 0}
+        order_pos = {}
+        for n_, ins_ in enumerate(prog):
+            if ins_[0] != "r":
+                order_pos[ins_[1]] = n_
+        term_at = {}
+        for ti, (e, f) in enumerate(mine):
+            rts = [x for x in term_roots((e, f)) if x not in remat and pg.byid[x][0] not in "ceg"]
+            term_at.setdefault(max([order_pos[x] for x in rts] + [-1]), []).append(ti)
+        done_terms = set()
+
+        def pending_terms():
+            return [ti for pos in sorted(term_at) for ti in term_at[pos] if ti not in done_terms]
+
+        def emit_term(ti):
+            done_terms.add(ti)
+            e, f = mine[ti]
+            sn, sb = acc_state["n"], acc_state["b"]
+            vals = [x[1] for x in f if x[0] == "v"]
+            pms = tuple(sorted(x[1] for x in f if x[0] == "pm"))
+            if not vals and not pms:
+                src, bd = acc_src(e)
+                cur, sb2 = f"s{sn}", sb
+                if sb2 + bd >= LIM:
+                    cur, sb2 = f"acc_fold({cur})", fold_bound(sb2)
+                if sb2 + bd >= LIM:
+                    src, bd = f"acc_fold({src})", fold_bound(bd)
+                w(f"  const Acc s{sn + 1} = acc_add({cur}, {src});")
+                acc_state["n"], acc_state["b"] = sn + 1, sb2 + bd
+                return
+            expr = ref(e)
+            ety = types[e]
+            for v in vals:
+                expr = f"emul({expr}, {ref(v)})"
+                if types[v] == "e":
+                    ety = "e"
+            if not pms:
+                cur, sb2 = room(f"s{sn}", sb, 1)
+                w(f"  const Acc s{sn + 1} = acc_add({cur}, acc_of({expr}));")
+                acc_state["n"], acc_state["b"] = sn + 1, sb2 + CANON
+                return
+            if len(pms) == 1:
+                k = pms[0]
+            else:
+                if pms not in combo_index:
+                    combo_index[pms] = len(combo_index)
+                k = f"NPM + {combo_index[pms]}"
+            e2, sb = add_prod(f"s{sn}", sb, expr, ety, k)
+            w(f"  const Acc s{sn + 1} = {e2};")
+            acc_state["n"], acc_state["b"] = sn + 1, sb
+
         w(f"// GENERATED by tools/gen_eval_check.py from risc0_amd/circuits/{circuit}.poly.ir — do not edit.")
         w(common_text)
         w(f"__global__ __launch_bounds__(256) void k{ki}(Args A) {{")
         w("  const uint32_t cycle = blockIdx.x * 256u + threadIdx.x;")
         w("  if (cycle >= A.domain) return;")
         w("  const uint32_t mask = A.domain - 1;")
+        if mine or last:
+            w("  const Acc s0 = Acc{{0, 0, 0, 0}};")
         for ins in prog:
             op, i = ins[0], ins[1]
-            if i not in need or op == "r":
+            if i not in need or op == "r" or i in remat:
                 continue
             if i in loaded:
                 kind, s_ = slot[i]
@@ -382,21 +475,22 @@ def emit(circuit, outdir, budget):
                     w(f"  FpExt v{i}; {{ uint4 t = reinterpret_cast<const uint4*>(A.me)[uint64_t({s_}u) * A.domain + cycle];"
                       f" v{i} = FpExt{{{{t.x, t.y, t.z, t.w}}}}; }}")
                 continue
+            if op == "l":
+                w(f"  const uint32_t v{i} = A.a[{ins[2]}][{ins[3]}u * A.domain + ((cycle - {4 * ins[4]}u) & mask)];")
+                continue
             if op == "c":
                 w(f"  const uint32_t v{i} = {enc(ins[2])}u;")
             elif op == "e":
                 w(f"  const FpExt v{i} = FpExt{{{{{', '.join(str(enc(x)) + 'u' for x in ins[2:6])}}}}};")
-            elif op == "l":
-                w(f"  const uint32_t v{i} = A.a[{ins[2]}][{ins[3]}u * A.domain + ((cycle - {4 * ins[4]}u) & mask)];")
             elif op == "g":
                 w(f"  const uint32_t v{i} = A.a[{ins[2]}][{ins[3]}];")
             elif op in "ab":
                 src, bd = acc_src(ins[2])
                 if op == "a":
-                    t, tty, k = f"v{ins[3]}", types[ins[3]], ins[4]
+                    t, tty, k = ref(ins[3]), types[ins[3]], ins[4]
                 else:
                     T, U, k = ins[3], ins[4], ins[5]
-                    t = f"emul(v{T}, v{U})"
+                    t = f"emul({ref(T)}, {ref(U)})"
                     tty = "e" if "e" in (types[T], types[U]) else "f"
                 expr, bd = add_prod(src, bd, t, tty, k)
                 w(f"  const Acc a{i} = {expr};")
@@ -405,12 +499,13 @@ def emit(circuit, outdir, budget):
                     w(f"  const FpExt v{i} = {reduced(f'a{i}', bd)};")
             else:
                 a, b = ins[2], ins[3]
+                ra, rb = ref(a), ref(b)
                 if types[a] == "f" and types[b] == "f":
                     fn = {"+": "fp_add", "-": "fp_sub", "*": "fp_mul"}[op]
-                    w(f"  const uint32_t v{i} = {fn}(v{a}, v{b});")
+                    w(f"  const uint32_t v{i} = {fn}({ra}, {rb});")
                 else:
                     fn = {"+": "eadd", "-": "esub", "*": "emul"}[op]
-                    w(f"  const FpExt v{i} = {fn}(v{a}, v{b});")
+                    w(f"  const FpExt v{i} = {fn}({ra}, {rb});")
             if i in produced:
                 kind, s_ = slot[i]
                 if kind == "f":
@@ -418,51 +513,21 @@ def emit(circuit, outdir, budget):
                 else:
                     w(f"  reinterpret_cast<uint4*>(A.me)[uint64_t({s_}u) * A.domain + cycle] ="
                       f" make_uint4(v{i}.c[0], v{i}.c[1], v{i}.c[2], v{i}.c[3]);")
+            for ti in term_at.get(order_pos[i], []):
+                emit_term(ti)
+            if op not in "ceg":
+                tick()
         if mine or last:
+            # previous kernels' sum (if any) joins at the end; terms were added as they completed
             w("  uint4* accp = reinterpret_cast<uint4*>(A.acc) + cycle;")
-            if first:
-                w("  Acc s0 = Acc{{0, 0, 0, 0}};")
-                sb = 0
-            else:
-                w("  Acc s0; { uint4 p = *accp; s0 = acc_of(FpExt{{p.x, p.y, p.z, p.w}}); }")
-                sb = CANON
-            sn = 0
-            for e, f in mine:
-                vals = [x[1] for x in f if x[0] == "v"]
-                pms = tuple(sorted(x[1] for x in f if x[0] == "pm"))
-                if not vals and not pms:
-                    src, bd = acc_src(e)
-                    cur, sb2 = f"s{sn}", sb
-                    if sb2 + bd >= LIM:
-                        cur, sb2 = f"acc_fold({cur})", fold_bound(sb2)
-                    if sb2 + bd >= LIM:
-                        src, bd = f"acc_fold({src})", fold_bound(bd)
-                    w(f"  const Acc s{sn + 1} = acc_add({cur}, {src});")
-                    sb = sb2 + bd
-                    sn += 1
-                    continue
-                expr = f"v{e}"
-                ety = types[e]
-                for v in vals:
-                    expr = f"emul({expr}, v{v})"
-                    if types[v] == "e":
-                        ety = "e"
-                if not pms:
-                    src = f"acc_of({expr})"
-                    cur, sb2 = room(f"s{sn}", sb, 1)
-                    w(f"  const Acc s{sn + 1} = acc_add({cur}, {src});")
-                    sb = sb2 + CANON
-                    sn += 1
-                    continue
-                if len(pms) == 1:
-                    k = pms[0]
-                else:
-                    if pms not in combo_index:
-                        combo_index[pms] = len(combo_index)
-                    k = f"NPM + {combo_index[pms]}"
-                e2, sb = add_prod(f"s{sn}", sb, expr, ety, k)
-                w(f"  const Acc s{sn + 1} = {e2};")
-                sn += 1
+            for ti in pending_terms():
+                emit_term(ti)
+            sn, sb = acc_state["n"], acc_state["b"]
+            if not first:
+                w(f"  Acc s{sn + 1}; {{ uint4 p = *accp; s{sn + 1} = acc_of(FpExt{{{{p.x, p.y, p.z, p.w}}}}); }}")
+                cur, sb2 = room(f"s{sn}", sb, 1)
+                w(f"  const Acc s{sn + 2} = acc_add({cur}, s{sn + 1});")
+                sn, sb = sn + 2, sb2 + CANON
             w(f"  FpExt s = {reduced(f's{sn}', sb)};")
             if last:
                 w("  s = fe_mul_fp(s, A.vinv[cycle & 3]);")
