@@ -34,6 +34,8 @@ def parse():
     ap.add_argument("--hashfn", default="poseidon2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-po2", type=int, default=16, help="segment size of the bounded CPU baseline sample")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="segments in flight per GPU (host threads, each with its own HIP stream)")
     return ap.parse_args()
 
 
@@ -73,16 +75,35 @@ def main():
     segs = segments_for_rank(rank, world, world * args.steps)
     phase_tot = {}
     last = {}
+    import threading
+    k = max(1, min(args.inflight, len(segs) or 1))
+    # per-thread globals buffer: prove_segment zeroizes it in place; the witness
+    # groups are only read and are shared
+    globs = [dg] + [hal.copy_from_elem("global", glob) for _ in range(k - 1)]
+    lock = threading.Lock()
 
-    def prove(_seg):
-        last["seal"], _mix = r.prove_segment(hal, args.circuit, args.po2, dc, dd, da, dg, version=version)
-        for k, v in r.last_profile().items():
-            phase_tot[k] = phase_tot.get(k, 0.0) + v
+    def prove_on(slot, n):
+        for _ in range(n):
+            seal, _mix = r.prove_segment(hal, args.circuit, args.po2, dc, dd, da, globs[slot], version=version)
+            prof = r.last_profile()
+            with lock:
+                last["seal"] = seal
+                for key, v in prof.items():
+                    phase_tot[key] = phase_tot.get(key, 0.0) + v
 
-    for _ in range(args.warmup):
-        prove(None)
+    def prove_batch(batch):
+        # `batch` segments over k host threads (r0vm-style queue depth)
+        n = len(batch)
+        share = [n // k + (1 if i < n % k else 0) for i in range(k)]
+        ts = [threading.Thread(target=prove_on, args=(i, share[i])) for i in range(k) if share[i]]
+        for t_ in ts:
+            t_.start()
+        for t_ in ts:
+            t_.join()
+
+    prove_batch([None] * max(args.warmup, k))  # warm every thread's stream, pool and tables
     phase_tot.clear()
-    _t, t = timed_segments(prove, segs, 0, hal.synchronize, dist)
+    _t, t = timed_segments(prove_batch, [segs], 0, hal.synchronize, dist)
     seal = last["seal"]
     cycles_total = world * args.steps * (1 << args.po2)
     value = cycles_total / t
@@ -94,7 +115,7 @@ def main():
     if rank == 0:
         kt = kernel_roofline(r, hal, args, circ, dc, dd, da, dg, version)
         roofline = kt
-        phases = {k: round(v / args.steps, 3) for k, v in phase_tot.items()}
+        phases = {key: round(v / args.steps, 3) for key, v in phase_tot.items()}
         print(json.dumps({"phases_ms": phases, "seal_words": int(seal.size)}), file=sys.stderr)
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args, circ)
@@ -116,7 +137,8 @@ def main():
             "config": {"workload": f"{args.circuit} segment po2={args.po2}, {args.hashfn} hashfn, "
                                    "witness resident in HBM -> seal on host",
                        "circuit": args.circuit, "po2": args.po2, "hashfn": args.hashfn,
-                       "segments_per_gpu": args.steps, "parallelism": f"segment-per-gpu x{world}"},
+                       "segments_per_gpu": args.steps, "segments_in_flight_per_gpu": k,
+                       "parallelism": f"segment-per-gpu x{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

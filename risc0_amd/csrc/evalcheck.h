@@ -17,6 +17,7 @@ struct EvalCheckArgs {
   uint32_t* mat_fp;             // scratch: mat_fp x domain words
   uint32_t* mat_ext;            // scratch: mat_ext x domain FpExt
   uint32_t domain;
+  uint32_t tile = 0;            // points per tile (0 = whole domain per launch)
 };
 
 struct EvalCheckInfo {

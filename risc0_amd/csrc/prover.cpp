@@ -230,6 +230,13 @@ void run_eval_check(const CircuitDef& c, uint32_t* check, const uint32_t* const*
   e.mat_ext = static_cast<uint32_t*>(scratch(size_t(info.mat_ext) * domain * 16 + 16, 24));
   e.check = check;
   e.domain = uint32_t(domain);
+  {
+    static const uint32_t tile_env = [] {
+      const char* t = getenv("R0_EC_TILE");
+      return t ? uint32_t(strtoul(t, nullptr, 0)) : 0u;
+    }();
+    e.tile = tile_env;
+  }
   double bytes = 16.0 * domain;
   for (int g = 0; g < 3; g++) bytes += 4.0 * domain * c.group_sizes[g];
   KScope ks("eval_check", bytes, double(domain) * info.modmuls_per_point);
@@ -481,7 +488,7 @@ struct Prover {
   }
 };
 
-std::string g_last_profile;
+thread_local std::string g_last_profile;  // per host thread (segments in flight)
 
 }  // namespace
 

@@ -1,5 +1,8 @@
-// Process-wide HIP runtime state: device selection, the single ordered stream,
-// a size-keyed device-buffer pool, cached constant tables and growable scratch.
+// HIP runtime state. Process-wide: device selection and cached constant tables.
+// Per host thread: the thread's ordered stream, its size-keyed device-buffer pool,
+// growable scratch and pinned upload arena — so several host threads can each run
+// whole segment proofs concurrently on one GPU (segments in flight), and a block
+// freed on one stream is only ever reused on that same stream.
 #include "runtime.h"
 
 #include <algorithm>
@@ -16,35 +19,48 @@ namespace r0 {
 
 namespace {
 std::mutex g_mu;
-hipStream_t g_stream = nullptr;
 int g_device = -1;
+bool g_device_fixed = false;
 std::unordered_map<std::string, uint32_t*> g_tables;
+std::unordered_map<void*, size_t> g_live;  // every pooled allocation -> bytes
 struct Scratch {
   void* p = nullptr;
   size_t bytes = 0;
 };
-std::map<int, Scratch> g_scratch;
-std::multimap<size_t, void*> g_pool;  // free blocks by size
-std::unordered_map<void*, size_t> g_live;
+struct Stage {
+  uint8_t* base = nullptr;
+  size_t cap = 0, used = 0;
+};
+struct ThreadCtx {
+  hipStream_t stream = nullptr;
+  std::map<int, Scratch> scratch;
+  std::multimap<size_t, void*> pool;  // free blocks by size, last used on `stream`
+  Stage stage;
+  std::vector<uint8_t*> stage_old;
+};
+thread_local ThreadCtx t_ctx;
 }  // namespace
 
 void ensure_init() {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (g_stream) return;
-  if (g_device < 0) {
-    int n = 0;
-    HIP_OK(hipGetDeviceCount(&n));
-    R0_REQUIRE(n > 0, "no HIP device visible");
-    g_device = 0;
+  if (t_ctx.stream) return;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_device < 0) {
+      int n = 0;
+      HIP_OK(hipGetDeviceCount(&n));
+      R0_REQUIRE(n > 0, "no HIP device visible");
+      g_device = 0;
+    }
+    g_device_fixed = true;
   }
-  HIP_OK(hipSetDevice(g_device));
-  HIP_OK(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
+  HIP_OK(hipSetDevice(g_device));  // the current device is per host thread
+  HIP_OK(hipStreamCreateWithFlags(&t_ctx.stream, hipStreamNonBlocking));
 }
 
 void set_device(int ordinal) {
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    R0_REQUIRE(!g_stream || ordinal == g_device, "r0hip already initialised on another device");
+    R0_REQUIRE(!g_device_fixed || ordinal == g_device, "r0hip already initialised on another device");
     g_device = ordinal;
   }
   ensure_init();
@@ -52,7 +68,7 @@ void set_device(int ordinal) {
 
 hipStream_t stream() {
   ensure_init();
-  return g_stream;
+  return t_ctx.stream;
 }
 
 const uint32_t* dev_table(const std::string& key, const std::function<std::vector<uint32_t>()>& gen) {
@@ -78,11 +94,10 @@ const uint32_t* dev_table(const std::string& key, const std::function<std::vecto
 
 void* scratch(size_t bytes, int slot) {
   ensure_init();
-  std::lock_guard<std::mutex> lk(g_mu);
-  Scratch& s = g_scratch[slot];
+  Scratch& s = t_ctx.scratch[slot];
   if (s.bytes < bytes) {
     if (s.p) {
-      HIP_OK(hipStreamSynchronize(g_stream));  // last user of the old block must be done
+      HIP_OK(hipStreamSynchronize(t_ctx.stream));  // last user of the old block must be done
       HIP_OK(hipFree(s.p));
     }
     size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
@@ -92,43 +107,33 @@ void* scratch(size_t bytes, int slot) {
   return s.p;
 }
 
-// ---- pinned staging for async uploads ---------------------------------------
-namespace {
-struct Stage {
-  uint8_t* base = nullptr;
-  size_t cap = 0, used = 0;
-};
-Stage g_stage;
-std::vector<uint8_t*> g_stage_old;
-}  // namespace
-
+// ---- pinned staging for async uploads (per thread) ---------------------------
 void upload_async(void* d_dst, const void* h_src, size_t bytes) {
   if (!bytes) return;
   ensure_init();
-  std::lock_guard<std::mutex> lk(g_mu);
+  Stage& st = t_ctx.stage;
   size_t need = (bytes + 255) & ~size_t(255);
-  if (g_stage.used + need > g_stage.cap) {
+  if (st.used + need > st.cap) {
     // keep the old arena alive (queued copies may still read it) until stage_reset
-    if (g_stage.base) g_stage_old.push_back(g_stage.base);
+    if (st.base) t_ctx.stage_old.push_back(st.base);
     size_t cap = std::max<size_t>(size_t(64) << 20, need * 2);
     void* p = nullptr;
     HIP_OK(hipHostMalloc(&p, cap, hipHostMallocDefault));
-    g_stage.base = static_cast<uint8_t*>(p);
-    g_stage.cap = cap;
-    g_stage.used = 0;
+    st.base = static_cast<uint8_t*>(p);
+    st.cap = cap;
+    st.used = 0;
   }
-  uint8_t* h = g_stage.base + g_stage.used;
-  g_stage.used += need;
+  uint8_t* h = st.base + st.used;
+  st.used += need;
   memcpy(h, h_src, bytes);
-  HIP_OK(hipMemcpyAsync(d_dst, h, bytes, hipMemcpyHostToDevice, g_stream));
+  HIP_OK(hipMemcpyAsync(d_dst, h, bytes, hipMemcpyHostToDevice, t_ctx.stream));
 }
 
 void stage_reset() {
-  if (g_stream) HIP_OK(hipStreamSynchronize(g_stream));
-  std::lock_guard<std::mutex> lk(g_mu);
-  for (auto* p : g_stage_old) (void)hipHostFree(p);
-  g_stage_old.clear();
-  g_stage.used = 0;
+  if (t_ctx.stream) HIP_OK(hipStreamSynchronize(t_ctx.stream));
+  for (auto* p : t_ctx.stage_old) (void)hipHostFree(p);
+  t_ctx.stage_old.clear();
+  t_ctx.stage.used = 0;
 }
 
 // ---- kernel timing -----------------------------------------------------------
@@ -200,11 +205,11 @@ void* dev_alloc(size_t bytes) {
   if (bytes == 0) bytes = 16;
   bytes = (bytes + 255) & ~size_t(255);
   {
-    std::lock_guard<std::mutex> lk(g_mu);
-    auto it = g_pool.find(bytes);
-    if (it != g_pool.end()) {
+    auto it = t_ctx.pool.find(bytes);
+    if (it != t_ctx.pool.end()) {
       void* p = it->second;
-      g_pool.erase(it);
+      t_ctx.pool.erase(it);
+      std::lock_guard<std::mutex> lk(g_mu);
       g_live[p] = bytes;
       return p;
     }
@@ -223,18 +228,21 @@ void* dev_alloc(size_t bytes) {
 
 void dev_free(void* p) {
   if (!p) return;
-  std::lock_guard<std::mutex> lk(g_mu);
-  auto it = g_live.find(p);
-  if (it == g_live.end()) return;
-  g_pool.emplace(it->second, p);
-  g_live.erase(it);
+  size_t bytes;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_live.find(p);
+    if (it == g_live.end()) return;
+    bytes = it->second;
+    g_live.erase(it);
+  }
+  t_ctx.pool.emplace(bytes, p);  // reused only by this thread, i.e. on this stream
 }
 
 void dev_trim() {
-  if (g_stream) HIP_OK(hipStreamSynchronize(g_stream));
-  std::lock_guard<std::mutex> lk(g_mu);
-  for (auto& kv : g_pool) (void)hipFree(kv.second);
-  g_pool.clear();
+  if (t_ctx.stream) HIP_OK(hipStreamSynchronize(t_ctx.stream));
+  for (auto& kv : t_ctx.pool) (void)hipFree(kv.second);
+  t_ctx.pool.clear();
 }
 
 }  // namespace r0

@@ -352,3 +352,33 @@ def test_prove_segment_seal_golden(hal, hal_sha, oracle, case):
     assert seal.size == case["seal_words"]
     assert G.digest(seal) == case["seal_sha256"]
     assert [int(x) for x in mix] == case["mix"]
+
+
+def test_prove_segments_concurrently_golden(hal, hal_sha, oracle):
+    """Segments in flight: host threads, each on its own HIP stream and buffer pool,
+    prove different golden cases at once; every seal still matches its fixture."""
+    import threading
+
+    import risc0_amd as r
+    cases = G.INDEX["seals"]
+    inputs = []
+    for case in cases:
+        h = hal if case["suite"] == "poseidon2" else hal_sha
+        code, data, accum, glob = G.seal_inputs(oracle, case["circuit"], case["po2"])
+        inputs.append((h, case, [dev(h, x) for x in (code, data, accum, glob)]))
+    out = [None] * len(inputs)
+
+    def run(i):
+        h, case, (c, d, a, g) = inputs[i]
+        for _ in range(2):
+            out[i] = r.prove_segment(h, case["circuit"], case["po2"], c, d, a, g,
+                                     version=2 if case["circuit"] == "rv32im" else None)
+
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(len(inputs))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for (h, case, _), (seal, mix) in zip(inputs, out):
+        assert G.digest(seal) == case["seal_sha256"], case
+        assert [int(x) for x in mix] == case["mix"]

@@ -246,6 +246,7 @@ def emit(circuit, outdir, budget):
         "  uint32_t* mf;         // materialised Fp values, [slot][domain]",
         "  uint32_t* me;         // materialised FpExt values, [slot][domain] AoS",
         "  uint32_t domain;",
+        "  uint32_t base, count;  // this launch covers points [base, base + count)",
         "};",
         f"constexpr int NPM = {npm};",
         "__device__ __forceinline__ FpExt eadd(FpExt a, FpExt b) { return fe_add(a, b); }",
@@ -458,8 +459,8 @@ def emit(circuit, outdir, budget):
         w(f"// GENERATED by tools/gen_eval_check.py from risc0_amd/circuits/{circuit}.poly.ir — do not edit.")
         w(common_text)
         w(f"__global__ __launch_bounds__(256) void k{ki}(Args A) {{")
-        w("  const uint32_t cycle = blockIdx.x * 256u + threadIdx.x;")
-        w("  if (cycle >= A.domain) return;")
+        w("  const uint32_t cycle = A.base + blockIdx.x * 256u + threadIdx.x;")
+        w("  if (cycle >= A.base + A.count) return;")
         w("  const uint32_t mask = A.domain - 1;")
         if mine or last:
             w("  const Acc s0 = Acc{{0, 0, 0, 0}};")
@@ -540,7 +541,7 @@ def emit(circuit, outdir, budget):
             w("  reinterpret_cast<uint4*>(A.acc)[cycle] = make_uint4(0u, 0u, 0u, 0u);")
         w("}")
         w(f"void launch_k{ki}(hipStream_t s, const Args& A) {{")
-        w(f"  hipLaunchKernelGGL(k{ki}, dim3(div_up(A.domain, 256)), dim3(256), 0, s, A);")
+        w(f"  hipLaunchKernelGGL(k{ki}, dim3(div_up(A.count, 256)), dim3(256), 0, s, A);")
         w("  HIP_OK(hipGetLastError());")
         w("}")
         w(f"}}  // namespace ec_{circuit}")
@@ -574,8 +575,15 @@ def emit(circuit, outdir, budget):
     w(f"  for (int i = 0; i < {nargs}; i++) A.a[i] = e.args[i];")
     w("  A.pm = e.poly_mix; A.pmn = e.poly_mix_nb; A.acc = e.acc; A.check = e.check; A.vinv = e.vinv; A.domain = e.domain;")
     w("  A.mf = e.mat_fp; A.me = e.mat_ext;")
+    w("  // tiles of e.tile points run every kernel before the next tile, so a tile's")
+    w("  // trace columns are re-read from the Infinity Cache rather than HBM")
+    w("  const uint32_t tile = e.tile ? e.tile : e.domain;")
+    w("  for (uint32_t b = 0; b < e.domain; b += tile) {")
+    w("    A.base = b;")
+    w("    A.count = e.domain - b < tile ? e.domain - b : tile;")
     for ki in range(len(kernels)):
-        w(f"  launch_k{ki}(s, A);")
+        w(f"    launch_k{ki}(s, A);")
+    w("  }")
     w("}")
     w("}  // namespace r0")
     with open(os.path.join(outdir, f"eval_check_{circuit}.hip"), "w") as f:
