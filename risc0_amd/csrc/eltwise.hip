@@ -6,6 +6,8 @@
 // evaluate_any/poly_divide, which are integer-VALU bound.
 #include "runtime.h"
 
+#include <map>
+
 #include <algorithm>
 
 namespace r0 {
@@ -112,71 +114,88 @@ __global__ __launch_bounds__(kThreads) void mix_kernel(uint32_t* out, const uint
 }
 
 // ---- batch_evaluate_any (cpu.rs:362-393) -----------------------------------------
-// out[k] = sum_i coeffs[which[k]][i] * x_k^i. Grid (eval, chunk): each lane sums
-// 16 coefficients against precomputed x^0..x^15 (Fp x FpExt: 4 modmul/coeff);
-// lanes combine by a Horner tree with x^16, x^32, ... (8 levels); the chunk
-// partial is scaled by x^(chunk_start) and written; a second kernel adds chunks.
-constexpr int kEvPer = 16;
-constexpr int kEvChunk = kThreads * kEvPer;  // 4096 coefficients per workgroup
+// out[k] = sum_i coeffs[which[k]][i] * xs[k]^i. Evaluations of the same polynomial
+// are grouped (a trace column has one tap per `back`), so each coefficient is read
+// once per group. A workgroup takes a 16384-coefficient chunk of one polynomial; a
+// lane owns 64 consecutive coefficients and, per evaluation x, forms
+// sum_j c_j x^j as four unreduced u64 dot products against the x^j table in LDS
+// (4 v_mad_u64_u32 per coefficient, folded every 4), scales it by x^(64 lane) and
+// the block adds lanes. A last kernel combines chunks by Horner in x^16384.
+constexpr int kEvLane = 64;                     // coefficients per lane
+constexpr int kEvChunk = kThreads * kEvLane;    // 16384 per workgroup
+constexpr int kEvTab = kEvLane + kThreads + 1;  // x^0..63, x^(64 t) t < 256, x^16384
 
-__global__ __launch_bounds__(kThreads) void eval_any_kernel(const uint32_t* __restrict__ coeffs, uint32_t log_n,
-                                                           const uint32_t* __restrict__ which,
-                                                           const uint32_t* __restrict__ xs, uint32_t* partial,
-                                                           uint32_t nchunks) {
-  __shared__ FpExt xp[kEvPer + 1];  // x^0..x^16
-  __shared__ FpExt red[kThreads];
-  __shared__ FpExt ypow[9];         // x^(16 * 2^l)
-  const uint32_t k = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
+__global__ __launch_bounds__(kThreads) void eval_tables_kernel(const uint32_t* __restrict__ xs, uint32_t evals,
+                                                             uint32_t* tab) {
+  const uint64_t id = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (id >= uint64_t(evals) * kEvTab) return;
+  const uint32_t k = uint32_t(id / kEvTab), e = uint32_t(id % kEvTab);
   const FpExt x = ld_fe(xs + 4 * k);
-  if (tid == 0) {
-    FpExt cur = fe_one();
-    for (int i = 0; i <= kEvPer; i++) {
-      xp[i] = cur;
-      cur = fe_mul(cur, x);
-    }
-    FpExt y = xp[kEvPer];
-    for (int l = 0; l < 9; l++) {
-      ypow[l] = y;
-      y = fe_mul(y, y);
-    }
-  }
-  __syncthreads();
-  const uint64_t n = uint64_t(1) << log_n;
-  const uint32_t* poly = coeffs + uint64_t(which[k]) * n;
-  const uint64_t start = uint64_t(chunk) * kEvChunk + uint64_t(tid) * kEvPer;
-  FpExt acc = fe_zero();
-  if (start < n) {
+  const uint64_t pw = e < kEvLane ? e : (e < kEvLane + kThreads ? uint64_t(kEvLane) * (e - kEvLane) : kEvChunk);
+  st_fe(tab + (uint64_t(k) * kEvTab + e) * 4, fe_pow(x, pw));
+}
+
+__global__ __launch_bounds__(kThreads) void eval_chunk_kernel(const uint32_t* __restrict__ coeffs, uint64_t n,
+                                                            const uint32_t* __restrict__ gpoly,
+                                                            const uint32_t* __restrict__ gbegin,
+                                                            const uint32_t* __restrict__ geval,
+                                                            const uint32_t* __restrict__ tab, uint32_t* partial,
+                                                            uint32_t nchunks) {
+  __shared__ FpExt xp[kEvLane];
+  __shared__ FpExt red[kThreads];
+  const uint32_t g = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
+  const uint32_t* poly = coeffs + uint64_t(gpoly[g]) * n;
+  const uint64_t start = uint64_t(chunk) * kEvChunk + uint64_t(tid) * kEvLane;
+  uint32_t c[kEvLane];
+  if (start + kEvLane <= n) {
     const uint4* src = reinterpret_cast<const uint4*>(poly + start);
-    uint32_t c[kEvPer];
 #pragma unroll
-    for (int q = 0; q < kEvPer / 4; q++) {
-      uint4 v = src[q];
-      c[4 * q] = v.x; c[4 * q + 1] = v.y; c[4 * q + 2] = v.z; c[4 * q + 3] = v.w;
+    for (int q = 0; q < kEvLane / 4; q++) {
+      const uint4 v = src[q];
+      c[4 * q] = v.x;
+      c[4 * q + 1] = v.y;
+      c[4 * q + 2] = v.z;
+      c[4 * q + 3] = v.w;
     }
+  } else {
 #pragma unroll
-    for (int i = 0; i < kEvPer; i++) acc = fe_add(acc, fe_mul_fp(xp[i], c[i]));
+    for (int j = 0; j < kEvLane; j++) c[j] = start + j < n ? poly[start + j] : 0u;
   }
-  red[tid] = acc;
-  __syncthreads();
-  // tree: level l combines lanes (2m, 2m+1) as a + b * x^(16*2^l)
-  for (int l = 0, w = kThreads / 2; w >= 1; l++, w >>= 1) {
-    FpExt v = fe_zero();
-    if (tid < (uint32_t)w) v = fe_add(red[2 * tid], fe_mul(red[2 * tid + 1], ypow[l]));
+  for (uint32_t q = gbegin[g]; q < gbegin[g + 1]; q++) {
+    const uint32_t k = geval[q];
+    const uint32_t* tk = tab + uint64_t(k) * kEvTab * 4;
+    __syncthreads();  // previous evaluation's readers of xp / red are done
+    if (tid < kEvLane) xp[tid] = ld_fe(tk + 4 * tid);
     __syncthreads();
-    if (tid < (uint32_t)w) red[tid] = v;
+    uint64_t acc[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < kEvLane; j++) {
+      const FpExt w = xp[j];
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[i] += uint64_t(c[j]) * w.c[i];
+      if (j % 4 == 3) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) acc[i] = fold64(acc[i]);
+      }
+    }
+    FpExt a{{mont_reduce(acc[0]), mont_reduce(acc[1]), mont_reduce(acc[2]), mont_reduce(acc[3])}};
+    red[tid] = fe_mul(a, ld_fe(tk + 4 * (kEvLane + tid)));
     __syncthreads();
-  }
-  if (tid == 0) {
-    FpExt scale = fe_pow(x, uint64_t(chunk) * kEvChunk);
-    st_fe(partial + (uint64_t(k) * nchunks + chunk) * 4, fe_mul(red[0], scale));
+    for (uint32_t w2 = kThreads / 2; w2 >= 1; w2 >>= 1) {
+      if (tid < w2) red[tid] = fe_add(red[tid], red[tid + w2]);
+      __syncthreads();
+    }
+    if (tid == 0) st_fe(partial + (uint64_t(k) * nchunks + chunk) * 4, red[0]);
   }
 }
 
-__global__ void eval_any_reduce(const uint32_t* partial, uint32_t nchunks, uint32_t* out, uint32_t evals) {
+__global__ void eval_any_reduce(const uint32_t* partial, uint32_t nchunks, const uint32_t* tab, uint32_t* out,
+                                uint32_t evals) {
   uint32_t k = blockIdx.x * kThreads + threadIdx.x;
   if (k >= evals) return;
+  const FpExt y = ld_fe(tab + (uint64_t(k) * kEvTab + kEvTab - 1) * 4);  // x^16384
   FpExt s = fe_zero();
-  for (uint32_t c = 0; c < nchunks; c++) s = fe_add(s, ld_fe(partial + (uint64_t(k) * nchunks + c) * 4));
+  for (uint32_t c = nchunks; c-- > 0;) s = fe_add(fe_mul(s, y), ld_fe(partial + (uint64_t(k) * nchunks + c) * 4));
   st_fe(out + uint64_t(k) * 4, s);
 }
 
@@ -432,24 +451,53 @@ void mix_poly_coeffs(hipStream_t s, uint32_t* out, const uint32_t* in, const uin
   HIP_OK(hipGetLastError());
 }
 
+void batch_evaluate_any_host(hipStream_t s, const uint32_t* coeffs, size_t poly_count, uint32_t log_n,
+                             const std::vector<uint32_t>& which, const uint32_t* xs, uint32_t* out) {
+  const size_t eval_count = which.size();
+  if (!eval_count) return;
+  const uint64_t n = uint64_t(1) << log_n;
+  const uint32_t nchunks = uint32_t((n + kEvChunk - 1) / kEvChunk);
+  // group evaluations by polynomial
+  std::map<uint32_t, std::vector<uint32_t>> groups;
+  for (size_t k = 0; k < eval_count; k++) {
+    R0_REQUIRE(which[k] < poly_count, "batch_evaluate_any: which out of range");
+    groups[which[k]].push_back(uint32_t(k));
+  }
+  std::vector<uint32_t> gpoly, gbegin{0}, geval;
+  for (auto& kv : groups) {
+    gpoly.push_back(kv.first);
+    geval.insert(geval.end(), kv.second.begin(), kv.second.end());
+    gbegin.push_back(uint32_t(geval.size()));
+  }
+  // one read of each evaluated polynomial; per coefficient and evaluation 4 products
+  KScope ks("batch_evaluate_any", double(groups.size()) * n * 4, double(eval_count) * n * 4);
+  R0_REQUIRE(groups.size() < 65536, "batch_evaluate_any: too many polynomials");
+  uint32_t* d_gpoly = static_cast<uint32_t*>(scratch(gpoly.size() * 4, 9));
+  uint32_t* d_gbegin = static_cast<uint32_t*>(scratch(gbegin.size() * 4, 10));
+  uint32_t* d_geval = static_cast<uint32_t*>(scratch(geval.size() * 4, 11));
+  upload_async(d_gpoly, gpoly.data(), gpoly.size() * 4);
+  upload_async(d_gbegin, gbegin.data(), gbegin.size() * 4);
+  upload_async(d_geval, geval.data(), geval.size() * 4);
+  uint32_t* tab = static_cast<uint32_t*>(scratch(eval_count * kEvTab * 16, 12));
+  uint32_t* partial = static_cast<uint32_t*>(scratch(eval_count * nchunks * 16, 2));
+  hipLaunchKernelGGL(eval_tables_kernel, dim3(div_up(eval_count * kEvTab, kThreads)), dim3(kThreads), 0, s, xs,
+                     uint32_t(eval_count), tab);
+  HIP_OK(hipGetLastError());
+  hipLaunchKernelGGL(eval_chunk_kernel, dim3(nchunks, unsigned(groups.size())), dim3(kThreads), 0, s, coeffs, n,
+                     d_gpoly, d_gbegin, d_geval, tab, partial, nchunks);
+  HIP_OK(hipGetLastError());
+  hipLaunchKernelGGL(eval_any_reduce, dim3(div_up(eval_count, kThreads)), dim3(kThreads), 0, s, partial, nchunks,
+                     tab, out, uint32_t(eval_count));
+  HIP_OK(hipGetLastError());
+}
+
 void batch_evaluate_any(hipStream_t s, const uint32_t* coeffs, size_t poly_count, uint32_t log_n,
                         const uint32_t* which, const uint32_t* xs, uint32_t* out, size_t eval_count) {
   if (!eval_count) return;
-  (void)poly_count;
-  uint64_t n = uint64_t(1) << log_n;
-  uint32_t nchunks = uint32_t((n + kEvChunk - 1) / kEvChunk);
-  // per coefficient: FpExt power step (16) + FpExt x Fp term (4)
-  KScope ks("batch_evaluate_any", double(std::min<size_t>(poly_count, eval_count)) * n * 4,
-            double(eval_count) * n * 20);
-  R0_REQUIRE(n % kEvPer == 0, "batch_evaluate_any: poly size must be a multiple of 16");
-  R0_REQUIRE(eval_count < 65536, "batch_evaluate_any: too many evaluations");
-  uint32_t* partial = static_cast<uint32_t*>(scratch(size_t(eval_count) * nchunks * 16, 2));
-  hipLaunchKernelGGL(eval_any_kernel, dim3(nchunks, unsigned(eval_count)), dim3(kThreads), 0, s, coeffs, log_n,
-                     which, xs, partial, nchunks);
-  HIP_OK(hipGetLastError());
-  hipLaunchKernelGGL(eval_any_reduce, dim3(div_up(eval_count, kThreads)), dim3(kThreads), 0, s, partial, nchunks,
-                     out, uint32_t(eval_count));
-  HIP_OK(hipGetLastError());
+  std::vector<uint32_t> h(eval_count);
+  HIP_OK(hipMemcpyAsync(h.data(), which, eval_count * 4, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  batch_evaluate_any_host(s, coeffs, poly_count, log_n, h, xs, out);
 }
 
 void poly_divide_rows(hipStream_t s, uint32_t* io, size_t n, const std::vector<std::vector<FpExt>>& zs,

@@ -299,10 +299,9 @@ struct Prover {
       DevBuf out((total + CHECK_SIZE) * 4);
       size_t off = 0;
       for (size_t id = 0; id < 3; id++) {
-        uint32_t* dw = upload(whichs[id], 30 + int(id));
         uint32_t* dx = upload(xss[id], 33 + int(id));
-        batch_evaluate_any(s, groups[id]->coeffs.p, groups[id]->count, uint32_t(po2), dw, dx, out.p + off * 4,
-                           whichs[id].size());
+        batch_evaluate_any_host(s, groups[id]->coeffs.p, groups[id]->count, uint32_t(po2), whichs[id], dx,
+                                out.p + off * 4);
         off += whichs[id].size();
       }
       std::vector<uint32_t> h(total * 4);
@@ -324,8 +323,7 @@ struct Prover {
       for (size_t i = 0; i < CHECK_SIZE; i++) which[i] = uint32_t(i);
       std::vector<FpExt> xs(CHECK_SIZE, z_pow);
       DevBuf out(CHECK_SIZE * 4);
-      batch_evaluate_any(s, check_group.coeffs.p, CHECK_SIZE, uint32_t(po2), upload(which, 36), upload(xs, 37), out.p,
-                         CHECK_SIZE);
+      batch_evaluate_any_host(s, check_group.coeffs.p, CHECK_SIZE, uint32_t(po2), which, upload(xs, 37), out.p);
       std::vector<uint32_t> h(CHECK_SIZE * 4);
       d2h(h.data(), out.p, h.size() * 4);
       for (size_t i = 0; i < CHECK_SIZE; i++) coeff_u.push_back(fe_from_words(&h[4 * i]));

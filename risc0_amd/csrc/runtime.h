@@ -84,6 +84,9 @@ void mix_poly_coeffs(hipStream_t s, uint32_t* out, const uint32_t* in, const uin
                      size_t input_size, size_t count);
 void batch_evaluate_any(hipStream_t s, const uint32_t* coeffs, size_t poly_count, uint32_t log_n,
                         const uint32_t* which, const uint32_t* xs, uint32_t* out, size_t eval_count);
+// the same with `which` on the host (groups evaluations by polynomial without a D2H)
+void batch_evaluate_any_host(hipStream_t s, const uint32_t* coeffs, size_t poly_count, uint32_t log_n,
+                             const std::vector<uint32_t>& which, const uint32_t* xs, uint32_t* out);
 void scatter(hipStream_t s, uint32_t* into, const uint32_t* index, const uint32_t* offsets,
              const uint32_t* values, size_t cycles);
 void copy_elem_slice(hipStream_t s, uint32_t* into, const uint32_t* from, size_t rows, size_t cols,
