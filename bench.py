@@ -34,8 +34,9 @@ def parse():
     ap.add_argument("--hashfn", default="poseidon2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-po2", type=int, default=16, help="segment size of the bounded CPU baseline sample")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="segments in flight per GPU (host threads, each with its own HIP stream)")
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="segments in flight per GPU (host threads, each with its own HIP stream); "
+                         "default 2, or 1 above po2=22 where one segment needs ~150 GB of HBM")
     return ap.parse_args()
 
 
@@ -76,7 +77,8 @@ def main():
     phase_tot = {}
     last = {}
     import threading
-    k = max(1, min(args.inflight, len(segs) or 1))
+    inflight = args.inflight if args.inflight is not None else (2 if args.po2 <= 22 else 1)
+    k = max(1, min(inflight, len(segs) or 1))
     # per-thread globals buffer: prove_segment zeroizes it in place; the witness
     # groups are only read and are shared
     globs = [dg] + [hal.copy_from_elem("global", glob) for _ in range(k - 1)]
@@ -122,7 +124,7 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "RISC-V cycles proved/sec at segment po2=20",
+            "metric": f"RISC-V cycles proved/sec at segment po2={args.po2}",
             "value": round(value, 1),
             "unit": "cycles/s",
             "n_gpus": world,

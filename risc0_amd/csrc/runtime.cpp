@@ -11,6 +11,7 @@
 #include <map>
 #include <tuple>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 
 #include "devmem.h"
@@ -31,12 +32,33 @@ struct Stage {
   uint8_t* base = nullptr;
   size_t cap = 0, used = 0;
 };
+// blocks left by exited threads (their stream was drained), reusable by anyone
+std::multimap<size_t, void*> g_orphans;
+std::thread::id g_main_thread;
+
 struct ThreadCtx {
   hipStream_t stream = nullptr;
   std::map<int, Scratch> scratch;
   std::multimap<size_t, void*> pool;  // free blocks by size, last used on `stream`
   Stage stage;
   std::vector<uint8_t*> stage_old;
+  ~ThreadCtx() {
+    // A worker thread hands its memory over when it exits. The main thread's context
+    // dies during process teardown, when the HIP runtime may already be gone.
+    if (!stream || std::this_thread::get_id() == g_main_thread) return;
+    (void)hipStreamSynchronize(stream);
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      for (auto& kv : pool) g_orphans.emplace(kv.first, kv.second);
+      for (auto& kv : scratch)
+        if (kv.second.p) g_orphans.emplace(kv.second.bytes, kv.second.p);
+    }
+    pool.clear();
+    scratch.clear();
+    for (auto* p : stage_old) (void)hipHostFree(p);
+    if (stage.base) (void)hipHostFree(stage.base);
+    (void)hipStreamDestroy(stream);
+  }
 };
 thread_local ThreadCtx t_ctx;
 }  // namespace
@@ -51,6 +73,7 @@ void ensure_init() {
       R0_REQUIRE(n > 0, "no HIP device visible");
       g_device = 0;
     }
+    if (!g_device_fixed) g_main_thread = std::this_thread::get_id();
     g_device_fixed = true;
   }
   HIP_OK(hipSetDevice(g_device));  // the current device is per host thread
@@ -213,6 +236,14 @@ void* dev_alloc(size_t bytes) {
       g_live[p] = bytes;
       return p;
     }
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto ot = g_orphans.lower_bound(bytes);  // exact or up to 25% larger
+    if (ot != g_orphans.end() && ot->first <= bytes + bytes / 4) {
+      void* p = ot->second;
+      g_live[p] = ot->first;
+      g_orphans.erase(ot);
+      return p;
+    }
   }
   void* p = nullptr;
   hipError_t e = hipMalloc(&p, bytes);
@@ -243,6 +274,9 @@ void dev_trim() {
   if (t_ctx.stream) HIP_OK(hipStreamSynchronize(t_ctx.stream));
   for (auto& kv : t_ctx.pool) (void)hipFree(kv.second);
   t_ctx.pool.clear();
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (auto& kv : g_orphans) (void)hipFree(kv.second);
+  g_orphans.clear();
 }
 
 }  // namespace r0
