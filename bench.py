@@ -171,14 +171,35 @@ def kernel_roofline(r, hal, args, circ, dc, dd, da, dg, version):
     avg_s = ms / 1000.0 / calls
     per_launch = alg_bytes / calls
     achieved = per_launch / avg_s / 1e9
+    traffic, src = pmc_traffic(name, calls, args)
     out = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None, "alg_bytes_per_launch": int(per_launch),
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "alg_bytes_per_launch": int(per_launch),
            "avg_launch_ms": round(avg_s * 1000, 4)}
+    if src:
+        out["traffic_source"] = src
     if alg_mm:
         mm = alg_mm / calls / avg_s
         out["valu"] = {"achieved": round(mm / 1e12, 3), "peak": MODMUL_PEAK / 1e12, "unit": "T modmul-equiv/s",
                        "frac": round(mm / MODMUL_PEAK, 4), "modmuls_per_launch": int(alg_mm / calls)}
     return out
+
+
+def pmc_traffic(family, calls, args):
+    """HBM bytes per launch of `family` from the newest committed rocprofv3 PMC summary
+    (profiles/r*_pmc_traffic.json, FETCH_SIZE/WRITE_SIZE passes of this same bench
+    command, gfx950-corrected by tools/pmc_traffic.py). PMC counters cannot be read from
+    inside the timed process, so the value is the committed measurement, labelled."""
+    import glob
+    if args.circuit != "rv32im" or args.po2 != 20 or args.hashfn != "poseidon2":
+        return None, None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)["per_proof"].get(family)
+    if not d:
+        return None, None
+    return int((d["read_bytes"] + d["write_bytes"]) / calls), os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(args, circ):

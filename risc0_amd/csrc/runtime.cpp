@@ -35,6 +35,8 @@ struct Stage {
 // blocks left by exited threads (their stream was drained), reusable by anyone
 std::multimap<size_t, void*> g_orphans;
 std::thread::id g_main_thread;
+std::vector<hipStream_t> g_free_streams;  // streams of exited threads (drained)
+std::vector<Stage> g_free_stages;         // their pinned upload arenas
 
 struct ThreadCtx {
   hipStream_t stream = nullptr;
@@ -43,21 +45,20 @@ struct ThreadCtx {
   Stage stage;
   std::vector<uint8_t*> stage_old;
   ~ThreadCtx() {
-    // A worker thread hands its memory over when it exits. The main thread's context
-    // dies during process teardown, when the HIP runtime may already be gone.
+    // A worker thread hands its stream and memory over when it exits — no HIP calls
+    // here (thread-exit destructors run after tools' per-thread state is gone). Every
+    // API call drains its stream before returning, so the blocks are idle. The main
+    // thread's context dies in process teardown and is left alone.
     if (!stream || std::this_thread::get_id() == g_main_thread) return;
-    (void)hipStreamSynchronize(stream);
-    {
-      std::lock_guard<std::mutex> lk(g_mu);
-      for (auto& kv : pool) g_orphans.emplace(kv.first, kv.second);
-      for (auto& kv : scratch)
-        if (kv.second.p) g_orphans.emplace(kv.second.bytes, kv.second.p);
-    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (auto& kv : pool) g_orphans.emplace(kv.first, kv.second);
+    for (auto& kv : scratch)
+      if (kv.second.p) g_orphans.emplace(kv.second.bytes, kv.second.p);
+    g_free_streams.push_back(stream);
+    if (stage.base) g_free_stages.push_back(Stage{stage.base, stage.cap, 0});
+    // superseded arenas in stage_old are left allocated (rare: only after growth)
     pool.clear();
     scratch.clear();
-    for (auto* p : stage_old) (void)hipHostFree(p);
-    if (stage.base) (void)hipHostFree(stage.base);
-    (void)hipStreamDestroy(stream);
   }
 };
 thread_local ThreadCtx t_ctx;
@@ -77,7 +78,18 @@ void ensure_init() {
     g_device_fixed = true;
   }
   HIP_OK(hipSetDevice(g_device));  // the current device is per host thread
-  HIP_OK(hipStreamCreateWithFlags(&t_ctx.stream, hipStreamNonBlocking));
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_free_streams.empty()) {
+      t_ctx.stream = g_free_streams.back();
+      g_free_streams.pop_back();
+    }
+    if (!g_free_stages.empty()) {
+      t_ctx.stage = g_free_stages.back();
+      g_free_stages.pop_back();
+    }
+  }
+  if (!t_ctx.stream) HIP_OK(hipStreamCreateWithFlags(&t_ctx.stream, hipStreamNonBlocking));
 }
 
 void set_device(int ordinal) {

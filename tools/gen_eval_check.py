@@ -210,6 +210,8 @@ def schedule(pg, budget):
 
 
 CHUNK = int(os.environ.get("EC_CHUNK", "0"))
+# minimum waves per SIMD requested from the register allocator (1 = no limit)
+WAVES = int(os.environ.get("EC_WAVES", "1"))
 
 
 def emit(circuit, outdir, budget):
@@ -458,7 +460,8 @@ def emit(circuit, outdir, budget):
 
         w(f"// GENERATED by tools/gen_eval_check.py from risc0_amd/circuits/{circuit}.poly.ir — do not edit.")
         w(common_text)
-        w(f"__global__ __launch_bounds__(256) void k{ki}(Args A) {{")
+        lb = "256" if WAVES <= 1 else f"256, {WAVES}"
+        w(f"__global__ __launch_bounds__({lb}) void k{ki}(Args A) {{")
         w("  const uint32_t cycle = A.base + blockIdx.x * 256u + threadIdx.x;")
         w("  if (cycle >= A.base + A.count) return;")
         w("  const uint32_t mask = A.domain - 1;")

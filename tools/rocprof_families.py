@@ -16,7 +16,7 @@ FAMILIES = [
     (r"ntt_pass_kernel<false", "ntt_evaluate"),
     (r"ntt_pass_kernel<true", "ntt_interpolate"),
     (r"bit_reverse", "bit_reverse"),
-    (r"eval_any", "batch_evaluate_any"),
+    (r"eval_any|eval_chunk|eval_tables", "batch_evaluate_any"),
     (r"mix_kernel", "mix_poly_coeffs"),
     (r"div_", "poly_divide"),
 ]
