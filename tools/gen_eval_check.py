@@ -130,6 +130,32 @@ def modmuls(pg):
     return n
 
 
+def dfs_order(pg, need, roots, leaves):
+    """Post-order over `need` from `roots`: an accumulate op visits its running sum
+    first, so each term value is computed just before it is added. `leaves` (loads,
+    constants, materialised values) are placed separately by the caller."""
+    out, seen = [], set()
+    for r in roots:
+        if r in seen or r not in need:
+            continue
+        stack = [(r, False)]
+        while stack:
+            v, done = stack.pop()
+            if done:
+                out.append(v)
+                continue
+            if v in seen:
+                continue
+            seen.add(v)
+            stack.append((v, True))
+            if v in leaves:
+                continue
+            ds = [d for d in deps(pg.byid[v]) if d in need and d not in seen]
+            for d in reversed(ds):  # first dep (the running sum) is visited first
+                stack.append((d, False))
+    return out
+
+
 def term_roots(t):
     return [t[0]] + [x[1] for x in t[1] if x[0] == "v"]
 
@@ -210,6 +236,10 @@ def schedule(pg, budget):
 
 
 CHUNK = int(os.environ.get("EC_CHUNK", "0"))
+# emission order: "ir" (the reference program's order) or "dfs" (each value computed
+# right before its first use, accumulation chains first; loads hoisted EC_PF ops ahead)
+ORDER = os.environ.get("EC_ORDER", "dfs")
+PF = int(os.environ.get("EC_PF", "512"))
 # minimum waves per SIMD requested from the register allocator (1 = no limit)
 WAVES = int(os.environ.get("EC_WAVES", "1"))
 
@@ -408,10 +438,32 @@ def emit(circuit, outdir, budget):
         # Each term is added to the running sum right after its last root is computed,
         # so term values do not stay live to the end of the kernel.
         acc_state = {"n": 0, "b": 0}
+        if ORDER == "dfs":
+            byid_ = pg.byid
+            leaves = set(v for v in need if v in loaded or byid_[v][0] in "clge")
+            oroots = sorted(set(roots), key=lambda v: pg.order[v])
+            body = [v for v in dfs_order(pg, need, oroots, leaves) if v not in leaves]
+            first_use = {}
+            for n_, v in enumerate(body):
+                for d in deps(byid_[v]):
+                    if d in leaves and d not in first_use:
+                        first_use[d] = n_
+            consts = [v for v in leaves if byid_[v][0] in "ceg"]
+            slots = {}
+            for v in leaves:
+                if byid_[v][0] in "ceg":
+                    continue
+                slots.setdefault(max(0, first_use.get(v, 0) - PF), []).append(v)
+            seq = sorted(consts, key=lambda v: pg.order[v])
+            for n_, v in enumerate(body):
+                seq += sorted(slots.get(n_, []), key=lambda v: pg.order[v])
+                seq.append(v)
+            kprog = [byid_[v] for v in seq]
+        else:
+            kprog = [ins_ for ins_ in prog if ins_[0] != "r"]
         order_pos = {}
-        for n_, ins_ in enumerate(prog):
-            if ins_[0] != "r":
-                order_pos[ins_[1]] = n_
+        for n_, ins_ in enumerate(kprog):
+            order_pos[ins_[1]] = n_
         term_at = {}
         for ti, (e, f) in enumerate(mine):
             rts = [x for x in term_roots((e, f)) if x not in remat and pg.byid[x][0] not in "ceg"]
@@ -467,7 +519,7 @@ def emit(circuit, outdir, budget):
         w("  const uint32_t mask = A.domain - 1;")
         if mine or last:
             w("  const Acc s0 = Acc{{0, 0, 0, 0}};")
-        for ins in prog:
+        for ins in kprog:
             op, i = ins[0], ins[1]
             if i not in need or op == "r" or i in remat:
                 continue
