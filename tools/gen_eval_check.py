@@ -241,12 +241,28 @@ CHUNK = int(os.environ.get("EC_CHUNK", "0"))
 ORDER = os.environ.get("EC_ORDER", "dfs")
 PF = int(os.environ.get("EC_PF", "512"))
 # minimum waves per SIMD requested from the register allocator (1 = no limit)
-WAVES = int(os.environ.get("EC_WAVES", "1"))
+WAVES = int(os.environ.get("EC_WAVES", "2"))
+
+
+def kernel_config(circuit, budget):
+    """Per-kernel (waves, prefetch) chosen by tools/tune_eval_check.py on an MI355X and
+    committed as risc0_amd/circuits/<circuit>.ectune.json; EC_WAVES/EC_PF (if set) or
+    the defaults apply to kernels it does not list (or when EC_NOTUNE is set)."""
+    path = os.path.join(ROOT, "risc0_amd", "circuits", circuit + ".ectune.json")
+    if os.environ.get("EC_NOTUNE") or "EC_WAVES" in os.environ or "EC_PF" in os.environ or not os.path.exists(path):
+        return {}
+    import json
+    with open(path) as f:
+        t = json.load(f)
+    if t.get("budget") != budget or t.get("order") != ORDER:
+        return {}
+    return {int(k): v for k, v in t["kernels"].items()}
 
 
 def emit(circuit, outdir, budget):
     pg = Program(circuit)
     terms, kernels = schedule(pg, budget)
+    tune = kernel_config(circuit, budget)
     prog, types = pg.prog, pg.types
     nargs = 1 + max(ins[2] for ins in prog if ins[0] in ("l", "g"))
     npm = max([ins[4] for ins in prog if ins[0] == "a"] + [ins[5] for ins in prog if ins[0] == "b"]) + 1
@@ -438,6 +454,8 @@ def emit(circuit, outdir, budget):
         # Each term is added to the running sum right after its last root is computed,
         # so term values do not stay live to the end of the kernel.
         acc_state = {"n": 0, "b": 0}
+        kwaves = tune.get(ki, {}).get("waves", WAVES)
+        kpf = tune.get(ki, {}).get("pf", PF)
         if ORDER == "dfs":
             byid_ = pg.byid
             leaves = set(v for v in need if v in loaded or byid_[v][0] in "clge")
@@ -453,7 +471,7 @@ def emit(circuit, outdir, budget):
             for v in leaves:
                 if byid_[v][0] in "ceg":
                     continue
-                slots.setdefault(max(0, first_use.get(v, 0) - PF), []).append(v)
+                slots.setdefault(max(0, first_use.get(v, 0) - kpf), []).append(v)
             seq = sorted(consts, key=lambda v: pg.order[v])
             for n_, v in enumerate(body):
                 seq += sorted(slots.get(n_, []), key=lambda v: pg.order[v])
@@ -512,7 +530,7 @@ def emit(circuit, outdir, budget):
 
         w(f"// GENERATED by tools/gen_eval_check.py from risc0_amd/circuits/{circuit}.poly.ir — do not edit.")
         w(common_text)
-        lb = "256" if WAVES <= 1 else f"256, {WAVES}"
+        lb = "256" if kwaves <= 1 else f"256, {kwaves}"
         w(f"__global__ __launch_bounds__({lb}) void k{ki}(Args A) {{")
         w("  const uint32_t cycle = A.base + blockIdx.x * 256u + threadIdx.x;")
         w("  if (cycle >= A.base + A.count) return;")
