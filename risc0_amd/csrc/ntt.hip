@@ -162,19 +162,20 @@ __device__ __forceinline__ void stages(uint32_t* lds, const uint32_t* tw, const 
 }
 
 
-// Column passes (C = 5, B >= 3): lane (j = tid & 31, t0 = tid >> 5) owns rows
-// t = 8i + t0, so rev_B(t) = rev_3(t0)*2^(B-3) + rev_{B-3}(i) and its twiddles are
-// base * c^k, k = rev_{B-3}(i) < E, with c = w_{2^(a+B)}^(low0+j) and
-// base = c^(rev_3(t0)*2^(B-3)): E running products (8 independent chains) replace
-// two table loads and a multiply per element.
-template <int B>
+// Column passes (2^C columns, B >= 8 - C): lane (j = tid mod 2^C, t0 = tid >> C)
+// owns rows t = R*i + t0 with R = 256 >> C, so rev_B(t) = rev_r(t0)*2^(B-r) +
+// rev_{B-r}(i) (r = log R) and its twiddles are base * c^k, k = rev_{B-r}(i) < E, with
+// c = w_{2^(a+B)}^(low0+j) and base = c^(rev_r(t0)*2^(B-r)): E running products
+// (8 independent chains) replace two table loads and a multiply per element.
+template <int B, int C>
 struct ColTwiddles {
-  static constexpr uint32_t E = 1u << (B - 3);
+  static constexpr uint32_t LR = 8 - C;  // log2 rows per i
+  static constexpr uint32_t E = 1u << (B - LR);
   uint32_t pw[E];
   __device__ __forceinline__ void init(const PassArgs& p, uint32_t ex, uint32_t t0) {
     const uint32_t c = fp_mul(p.sc_hi[ex >> p.sc_split], p.sc_lo[ex & ((1u << p.sc_split) - 1)]);
     constexpr uint32_t S = E < 8 ? E : 8;
-    pw[0] = fp_pow(c, uint64_t(bitrev_n(t0, 3)) << (B - 3));
+    pw[0] = fp_pow(c, uint64_t(bitrev_n(t0, LR)) << (B - LR));
 #pragma unroll
     for (uint32_t k = 1; k < S; k++) pw[k] = fp_mul(pw[k - 1], c);
     uint32_t step = c;
@@ -183,8 +184,19 @@ struct ColTwiddles {
 #pragma unroll
     for (uint32_t k = S; k < E; k++) pw[k] = fp_mul(pw[k - S], step);
   }
-  __device__ __forceinline__ uint32_t at(uint32_t i) const { return pw[bitrev_n(i, B - 3)]; }
+  __device__ __forceinline__ uint32_t at(uint32_t i) const { return pw[bitrev_n(i, B - LR)]; }
 };
+
+// Column passes with 2^C < 32 columns cover half an L2 line per workgroup. Consecutive
+// block ids land on consecutive XCDs, so the block -> column-group map pairs blocks
+// b and b+8 (same XCD, dispatched together) on the two halves of each 128-B line.
+template <int C>
+__device__ __forceinline__ uint64_t col_block(uint64_t b) {
+  if constexpr (C >= 5) return b;
+  constexpr uint64_t H = uint64_t(1) << (C < 5 ? 5 - C : 0);  // workgroups per 128-B line
+  const uint64_t grp = b / (8 * H), r = b % (8 * H);
+  return grp * (8 * H) + (r % 8) * H + r / 8;
+}
 
 template <bool INV, bool EXPAND, bool LAST, bool COLS, int B, int C, int EB>
 __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
@@ -193,7 +205,7 @@ __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
   const uint32_t tid = threadIdx.x;
   constexpr uint32_t nb = 1u << B;
   constexpr uint32_t total = nb << C;
-  const uint64_t wg = blockIdx.x;
+  const uint64_t wg = COLS ? col_block<C>(blockIdx.x) : uint64_t(blockIdx.x);
   // stage twiddles -> LDS (entries 1 .. 2^B - 1)
 #pragma unroll
   for (uint32_t i = 0; i < (nb + kThreads - 1) / kThreads; i++) {
@@ -238,7 +250,7 @@ __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
         }
       } else compact[q] = r[i];
     }
-  } else if constexpr (B < 3) {
+  } else if constexpr (B < 8 - C) {
     // tiny column passes: plain mapping, table twiddles
     constexpr uint32_t E = (total + kThreads - 1) / kThreads;
 #pragma unroll
@@ -258,32 +270,34 @@ __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
     // rev_B(t) = u = r0*E + i, i < E, so its forward pre-scale factors
     // w_{2^(a+B)}^{(low0+j)*u} are one running product (c^i) — no table loads.
     constexpr uint32_t E = total / kThreads;
+    constexpr uint32_t R = kThreads >> C;  // rows per i
     const uint32_t j = tid & ((1u << C) - 1), t0 = tid >> C;
     uint32_t r[E];
 #pragma unroll
     for (uint32_t i = 0; i < E; i++)
-      r[i] = p.out[(g_hi << (p.a + B)) + (uint64_t(8 * i + t0) << p.a) + low0 + j];
+      r[i] = p.out[(g_hi << (p.a + B)) + (uint64_t(R * i + t0) << p.a) + low0 + j];
     if (!INV) {
-      ColTwiddles<B> tf;
+      ColTwiddles<B, C> tf;
       tf.init(p, low0 + j, t0);
 #pragma unroll
       for (uint32_t i = 0; i < E; i++) r[i] = fp_mul(r[i], tf.at(i));
     }
 #pragma unroll
-    for (uint32_t i = 0; i < E; i++) lds[lidx<COLS, B, C>(j, 8 * i + t0)] = r[i];
+    for (uint32_t i = 0; i < E; i++) lds[lidx<COLS, B, C>(j, R * i + t0)] = r[i];
   }
   __syncthreads();
   if (!INV) stages<false, COLS, B, C, (EB < B ? EB : 0)>(lds, tw, compact);
   else stages<true, COLS, B, C>(lds, tw);
   // ---- store (inverse column passes post-scale; last inverse pass normalises) ----
-  if constexpr (COLS && B >= 3) {
+  if constexpr (COLS && B >= 8 - C) {
     constexpr uint32_t E = total / kThreads;
+    constexpr uint32_t R = kThreads >> C;
     const uint32_t j = tid & ((1u << C) - 1), t0 = tid >> C;
-    ColTwiddles<B> tf;
+    ColTwiddles<B, C> tf;
     if (INV) tf.init(p, low0 + j, t0);
 #pragma unroll
     for (uint32_t i = 0; i < E; i++) {
-      const uint32_t t = 8 * i + t0;
+      const uint32_t t = R * i + t0;
       uint32_t v = lds[lidx<COLS, B, C>(j, t)];
       if (INV) v = fp_mul(v, tf.at(i));
       p.out[(g_hi << (p.a + B)) + (uint64_t(t) << p.a) + low0 + j] = v;
@@ -427,13 +441,19 @@ std::vector<std::pair<uint32_t, uint32_t>> plan(uint32_t L) {
   return v;
 }
 
+// columns per workgroup of a column pass (log2): 16 columns (32 KiB of LDS at B = 9,
+// four workgroups per CU; see col_block for the L2-line pairing) for the deep passes,
+// 32 columns below B = 8 where LDS does not limit occupancy (measured: B = 9 forward
+// 3.47 -> 2.32 ms with 16 columns; B = 7 inverse 0.45 -> 0.52 ms, so it keeps 32)
+constexpr int col_c(int B) { return B >= 8 ? 4 : 5; }
+
 // rows per workgroup of a row pass: enough rows that a workgroup holds >= 2048 words
 constexpr int row_c(int B) { return B >= 11 ? 0 : 11 - B; }
 
 template <bool INV, bool EXPAND, bool LAST, bool COLS, int B, int EB>
 void launch_pass_be(hipStream_t s, const PassArgs& p) {
-  constexpr int C = COLS ? 5 : row_c(B);
-  if (COLS) R0_REQUIRE(p.a >= uint32_t(C), "column pass needs >= 32 columns");
+  constexpr int C = COLS ? col_c(B) : row_c(B);
+  if (COLS) R0_REQUIRE(p.a >= 5, "column pass needs >= 32 columns");
   const size_t lds =
       4 * (size_t(lds_words<COLS, B, C>()) + (size_t(1) << B) + (EB > 0 && EB < B ? (size_t(1) << (B + C - EB)) : 0));
   uint64_t nwg = COLS ? (p.groups >> C) : ((p.groups + (uint64_t(1) << C) - 1) >> C);
