@@ -140,16 +140,23 @@ R0_HD void poseidon2_mix(uint32_t* c) {
 #pragma unroll
   for (int i = 0; i < 24; i++) c[i] = p2_red39(y[i]);
 #pragma unroll
+  // Partial rounds keep every cell lazy in [0, 2p): with cells c < X the M_INT output
+  // REDC(c*d + sf) < 0.469 X + sf/2^32 + p, whose fixed point (sf < 2^57 + 2^32 after
+  // two folds) is 3.86e9 < 2p < 2^32, so nothing is canonicalised until the end. The
+  // sum is two 12-term halves (12 * 2p * (2^32 mod p) < 2^64).
   for (int r = 0; r < 21; r++) {
-    c[0] = p2_sbox_lazy(fp_add(c[0], kP2Partial[r]));
-    c[0] = umin(c[0], c[0] - kP);
-    uint64_t sf = 0;
+    c[0] = p2_sbox_lazy(fp_add(umin(c[0], c[0] - kP), kP2Partial[r]));
+    uint64_t s0 = 0, s1 = 0;
 #pragma unroll
-    for (int i = 0; i < 24; i++) sf += uint64_t(c[i]) * kFoldC;
-    sf = fold64(sf);
+    for (int i = 0; i < 12; i++) s0 += uint64_t(c[i]) * kFoldC;
 #pragma unroll
-    for (int i = 0; i < 24; i++) c[i] = mont_reduce(uint64_t(c[i]) * kP2Diag[i] + sf);
+    for (int i = 12; i < 24; i++) s1 += uint64_t(c[i]) * kFoldC;
+    const uint64_t sf = fold64(fold64(s0) + fold64(s1));
+#pragma unroll
+    for (int i = 0; i < 24; i++) c[i] = mont_lazy(uint64_t(c[i]) * kP2Diag[i] + sf);
   }
+#pragma unroll
+  for (int i = 0; i < 24; i++) c[i] = umin(c[i], c[i] - kP);
 #pragma unroll
   for (int r = 4; r < 8; r++) {
 #pragma unroll
