@@ -23,7 +23,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "risc0_amd", "csrc")
 VAR = os.path.join(ROOT, "risc0_amd", "lib_variants")
 OUT = os.path.join(ROOT, "gpurun_out", "tune")
-GRID = [(w, pf) for w in (1, 2) for pf in (256, 512, 768)]
+GRID = [(w, pf) for w in (1, 2) for pf in (128, 256, 384, 512, 640, 768, 1024)]
 BUDGET = 4000
 
 
