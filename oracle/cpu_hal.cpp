@@ -279,6 +279,10 @@ void oracle_rng_free(void* r) { delete static_cast<Rng*>(r); }
 void oracle_rng_mix(void* r, const uint32_t* d) { static_cast<Rng*>(r)->mix(*reinterpret_cast<const Digest*>(d)); }
 uint32_t oracle_rng_random_bits(void* r, size_t bits) { return static_cast<Rng*>(r)->random_bits(bits); }
 uint32_t oracle_rng_random_elem(void* r) { return static_cast<Rng*>(r)->random_elem().v; }
+void oracle_rng_random_ext_elem(void* r, uint32_t* out) {
+  ExtElem e = static_cast<Rng*>(r)->random_ext_elem();
+  for (int i = 0; i < 4; i++) out[i] = e.e[i].v;
+}
 size_t oracle_num_threads() { return num_threads(); }
 
 }  // extern "C"

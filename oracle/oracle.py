@@ -47,6 +47,8 @@ def lib():
                                                          [C.c_size_t] if f == "oracle_rng_random_bits" else [])
         _lib.oracle_rng_random_bits.restype = C.c_uint32
         _lib.oracle_rng_random_elem.restype = C.c_uint32
+        _lib.oracle_rng_random_ext_elem.argtypes = [C.c_void_p, u32p]
+        _lib.oracle_rng_random_ext_elem.restype = None
         _lib.oracle_encode.restype = C.c_uint32
         _lib.oracle_decode.restype = C.c_uint32
         _lib.oracle_elem_pow.restype = C.c_uint32
@@ -232,6 +234,11 @@ class Rng:
 
     def random_elem(self):
         return lib().oracle_rng_random_elem(self.h)
+
+    def random_ext_elem(self):
+        out = np.zeros(4, np.uint32)
+        lib().oracle_rng_random_ext_elem(self.h, ptr(out))
+        return out
 
 
 # ---------------------------------------------------------------------------

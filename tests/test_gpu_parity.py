@@ -382,3 +382,29 @@ def test_prove_segments_concurrently_golden(hal, hal_sha, oracle):
     for (h, case, _), (seal, mix) in zip(inputs, out):
         assert G.digest(seal) == case["seal_sha256"], case
         assert [int(x) for x in mix] == case["mix"]
+
+
+@pytest.mark.parametrize("circuit,suite,po2", [("rv32im", "poseidon2", 20), ("rv32im", "poseidon2", 16),
+                                               ("recursion", "sha-256", 18)])
+def test_full_size_seal_verifies(hal, hal_sha, oracle, circuit, suite, po2):
+    """At BASELINE sizes the CPU oracle cannot prove, the HIP seal passes the reference
+    verifier's checks (tests/verifier.py: transcript, all Merkle openings, DEEP-ALI
+    combination, every FRI fold and the final polynomial); flipped bits are rejected."""
+    import risc0_amd as r
+    import verifier
+    h = hal if suite == "poseidon2" else hal_sha
+    s = oracle.POSEIDON2 if suite == "poseidon2" else oracle.SHA256
+    d = oracle.load_circuit_json(circuit)
+    rng = np.random.default_rng(0x5249534330 + po2)
+    n = 1 << po2
+    gs = d["group_sizes"]
+    bufs = [dev(h, oracle.rand_elems(rng, gs[g] * n)) for g in (1, 2, 0)]
+    glob = dev(h, oracle.rand_elems(rng, d["output_size"]))
+    seal, _mix = r.prove_segment(h, circuit, po2, *bufs, glob, version=2 if circuit == "rv32im" else None)
+    res = verifier.verify(oracle, circuit, seal, s)
+    assert res["po2"] == po2
+    for where in (seal.size // 3, seal.size - 5):
+        bad = seal.copy()
+        bad[where] ^= np.uint32(1 << 9)
+        with pytest.raises(verifier.VerificationError):
+            verifier.verify(oracle, circuit, bad, s)
