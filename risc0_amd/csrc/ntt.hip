@@ -30,7 +30,7 @@ constexpr int kThreads = 256;
 
 struct PassArgs {
   uint32_t* out;
-  const uint32_t* in;       // expand source (first forward pass) or == out
+  const uint32_t* in;       // source: the caller's buffer for the first pass, == out after
   const uint32_t* local_tw; // [2^(s-1) + k] = w_{2^s}^k, s = 1..B (fwd or rev roots)
   const uint32_t* sc_lo;    // w_{2^(a+B)}^e = sc_hi[e >> sc_split] * sc_lo[e & mask]
   const uint32_t* sc_hi;
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
     // stands for 2^EB replicated slots, which the first stage group reads in place)
     constexpr uint32_t NIN = total >> EB;
     constexpr uint32_t EIN = (NIN + kThreads - 1) / kThreads;
-    const uint32_t* src = EXPAND ? p.in : p.out;
+    const uint32_t* src = p.in;
     const uint64_t base = wg << (B + C - EB);
     const uint64_t limit = p.groups << (B - EB);
     uint32_t r[EIN];
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
       const uint32_t idx = i * kThreads + tid;
       if (total % kThreads != 0 && idx >= total) continue;
       const uint32_t j = idx & ((1u << C) - 1), t = idx >> C;
-      uint32_t v = p.out[(g_hi << (p.a + B)) + (uint64_t(t) << p.a) + low0 + j];
+      uint32_t v = p.in[(g_hi << (p.a + B)) + (uint64_t(t) << p.a) + low0 + j];
       if (!INV) {
         const uint32_t ex = (low0 + j) * bitrev_n(t, B);
         v = fp_mul(v, fp_mul(p.sc_hi[ex >> p.sc_split], p.sc_lo[ex & ((1u << p.sc_split) - 1)]));
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
     uint32_t r[E];
 #pragma unroll
     for (uint32_t i = 0; i < E; i++)
-      r[i] = p.out[(g_hi << (p.a + B)) + (uint64_t(R * i + t0) << p.a) + low0 + j];
+      r[i] = p.in[(g_hi << (p.a + B)) + (uint64_t(R * i + t0) << p.a) + low0 + j];
     if (!INV) {
       ColTwiddles<B, C> tf;
       tf.init(p, low0 + j, t0);
@@ -522,7 +522,7 @@ void ntt_evaluate(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count
   for (size_t i = 0; i < pl.size(); i++) {
     PassArgs p{};
     p.out = out;
-    p.in = in;
+    p.in = i == 0 ? in : out;
     p.eb = eb;
     fill_pass(p, false, L, pl[i].first, pl[i].second, count);
     if (i == 0) launch_pass<false, true, false, false>(s, p, pl[i].second);
@@ -531,13 +531,23 @@ void ntt_evaluate(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count
 }
 
 void ntt_interpolate(hipStream_t s, uint32_t* io, size_t count, uint32_t L, bool zk) {
-  if (count == 0 || L == 0) return;  // size-1 transform (and 3^0 shift) is the identity
+  ntt_interpolate_from(s, io, io, count, L, zk);
+}
+
+// io = interpolate(src): the first pass reads `src` (e.g. the witness) directly, so an
+// out-of-place transform costs no extra copy
+void ntt_interpolate_from(hipStream_t s, uint32_t* io, const uint32_t* src, size_t count, uint32_t L, bool zk) {
+  if (count == 0) return;
+  if (L == 0) {  // size-1 transform (and 3^0 shift) is the identity
+    if (src != io) HIP_OK(hipMemcpyAsync(io, src, count * 4, hipMemcpyDeviceToDevice, s));
+    return;
+  }
   KScope ks("ntt_interpolate", double(count) * 8 * (size_t(1) << L), double(count) * double(size_t(1) << L) / 2 * L);
   auto pl = plan(L);
   for (size_t i = pl.size(); i-- > 0;) {
     PassArgs p{};
     p.out = io;
-    p.in = io;
+    p.in = i == pl.size() - 1 ? src : io;
     fill_pass(p, true, L, pl[i].first, pl[i].second, count);
     if (i == 0) {
       uint32_t b = pl[0].second;

@@ -259,8 +259,7 @@ struct Prover {
   void commit_group(size_t g, const uint32_t* witness) {
     size_t gs = c.group_size(g);
     DevBuf coeffs(gs * cycles);
-    HIP_OK(hipMemcpyAsync(coeffs.p, witness, gs * cycles * 4, hipMemcpyDeviceToDevice, stream()));
-    ntt_interpolate(stream(), coeffs.p, gs, uint32_t(po2), true);
+    ntt_interpolate_from(stream(), coeffs.p, witness, gs, uint32_t(po2), true);
     groups[g].reset(new PolyGroup(suite, std::move(coeffs), gs, po2));
     groups[g]->tree.commit(iop);
   }

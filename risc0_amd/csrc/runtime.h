@@ -63,6 +63,8 @@ inline unsigned div_up(size_t a, size_t b) { return unsigned((a + b - 1) / b); }
 void ntt_evaluate(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count, uint32_t log_out,
                   uint32_t expand_bits);
 void ntt_interpolate(hipStream_t s, uint32_t* io, size_t count, uint32_t log_n, bool zk_shift);
+void ntt_interpolate_from(hipStream_t s, uint32_t* io, const uint32_t* src, size_t count, uint32_t log_n,
+                          bool zk_shift);
 void bit_reverse(hipStream_t s, uint32_t* io, size_t count, uint32_t log_n);
 void zk_shift(hipStream_t s, uint32_t* io, size_t count, uint32_t log_n);
 
