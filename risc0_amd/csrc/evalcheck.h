@@ -9,6 +9,7 @@ namespace r0 {
 struct EvalCheckArgs {
   const uint32_t* const* args;  // poly_fp argument buffers, circuit order
   size_t nargs;
+  const uint32_t* const* colptr;  // device table: base pointer of every column the program reads
   const uint32_t* poly_mix;     // poly_mix powers + folded products (FpExt AoS, Montgomery)
   const uint32_t* poly_mix_nb;  // the same table times NBETA = -11 (lazy extension products)
   uint32_t* acc;                // scratch: domain x FpExt
@@ -26,7 +27,10 @@ struct EvalCheckInfo {
   int npm;            // number of poly_mix powers the kernels index directly
   int nargs;
   int mat_fp, mat_ext, kernels;
-  double modmuls_per_point;  // field multiplications of the restated poly_fp (+4 for the 1/Z scale)
+  double modmuls_per_point;
+  int ncols;             // columns the program reads: (argument, column) pairs
+  const int* col_arg;
+  const int* col_idx;  // field multiplications of the restated poly_fp (+4 for the 1/Z scale)
 };
 
 void eval_check_rv32im(hipStream_t s, const EvalCheckArgs& e);

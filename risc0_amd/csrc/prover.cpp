@@ -220,6 +220,10 @@ void run_eval_check(const CircuitDef& c, uint32_t* check, const uint32_t* const*
   EvalCheckArgs e;
   e.args = args.data();
   e.nargs = args.size();
+  // one base pointer per column the generated program reads (saddr-form tap loads)
+  std::vector<const uint32_t*> colptr(info.ncols);
+  for (int i = 0; i < info.ncols; i++) colptr[i] = args[info.col_arg[i]] + size_t(info.col_idx[i]) * domain;
+  e.colptr = reinterpret_cast<const uint32_t* const*>(upload(colptr, 26));
   e.poly_mix = upload(pm, 20);
   std::vector<FpExt> pmn(pm.size());
   for (size_t i = 0; i < pm.size(); i++) pmn[i] = fe_mul_fp(pm[i], kNBeta);

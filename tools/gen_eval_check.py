@@ -235,13 +235,29 @@ def schedule(pg, budget):
     return terms, kernels
 
 
-CHUNK = int(os.environ.get("EC_CHUNK", "0"))
 # emission order: "ir" (the reference program's order) or "dfs" (each value computed
 # right before its first use, accumulation chains first; loads hoisted EC_PF ops ahead)
 ORDER = os.environ.get("EC_ORDER", "dfs")
 PF = int(os.environ.get("EC_PF", "512"))
 # minimum waves per SIMD requested from the register allocator (1 = no limit)
 WAVES = int(os.environ.get("EC_WAVES", "2"))
+# Variants measured on MI355X (per-kernel rocprofv3 sums, rv32im po2=20, tools/ec_variants.sh):
+#   canonical results (default)                  28.6-28.8 ms
+#   EC_CANON=0 lazy range analysis               34.3-34.8 ms: 2-11% fewer VALU instructions,
+#                                                but more live registers -> spills in 6 kernels
+#   EC_SADDR=1 saddr tap loads                   28.9-30.0 ms: -1.1k VALU per big kernel, no gain
+#   EC_SPLIT=2 / 3 split accumulation chains     30.6 / 32.7 ms (register pressure)
+# The kernels are bound by register pressure and issue stalls (SQ_WAIT_INST_ANY 30-55% of
+# wave cycles), not by the count of VALU instructions.
+# EC_CANON=1: every Fp/FpExt result canonical; EC_CANON=0: the lazy range analysis below
+CANON_ALL = os.environ.get("EC_CANON", "1") == "1"
+# EC_SADDR=0: taps addressed as A.a[arg][col * domain + row] (64-bit VALU address per load);
+# EC_SADDR=1: scalar column base (A.cp) + one 32-bit lane offset per `back`
+SADDR = os.environ.get("EC_SADDR", "0") == "1"
+# EC_SPLIT=n: each accumulation chain (ACC + T*pm[k], ...) runs as n interleaved partial
+# sums, joined where the value is used, so consecutive products do not wait on each
+# other's v_mad_u64_u32 results
+SPLIT = int(os.environ.get("EC_SPLIT", "1"))
 
 
 def kernel_config(circuit, budget):
@@ -259,7 +275,42 @@ def kernel_config(circuit, budget):
     return {int(k): v for k, v in t["kernels"].items()}
 
 
-def emit(circuit, outdir, budget):
+# ---- value-range analysis --------------------------------------------------------
+# Every Fp word (and every limb of an FpExt) is kept as a 32-bit integer congruent to
+# its Montgomery word mod p, below a bound M (inclusive maximum) that the generator
+# knows exactly. Reductions are emitted only where an operation could overflow:
+#   x + y                     M = Mx + My                      (< 2^32)
+#   x - y = x + (k p - y)     M = Mx + k p,  k p >= My
+#   lmul(x, y) (REDC, no min) M = (Mx My + (2^32 - 1) p) >> 32  (Mx My + (2^32-1) p < 2^64)
+#   lred(x) = min(x, x - p)   M = max(p - 1, Mx - p)
+# FpExt products form four 4-term sums in 64 bits (< 2^64), fold hi*(2^32 mod p)+lo and
+# REDC. Anything that leaves the kernel (the accumulator, check, materialised values) is
+# canonical, so outputs are the reference's words exactly.
+U32 = 2**32 - 1
+U64 = 2**64 - 1
+FOLDC = 2**32 % P
+
+
+def redc_max(t):
+    assert t + U32 * P <= U64
+    return (t + U32 * P) >> 32
+
+
+def fold_max(x):
+    return (x >> 32) * FOLDC + U32
+
+
+def mul_ok(ma, mb):
+    t = ma * mb
+    return t + U32 * P <= U64 and redc_max(t) <= U32
+
+
+def emul_ok(ma, mb):
+    # four products per limb, b's upper limbs enter as canonical NBETA*b
+    return 4 * ma * max(mb, P - 1) <= U64
+
+
+def emit(circuit, outdir, budget, host=False):
     pg = Program(circuit)
     terms, kernels = schedule(pg, budget)
     tune = kernel_config(circuit, budget)
@@ -277,15 +328,29 @@ def emit(circuit, outdir, budget):
             slot[v] = ("e", ne)
             ne += 1
     combo_index = {}
-    os.makedirs(outdir, exist_ok=True)
+    # trace columns read by the program: the host passes one base pointer per column
+    # (A.cp), so a tap is a global load with a scalar base and a shared 32-bit lane
+    # offset per `back` (no per-load 64-bit address arithmetic on the VALU)
+    colslot = {}
+    for ins in prog:
+        if ins[0] == "l" and (ins[2], ins[3]) not in colslot:
+            colslot[(ins[2], ins[3])] = len(colslot)
+    if outdir:
+        os.makedirs(outdir, exist_ok=True)
 
     common = [
         '#include "bb31.h"',
+        "#if defined(R0_EC_HOST)",
+        "#define EC_FN static inline",
+        "#else",
         '#include "evalcheck.h"',
+        "#define EC_FN __device__ __forceinline__",
+        "#endif",
         "namespace r0 {",
         f"namespace ec_{circuit} {{",
         "struct Args {",
         f"  const uint32_t* a[{nargs}];",
+        "  const uint32_t* const* cp;  // column base pointers (kColArg/kColIdx order)",
         "  const uint32_t* pm;   // poly_mix powers then folded products, FpExt AoS",
         "  const uint32_t* pmn;  // the same times NBETA",
         "  uint32_t* acc;        // FpExt AoS accumulator per point",
@@ -297,47 +362,76 @@ def emit(circuit, outdir, budget):
         "  uint32_t base, count;  // this launch covers points [base, base + count)",
         "};",
         f"constexpr int NPM = {npm};",
-        "__device__ __forceinline__ FpExt eadd(FpExt a, FpExt b) { return fe_add(a, b); }",
-        "__device__ __forceinline__ FpExt eadd(FpExt a, uint32_t b) { a.c[0] = fp_add(a.c[0], b); return a; }",
-        "__device__ __forceinline__ FpExt eadd(uint32_t a, FpExt b) { b.c[0] = fp_add(a, b.c[0]); return b; }",
-        "__device__ __forceinline__ FpExt esub(FpExt a, FpExt b) { return fe_sub(a, b); }",
-        "__device__ __forceinline__ FpExt esub(FpExt a, uint32_t b) { a.c[0] = fp_sub(a.c[0], b); return a; }",
-        "__device__ __forceinline__ FpExt esub(uint32_t a, FpExt b) { return fe_sub(fe_from_fp(a), b); }",
-        "__device__ __forceinline__ FpExt emul(FpExt a, FpExt b) { return fe_mul(a, b); }",
-        "__device__ __forceinline__ FpExt emul(FpExt a, uint32_t b) { return fe_mul_fp(a, b); }",
-        "__device__ __forceinline__ FpExt emul(uint32_t a, FpExt b) { return fe_mul_fp(b, a); }",
-        "__device__ __forceinline__ uint32_t emul(uint32_t a, uint32_t b) { return fp_mul(a, b); }",
-        "// Lazy FpExt accumulator: four unreduced 64-bit sums of Montgomery products",
-        "// (each < p^2); the generator tracks an upper bound per value and folds",
-        "// (hi * (2^32 mod p) + lo, < 2^60) before a sum could reach 2^64.",
+        "// lazy Fp/FpExt words: congruent mod p, below a generator-tracked bound (see",
+        "// tools/gen_eval_check.py); lred/xred take one p off values >= p",
+        "EC_FN uint32_t lmul(uint32_t a, uint32_t b) {",
+        "  const uint64_t t = uint64_t(a) * b;",
+        "  const uint32_t m = uint32_t(t) * kNegPinv;",
+        "  return uint32_t((t + uint64_t(m) * kP) >> 32);",
+        "}",
+        "// tap load: scalar column base + 32-bit byte offset (saddr-form global load)",
+        "EC_FN uint32_t ldc(const uint32_t* p, uint32_t off) {",
+        "  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(p) + off);",
+        "}",
+        "EC_FN uint32_t lred(uint32_t x) { return umin(x, x - kP); }",
+        "EC_FN uint32_t lsub(uint32_t a, uint32_t b, uint32_t kp) { return a + (kp - b); }",
+        "EC_FN FpExt xred(FpExt a) { return FpExt{{lred(a.c[0]), lred(a.c[1]), lred(a.c[2]), lred(a.c[3])}}; }",
+        "EC_FN FpExt xadd(FpExt a, FpExt b) { return FpExt{{a.c[0] + b.c[0], a.c[1] + b.c[1], a.c[2] + b.c[2], a.c[3] + b.c[3]}}; }",
+        "EC_FN FpExt xaddf(FpExt a, uint32_t b) { a.c[0] += b; return a; }",
+        "EC_FN FpExt xsub(FpExt a, FpExt b, uint32_t kp) {",
+        "  return FpExt{{lsub(a.c[0], b.c[0], kp), lsub(a.c[1], b.c[1], kp), lsub(a.c[2], b.c[2], kp), lsub(a.c[3], b.c[3], kp)}};",
+        "}",
+        "EC_FN FpExt xsubf(FpExt a, uint32_t b, uint32_t kp) { a.c[0] = lsub(a.c[0], b, kp); return a; }",
+        "EC_FN FpExt fsubx(uint32_t a, FpExt b, uint32_t kp) {",
+        "  return FpExt{{lsub(a, b.c[0], kp), kp - b.c[1], kp - b.c[2], kp - b.c[3]}};",
+        "}",
+        "EC_FN FpExt xmulf(FpExt a, uint32_t b) { return FpExt{{lmul(a.c[0], b), lmul(a.c[1], b), lmul(a.c[2], b), lmul(a.c[3], b)}}; }",
+        "// extension product; b's upper limbs times NBETA are canonical; four 4-term sums,",
+        "// folded and REDC'd without the final min",
+        "EC_FN FpExt xmul(FpExt a, FpExt b) {",
+        "  const uint32_t n1 = fp_mul(kNBeta, b.c[1]), n2 = fp_mul(kNBeta, b.c[2]), n3 = fp_mul(kNBeta, b.c[3]);",
+        "  const uint64_t a0 = a.c[0], a1 = a.c[1], a2 = a.c[2], a3 = a.c[3];",
+        "  const uint64_t s0 = a0 * b.c[0] + a1 * n3 + a2 * n2 + a3 * n1;",
+        "  const uint64_t s1 = a0 * b.c[1] + a1 * b.c[0] + a2 * n3 + a3 * n2;",
+        "  const uint64_t s2 = a0 * b.c[2] + a1 * b.c[1] + a2 * b.c[0] + a3 * n3;",
+        "  const uint64_t s3 = a0 * b.c[3] + a1 * b.c[2] + a2 * b.c[1] + a3 * b.c[0];",
+        "  auto r = [](uint64_t t) { t = fold64(t); const uint32_t m = uint32_t(t) * kNegPinv;",
+        "                            return uint32_t((t + uint64_t(m) * kP) >> 32); };",
+        "  return FpExt{{r(s0), r(s1), r(s2), r(s3)}};",
+        "}",
+        "// Lazy FpExt accumulator: four unreduced 64-bit sums of Montgomery products;",
+        "// the generator tracks an upper bound and folds (hi * (2^32 mod p) + lo) before a",
+        "// sum could reach 2^64.",
         "struct Acc { uint64_t c[4]; };",
-        "// a canonical value v enters as v * 2^32 (mod p), so the final REDC returns v",
-        "__device__ __forceinline__ Acc acc_of(FpExt a) {",
+        "// a value v enters as v * 2^32 (mod p), so the final REDC returns v",
+        "EC_FN Acc acc_of(FpExt a) {",
         "  return Acc{{uint64_t(a.c[0]) * kFoldC, uint64_t(a.c[1]) * kFoldC, uint64_t(a.c[2]) * kFoldC,",
         "              uint64_t(a.c[3]) * kFoldC}};",
         "}",
-        "__device__ __forceinline__ Acc acc_of(uint32_t a) { return Acc{{uint64_t(a) * kFoldC, 0, 0, 0}}; }",
-        "__device__ __forceinline__ Acc acc_fold(Acc a) {",
+        "EC_FN Acc acc_of(uint32_t a) { return Acc{{uint64_t(a) * kFoldC, 0, 0, 0}}; }",
+        "EC_FN Acc acc_fold(Acc a) {",
         "#pragma unroll",
         "  for (int i = 0; i < 4; i++) a.c[i] = fold64(a.c[i]);",
         "  return a;",
         "}",
-        "__device__ __forceinline__ FpExt acc_red(Acc a) {",
+        "EC_FN FpExt acc_red(Acc a) {",
         "  return FpExt{{mont_reduce(a.c[0]), mont_reduce(a.c[1]), mont_reduce(a.c[2]), mont_reduce(a.c[3])}};",
         "}",
-        "__device__ __forceinline__ Acc acc_add(Acc a, Acc b) {",
+        "EC_FN uint32_t redc_lazy(uint64_t t) { const uint32_t m = uint32_t(t) * kNegPinv; return uint32_t((t + uint64_t(m) * kP) >> 32); }",
+        "EC_FN FpExt acc_lred(Acc a) { return FpExt{{redc_lazy(a.c[0]), redc_lazy(a.c[1]), redc_lazy(a.c[2]), redc_lazy(a.c[3])}}; }",
+        "EC_FN Acc acc_add(Acc a, Acc b) {",
         "#pragma unroll",
         "  for (int i = 0; i < 4; i++) a.c[i] += b.c[i];",
         "  return a;",
         "}",
         "// a += t * pm[k]  (t in Fp)",
-        "__device__ __forceinline__ Acc acc_fp(Acc a, uint32_t t, const uint32_t* pm, int k) {",
+        "EC_FN Acc acc_fp(Acc a, uint32_t t, const uint32_t* pm, int k) {",
         "#pragma unroll",
         "  for (int i = 0; i < 4; i++) a.c[i] += uint64_t(t) * pm[4 * k + i];",
         "  return a;",
         "}",
         "// a += t * pm[k]  (t in FpExt; x^4 = NBETA folded into pmn = NBETA * pm)",
-        "__device__ __forceinline__ Acc acc_ext(Acc a, FpExt t, const uint32_t* pm, const uint32_t* pmn, int k) {",
+        "EC_FN Acc acc_ext(Acc a, FpExt t, const uint32_t* pm, const uint32_t* pmn, int k) {",
         "  const uint32_t* q = pm + 4 * k;",
         "  const uint32_t* n = pmn + 4 * k;",
         "  a.c[0] += uint64_t(t.c[0]) * q[0] + uint64_t(t.c[1]) * n[3] + uint64_t(t.c[2]) * n[2] + uint64_t(t.c[3]) * n[1];",
@@ -350,13 +444,11 @@ def emit(circuit, outdir, budget):
     common_text = "\n".join(common) + "\n"
 
     stats = []
-    PROD = (P - 1) ** 2
-    LIM = 2**64
+    bodies = []
+    PM = P - 1  # bound of a canonical word / of every pm, pmn word
     RED = P * 2**32
-    CANON = (P - 1) * (2**32 % P)  # bound of acc_of(canonical)
-
-    def fold_bound(bd):
-        return (bd >> 32) * (2**32 % P) + 2**32 - 1
+    CANON = PM * FOLDC  # bound of acc_of(canonical)
+    one, two, mone = enc(1), enc(2), enc(P - 1)
 
     for ki, items in enumerate(kernels):
         roots = []
@@ -367,7 +459,7 @@ def emit(circuit, outdir, budget):
         loaded = set(v for v in need if v in pg.mat and v not in produced)
         first, last = ki == 0, ki == len(kernels) - 1
         mine = [it[3] for it in items if it[2] == "term"]
-        # accumulate ops computed here stay lazy (Acc a<i>); canonical v<i> only where needed
+        # accumulate ops computed here stay lazy (Acc a<i>); FpExt v<i> only where needed
         lazy = set(v for v in need if v not in loaded and pg.byid[v][0] in "ab")
         canon = set(produced & lazy)
         for v in need:
@@ -384,75 +476,191 @@ def emit(circuit, outdir, budget):
             for x in f:
                 if x[0] == "v" and x[1] in lazy:
                     canon.add(x[1])
-        bound = {}
+        parts = {}   # lazy accumulation value -> its partial sums [(Acc name, 64-bit bound)]
+        chainpos = {}
+        Mv = {}      # word bounds of v<i>
+        cval = {}    # Fp constants: Montgomery word
+        red_memo = {}
+        offs = set()
+        tmp = {"n": 0}
         L = []
         w = L.append
 
-        # Trace taps and materialised values are re-loaded where they are used instead of
-        # being kept live: the program is cut into chunks of CHUNK ops separated by a
-        # compiler memory barrier, and a load is emitted (once) in each chunk that needs
-        # it. Without this LLVM hoists all ~400 loads to the top and the kernels need
-        # 450-512 VGPR+AGPR (one wave per SIMD, exposed load latency).
-        remat = set(v for v in need if v in loaded or pg.byid[v][0] == "l") if CHUNK else set()
-        chunk = {"n": 0, "ops": 0, "have": {}}
+        def fresh():
+            tmp["n"] += 1
+            return f"t{tmp['n']}"
 
-        def ref(x):
-            if x not in remat:
-                return f"v{x}"
-            h = chunk["have"]
-            if x not in h:
-                nm = f"v{x}_{chunk['n']}"
-                h[x] = nm
-                if x in loaded:
-                    kind, s_ = slot[x]
-                    if kind == "f":
-                        w(f"  const uint32_t {nm} = A.mf[uint64_t({s_}u) * A.domain + cycle];")
-                    else:
-                        w(f"  FpExt {nm}; {{ uint4 t = reinterpret_cast<const uint4*>(A.me)[uint64_t({s_}u) * A.domain"
-                          f" + cycle]; {nm} = FpExt{{{{t.x, t.y, t.z, t.w}}}}; }}")
+        def opd(x):
+            return (f"v{x}", Mv[x], types[x], x)
+
+        def decl(ty):
+            return "uint32_t" if ty == "f" else "FpExt"
+
+        def reduce1(o):
+            nm, M, ty, key = o
+            assert M >= P
+            if key is not None:
+                for nm2, m2 in red_memo.get(key, []):
+                    if m2 < M:
+                        return (nm2, m2, ty, key)
+            n2 = fresh()
+            w(f"  const {decl(ty)} {n2} = {'lred' if ty == 'f' else 'xred'}({nm});")
+            m2 = max(PM, M - P)
+            if key is not None:
+                red_memo.setdefault(key, []).append((n2, m2))
+            return (n2, m2, ty, key)
+
+        def canonical(o):
+            while o[1] >= P:
+                o = reduce1(o)
+            return o
+
+        def larger_first(a, b):
+            return (a, b) if a[1] >= b[1] else (b, a)
+
+        def out(ty, expr, M, name=None):
+            """declare a value; CANON_ALL reduces every result (the pre-range-analysis
+            arithmetic, kept for A/B runs)"""
+            nm = name or fresh()
+            if CANON_ALL:
+                r = "lred" if ty == "f" else "xred"
+                while M >= P:
+                    expr, M = f"{r}({expr})", max(PM, M - P)
+            w(f"  const {decl(ty)} {nm} = {expr};")
+            return (nm, M, ty, None)
+
+        def op_add(a, b, name=None):
+            while a[1] + b[1] > U32:
+                if a[1] >= b[1]:
+                    a = reduce1(a)
                 else:
-                    ins = pg.byid[x]
-                    w(f"  const uint32_t {nm} = A.a[{ins[2]}][{ins[3]}u * A.domain + ((cycle - {4 * ins[4]}u) & mask)];")
-            return h[x]
+                    b = reduce1(b)
+            ta, tb = a[2], b[2]
+            M = a[1] + b[1]
+            if ta == "f" and tb == "f":
+                return out("f", f"{a[0]} + {b[0]}", M, name)
+            if ta == "e" and tb == "e":
+                return out("e", f"xadd({a[0]}, {b[0]})", M, name)
+            if ta == "e":
+                return out("e", f"xaddf({a[0]}, {b[0]})", M, name)
+            return out("e", f"xaddf({b[0]}, {a[0]})", M, name)
 
-        def tick():
-            chunk["ops"] += 1
-            if CHUNK and chunk["ops"] >= CHUNK:
-                w("  asm volatile(\"\" ::: \"memory\");")
-                chunk["n"] += 1
-                chunk["ops"] = 0
-                chunk["have"] = {}
+        def op_sub(a, b, name=None):
+            while True:
+                k = max(1, -(-b[1] // P))
+                kp = k * P
+                if a[1] + kp <= U32:
+                    break
+                if a[1] >= b[1]:
+                    a = reduce1(a)
+                else:
+                    b = reduce1(b)
+            M = a[1] + kp
+            ta, tb = a[2], b[2]
+            if ta == "f" and tb == "f":
+                return out("f", f"lsub({a[0]}, {b[0]}, {kp}u)", M, name)
+            if ta == "e" and tb == "e":
+                return out("e", f"xsub({a[0]}, {b[0]}, {kp}u)", M, name)
+            if ta == "e":
+                return out("e", f"xsubf({a[0]}, {b[0]}, {kp}u)", M, name)
+            return out("e", f"fsubx({a[0]}, {b[0]}, {kp}u)", M, name)
+
+        def op_mul(a, b, name=None):
+            ta, tb = a[2], b[2]
+            if ta == "f" and tb == "f":
+                for x, y in ((a, b), (b, a)):
+                    c = cval.get(x[3]) if x[3] is not None else None
+                    if c == one:
+                        return out("f", y[0], y[1], name)
+                    if c == two and 2 * y[1] <= U32:
+                        return out("f", f"{y[0]} + {y[0]}", 2 * y[1], name)
+                    if c == mone:
+                        kp = max(1, -(-y[1] // P)) * P
+                        return out("f", f"{kp}u - {y[0]}", kp, name)
+            if ta == "e" and tb == "e":
+                while not emul_ok(a[1], b[1]):
+                    if a[1] >= b[1]:
+                        a = reduce1(a)
+                    else:
+                        b = reduce1(b)
+                M = redc_max(fold_max(4 * a[1] * max(b[1], PM)))
+                return out("e", f"xmul({a[0]}, {b[0]})", M, name)
+            while not mul_ok(a[1], b[1]):
+                if a[1] >= b[1]:
+                    a = reduce1(a)
+                else:
+                    b = reduce1(b)
+            M = redc_max(a[1] * b[1])
+            if ta == "f" and tb == "f":
+                return out("f", f"lmul({a[0]}, {b[0]})", M, name)
+            if ta == "e":
+                return out("e", f"xmulf({a[0]}, {b[0]})", M, name)
+            return out("e", f"xmulf({b[0]}, {a[0]})", M, name)
+
+        joined = {}
 
         def acc_src(x):
-            """(expression, bound) of an Acc holding value x."""
-            if x in lazy:
-                return f"a{x}", bound[x]
-            return f"acc_of({ref(x)})", CANON
+            """(expression, bound) of an Acc holding value x (partial sums joined)."""
+            if x not in lazy:
+                return f"acc_of(v{x})", Mv[x] * FOLDC
+            ps = parts[x]
+            if len(ps) == 1:
+                return ps[0]
+            if x not in joined:
+                e, b = ps[0]
+                for n_, (e2, b2) in enumerate(ps[1:]):
+                    if b + b2 > U64:
+                        e2, b2 = f"acc_fold({e2})", fold_max(b2)
+                    e, b = room(e, b, b2)
+                    nm = f"a{x}_j{n_}"
+                    w(f"  const Acc {nm} = acc_add({e}, {e2});")
+                    e, b = nm, b + b2
+                joined[x] = (e, b)
+            return joined[x]
 
-        def room(expr, bd, k):
-            """fold expr first if adding k more products could overflow 64 bits."""
-            if bd + k * PROD >= LIM:
-                return f"acc_fold({expr})", fold_bound(bd)
+        def acc_parts(x):
+            if x in lazy:
+                return list(parts[x]), chainpos[x] + 1
+            return [(f"acc_of(v{x})", Mv[x] * FOLDC)], 1
+
+        def room(expr, bd, add):
+            """fold expr first if adding `add` could overflow 64 bits."""
+            if bd + add > U64:
+                bd = fold_max(bd)
+                expr = f"acc_fold({expr})"
+                assert bd + add <= U64
             return expr, bd
 
-        def reduced(expr, bd):
+        def add_prod(expr, bd, t, k):
+            """Acc expression for expr + t * pm[k]; t an operand."""
+            if t[2] == "e":
+                while 4 * t[1] * PM + fold_max(U64) > U64:
+                    t = reduce1(t)
+                add = 4 * t[1] * PM
+                expr, bd = room(expr, bd, add)
+                return f"acc_ext({expr}, {t[0]}, A.pm, A.pmn, {k})", bd + add
+            add = t[1] * PM
+            expr, bd = room(expr, bd, add)
+            return f"acc_fp({expr}, {t[0]}, A.pm, {k})", bd + add
+
+        def acc_to_ext(expr, bd, name):
+            """lazy FpExt of an Acc (REDC without the final min)"""
+            if bd + U32 * P > U64 or redc_max(bd) > U32:
+                expr, bd = f"acc_fold({expr})", fold_max(bd)
+            M = redc_max(bd)
+            if CANON_ALL:
+                if bd >= RED:
+                    expr = f"acc_fold({expr})"
+                w(f"  const FpExt {name} = acc_red({expr});")
+                return PM
+            w(f"  const FpExt {name} = acc_lred({expr});")
+            return M
+
+        def canon_out(expr, bd):
             if bd >= RED:
                 return f"acc_red(acc_fold({expr}))"
             return f"acc_red({expr})"
 
-        def pmidx(k):
-            return str(k)
-
-        def add_prod(expr, bd, t, tty, k):
-            """Acc expression for expr + t * pm[k]; t canonical of type tty."""
-            n = 1 if tty == "f" else 4
-            expr, bd = room(expr, bd, n)
-            if tty == "f":
-                return f"acc_fp({expr}, {t}, A.pm, {k})", bd + PROD
-            return f"acc_ext({expr}, {t}, A.pm, A.pmn, {k})", bd + 4 * PROD
-
-        # Each term is added to the running sum right after its last root is computed,
-        # so term values do not stay live to the end of the kernel.
         acc_state = {"n": 0, "b": 0}
         kwaves = tune.get(ki, {}).get("waves", WAVES)
         kpf = tune.get(ki, {}).get("pf", PF)
@@ -484,7 +692,7 @@ def emit(circuit, outdir, budget):
             order_pos[ins_[1]] = n_
         term_at = {}
         for ti, (e, f) in enumerate(mine):
-            rts = [x for x in term_roots((e, f)) if x not in remat and pg.byid[x][0] not in "ceg"]
+            rts = [x for x in term_roots((e, f)) if pg.byid[x][0] not in "ceg"]
             term_at.setdefault(max([order_pos[x] for x in rts] + [-1]), []).append(ti)
         done_terms = set()
 
@@ -500,23 +708,21 @@ def emit(circuit, outdir, budget):
             if not vals and not pms:
                 src, bd = acc_src(e)
                 cur, sb2 = f"s{sn}", sb
-                if sb2 + bd >= LIM:
-                    cur, sb2 = f"acc_fold({cur})", fold_bound(sb2)
-                if sb2 + bd >= LIM:
-                    src, bd = f"acc_fold({src})", fold_bound(bd)
+                if sb2 + bd > U64:
+                    cur, sb2 = f"acc_fold({cur})", fold_max(sb2)
+                if sb2 + bd > U64:
+                    src, bd = f"acc_fold({src})", fold_max(bd)
                 w(f"  const Acc s{sn + 1} = acc_add({cur}, {src});")
                 acc_state["n"], acc_state["b"] = sn + 1, sb2 + bd
                 return
-            expr = ref(e)
-            ety = types[e]
+            cur = opd(e)
             for v in vals:
-                expr = f"emul({expr}, {ref(v)})"
-                if types[v] == "e":
-                    ety = "e"
+                cur = op_mul(cur, opd(v))
             if not pms:
-                cur, sb2 = room(f"s{sn}", sb, 1)
-                w(f"  const Acc s{sn + 1} = acc_add({cur}, acc_of({expr}));")
-                acc_state["n"], acc_state["b"] = sn + 1, sb2 + CANON
+                add = cur[1] * FOLDC
+                s, sb2 = room(f"s{sn}", sb, add)
+                w(f"  const Acc s{sn + 1} = acc_add({s}, acc_of({cur[0]}));")
+                acc_state["n"], acc_state["b"] = sn + 1, sb2 + add
                 return
             if len(pms) == 1:
                 k = pms[0]
@@ -524,22 +730,15 @@ def emit(circuit, outdir, budget):
                 if pms not in combo_index:
                     combo_index[pms] = len(combo_index)
                 k = f"NPM + {combo_index[pms]}"
-            e2, sb = add_prod(f"s{sn}", sb, expr, ety, k)
+            e2, sb = add_prod(f"s{sn}", sb, cur, k)
             w(f"  const Acc s{sn + 1} = {e2};")
             acc_state["n"], acc_state["b"] = sn + 1, sb
 
-        w(f"// GENERATED by tools/gen_eval_check.py from risc0_amd/circuits/{circuit}.poly.ir — do not edit.")
-        w(common_text)
-        lb = "256" if kwaves <= 1 else f"256, {kwaves}"
-        w(f"__global__ __launch_bounds__({lb}) void k{ki}(Args A) {{")
-        w("  const uint32_t cycle = A.base + blockIdx.x * 256u + threadIdx.x;")
-        w("  if (cycle >= A.base + A.count) return;")
-        w("  const uint32_t mask = A.domain - 1;")
         if mine or last:
             w("  const Acc s0 = Acc{{0, 0, 0, 0}};")
         for ins in kprog:
             op, i = ins[0], ins[1]
-            if i not in need or op == "r" or i in remat:
+            if i not in need or op == "r":
                 continue
             if i in loaded:
                 kind, s_ = slot[i]
@@ -548,49 +747,60 @@ def emit(circuit, outdir, budget):
                 else:
                     w(f"  FpExt v{i}; {{ uint4 t = reinterpret_cast<const uint4*>(A.me)[uint64_t({s_}u) * A.domain + cycle];"
                       f" v{i} = FpExt{{{{t.x, t.y, t.z, t.w}}}}; }}")
+                Mv[i] = PM
+                continue
+            if op == "l" and not SADDR:
+                w(f"  const uint32_t v{i} = A.a[{ins[2]}][{ins[3]}u * A.domain + ((cycle - {4 * ins[4]}u) & mask)];")
+                Mv[i] = PM
                 continue
             if op == "l":
-                w(f"  const uint32_t v{i} = A.a[{ins[2]}][{ins[3]}u * A.domain + ((cycle - {4 * ins[4]}u) & mask)];")
+                back = ins[4]
+                if back not in offs:
+                    offs.add(back)
+                    w(f"  const uint32_t o{back} = ((cycle - {4 * back}u) & mask) * 4u;")
+                w(f"  const uint32_t v{i} = ldc(A.cp[{colslot[(ins[2], ins[3])]}], o{back});")
+                Mv[i] = PM
                 continue
             if op == "c":
-                w(f"  const uint32_t v{i} = {enc(ins[2])}u;")
+                cval[i] = enc(ins[2])
+                w(f"  const uint32_t v{i} = {cval[i]}u;")
+                Mv[i] = cval[i]
             elif op == "e":
-                w(f"  const FpExt v{i} = FpExt{{{{{', '.join(str(enc(x)) + 'u' for x in ins[2:6])}}}}};")
+                ev = [enc(x) for x in ins[2:6]]
+                w(f"  const FpExt v{i} = FpExt{{{{{', '.join(str(x) + 'u' for x in ev)}}}}};")
+                Mv[i] = max(ev)
             elif op == "g":
                 w(f"  const uint32_t v{i} = A.a[{ins[2]}][{ins[3]}];")
+                Mv[i] = PM
             elif op in "ab":
-                src, bd = acc_src(ins[2])
+                ps, pos = acc_parts(ins[2])
                 if op == "a":
-                    t, tty, k = ref(ins[3]), types[ins[3]], ins[4]
+                    t, k = opd(ins[3]), ins[4]
                 else:
-                    T, U, k = ins[3], ins[4], ins[5]
-                    t = f"emul({ref(T)}, {ref(U)})"
-                    tty = "e" if "e" in (types[T], types[U]) else "f"
-                expr, bd = add_prod(src, bd, t, tty, k)
+                    t, k = op_mul(opd(ins[3]), opd(ins[4])), ins[5]
+                idx = pos % SPLIT
+                if idx >= len(ps):
+                    ps.append(("Acc{{0, 0, 0, 0}}", 0))
+                expr, bd = add_prod(ps[idx][0], ps[idx][1], t, k)
                 w(f"  const Acc a{i} = {expr};")
-                bound[i] = bd
+                ps[idx] = (f"a{i}", bd)
+                parts[i], chainpos[i] = ps, pos
                 if i in canon:
-                    w(f"  const FpExt v{i} = {reduced(f'a{i}', bd)};")
+                    e_, b_ = acc_src(i)
+                    Mv[i] = acc_to_ext(e_, b_, f"v{i}")
             else:
-                a, b = ins[2], ins[3]
-                ra, rb = ref(a), ref(b)
-                if types[a] == "f" and types[b] == "f":
-                    fn = {"+": "fp_add", "-": "fp_sub", "*": "fp_mul"}[op]
-                    w(f"  const uint32_t v{i} = {fn}({ra}, {rb});")
-                else:
-                    fn = {"+": "eadd", "-": "esub", "*": "emul"}[op]
-                    w(f"  const FpExt v{i} = {fn}({ra}, {rb});")
+                fn = {"+": op_add, "-": op_sub, "*": op_mul}[op]
+                Mv[i] = fn(opd(ins[2]), opd(ins[3]), name=f"v{i}")[1]
             if i in produced:
                 kind, s_ = slot[i]
+                o = canonical(opd(i))
                 if kind == "f":
-                    w(f"  A.mf[uint64_t({s_}u) * A.domain + cycle] = v{i};")
+                    w(f"  A.mf[uint64_t({s_}u) * A.domain + cycle] = {o[0]};")
                 else:
                     w(f"  reinterpret_cast<uint4*>(A.me)[uint64_t({s_}u) * A.domain + cycle] ="
-                      f" make_uint4(v{i}.c[0], v{i}.c[1], v{i}.c[2], v{i}.c[3]);")
+                      f" make_uint4({o[0]}.c[0], {o[0]}.c[1], {o[0]}.c[2], {o[0]}.c[3]);")
             for ti in term_at.get(order_pos[i], []):
                 emit_term(ti)
-            if op not in "ceg":
-                tick()
         if mine or last:
             # previous kernels' sum (if any) joins at the end; terms were added as they completed
             w("  uint4* accp = reinterpret_cast<uint4*>(A.acc) + cycle;")
@@ -599,10 +809,10 @@ def emit(circuit, outdir, budget):
             sn, sb = acc_state["n"], acc_state["b"]
             if not first:
                 w(f"  Acc s{sn + 1}; {{ uint4 p = *accp; s{sn + 1} = acc_of(FpExt{{{{p.x, p.y, p.z, p.w}}}}); }}")
-                cur, sb2 = room(f"s{sn}", sb, 1)
+                cur, sb2 = room(f"s{sn}", sb, CANON)
                 w(f"  const Acc s{sn + 2} = acc_add({cur}, s{sn + 1});")
                 sn, sb = sn + 2, sb2 + CANON
-            w(f"  FpExt s = {reduced(f's{sn}', sb)};")
+            w(f"  FpExt s = {canon_out(f's{sn}', sb)};")
             if last:
                 w("  s = fe_mul_fp(s, A.vinv[cycle & 3]);")
                 w("  #pragma unroll")
@@ -612,40 +822,93 @@ def emit(circuit, outdir, budget):
         if first and not mine and not last:
             # keep the accumulator defined for later kernels
             w("  reinterpret_cast<uint4*>(A.acc)[cycle] = make_uint4(0u, 0u, 0u, 0u);")
-        w("}")
-        w(f"void launch_k{ki}(hipStream_t s, const Args& A) {{")
-        w(f"  hipLaunchKernelGGL(k{ki}, dim3(div_up(A.count, 256)), dim3(256), 0, s, A);")
-        w("  HIP_OK(hipGetLastError());")
-        w("}")
-        w(f"}}  // namespace ec_{circuit}")
-        w("}  // namespace r0")
-        with open(os.path.join(outdir, f"eval_check_{circuit}_k{ki}.hip"), "w") as f:
-            f.write("\n".join(L) + "\n")
+        bodies.append((L, kwaves))
         stats.append(pg.cone_cost(roots))
-    # accumulator initialisation: kernels after the first add into acc; if the first
-    # kernel has no terms it zeroes it (above).
+
     flat = []
     for pms, j in sorted(combo_index.items(), key=lambda kv: kv[1]):
         flat += [len(pms)] + list(pms)
-    L = []
+    head = (f"// GENERATED by tools/gen_eval_check.py from risc0_amd/circuits/{circuit}.poly.ir — do not edit.\n"
+            + common_text)
+    info = [
+        f"void eval_check_{circuit}_info(EvalCheckInfo* info) {{",
+        f"  info->combos = ec_{circuit}::kPmCombos; info->ncombos = {len(combo_index)}; info->npm = ec_{circuit}::NPM;",
+        f"  info->nargs = {nargs}; info->mat_fp = {nf}; info->mat_ext = {ne}; info->kernels = {len(kernels)};",
+        f"  info->modmuls_per_point = {modmuls(pg) + 4};",
+        f"  info->ncols = {len(colslot)}; info->col_arg = ec_{circuit}::kColArg; info->col_idx = ec_{circuit}::kColIdx;",
+        "}",
+    ]
+    combos_line = f"const int kPmCombos[] = {{{', '.join(str(x) for x in flat) or '0'}}};"
+    cols = sorted(colslot, key=colslot.get)
+    combos_line += (f"\nconst int kColArg[] = {{{', '.join(str(a) for a, _ in cols)}}};"
+                    f"\nconst int kColIdx[] = {{{', '.join(str(c) for _, c in cols)}}};")
+    if host:
+        # one host translation unit: every kernel body as a per-point function, for the
+        # CPU check of the generated arithmetic (tests/test_ec_host.py)
+        T = ["#define R0_EC_HOST 1", "#include <stddef.h>", "#include <stdint.h>",
+             "struct uint4 { uint32_t x, y, z, w; };",
+             "static inline uint4 make_uint4(uint32_t x, uint32_t y, uint32_t z, uint32_t w) { return uint4{x, y, z, w}; }",
+             head]
+        for ki, (L, _) in enumerate(bodies):
+            T.append(f"static void k{ki}(const Args& A, uint32_t cycle) {{")
+            T.append("  const uint32_t mask = A.domain - 1;")
+            T += L
+            T.append("}")
+        T.append(f"constexpr int NK = {len(bodies)};")
+        T.append(f"static void (*const kTable[NK])(const Args&, uint32_t) = {{{', '.join(f'k{i}' for i in range(len(bodies)))}}};")
+        T.append(combos_line)
+        T.append(f"}}  // namespace ec_{circuit}")
+        T.append("}  // namespace r0")
+        T += [
+            f'extern "C" int ec_host_{circuit}_combos(const int** combos, int* npm) {{',
+            f"  *combos = r0::ec_{circuit}::kPmCombos; *npm = r0::ec_{circuit}::NPM; return {len(combo_index)};",
+            "}",
+            f'extern "C" void ec_host_{circuit}(const uint32_t* const* args, const uint32_t* pm, const uint32_t* pmn,',
+            "    const uint32_t* vinv, uint32_t* acc, uint32_t* mf, uint32_t* me, uint32_t* check, uint32_t domain) {",
+            f"  using namespace r0::ec_{circuit};",
+            "  Args A;",
+            f"  for (int i = 0; i < {nargs}; i++) A.a[i] = args[i];",
+            f"  const uint32_t* cp[{len(colslot)}];",
+            f"  for (int i = 0; i < {len(colslot)}; i++) cp[i] = args[kColArg[i]] + size_t(kColIdx[i]) * domain;",
+            "  A.cp = cp;",
+            "  A.pm = pm; A.pmn = pmn; A.acc = acc; A.check = check; A.vinv = vinv; A.mf = mf; A.me = me;",
+            "  A.domain = domain; A.base = 0; A.count = domain;",
+            "  for (int k = 0; k < NK; k++)",
+            "    for (uint32_t c = 0; c < domain; c++) kTable[k](A, c);",
+            "}",
+        ]
+        return "\n".join(T) + "\n"
+
+    for ki, (L, kwaves) in enumerate(bodies):
+        K = [head]
+        lb = "256" if kwaves <= 1 else f"256, {kwaves}"
+        K.append(f"__global__ __launch_bounds__({lb}) void k{ki}(Args A) {{")
+        K.append("  const uint32_t cycle = A.base + blockIdx.x * 256u + threadIdx.x;")
+        K.append("  if (cycle >= A.base + A.count) return;")
+        K.append("  const uint32_t mask = A.domain - 1;")
+        K += L
+        K.append("}")
+        K.append(f"void launch_k{ki}(hipStream_t s, const Args& A) {{")
+        K.append(f"  hipLaunchKernelGGL(k{ki}, dim3(div_up(A.count, 256)), dim3(256), 0, s, A);")
+        K.append("  HIP_OK(hipGetLastError());")
+        K.append("}")
+        K.append(f"}}  // namespace ec_{circuit}")
+        K.append("}  // namespace r0")
+        with open(os.path.join(outdir, f"eval_check_{circuit}_k{ki}.hip"), "w") as f:
+            f.write("\n".join(K) + "\n")
+    L = [head]
     w = L.append
-    w(f"// GENERATED by tools/gen_eval_check.py — {circuit}: {len(prog)} IR ops, {len(terms)} terms,")
-    w(f"// {len(kernels)} kernels, {nf} Fp + {ne} FpExt materialised values per point.")
-    w(common_text)
     for ki in range(len(kernels)):
         w(f"void launch_k{ki}(hipStream_t s, const Args& A);")
-    w(f"const int kPmCombos[] = {{{', '.join(str(x) for x in flat) or '0'}}};")
+    w(combos_line)
     w(f"}}  // namespace ec_{circuit}")
-    w(f"void eval_check_{circuit}_info(EvalCheckInfo* info) {{")
-    w(f"  info->combos = ec_{circuit}::kPmCombos; info->ncombos = {len(combo_index)}; info->npm = ec_{circuit}::NPM;")
-    w(f"  info->nargs = {nargs}; info->mat_fp = {nf}; info->mat_ext = {ne}; info->kernels = {len(kernels)};")
-    w(f"  info->modmuls_per_point = {modmuls(pg) + 4};")
-    w("}")
+    L += info
     w(f"void eval_check_{circuit}(hipStream_t s, const EvalCheckArgs& e) {{")
     w(f"  using namespace ec_{circuit};")
     w(f"  R0_REQUIRE(e.nargs == {nargs}, \"eval_check_{circuit}: wrong argument count\");")
     w("  Args A;")
     w(f"  for (int i = 0; i < {nargs}; i++) A.a[i] = e.args[i];")
+    w("  A.cp = e.colptr;")
     w("  A.pm = e.poly_mix; A.pmn = e.poly_mix_nb; A.acc = e.acc; A.check = e.check; A.vinv = e.vinv; A.domain = e.domain;")
     w("  A.mf = e.mat_fp; A.me = e.mat_ext;")
     w("  // tiles of e.tile points run every kernel before the next tile, so a tile's")
@@ -668,4 +931,10 @@ def emit(circuit, outdir, budget):
 
 
 if __name__ == "__main__":
-    emit(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 4000)
+    if sys.argv[1] == "--host":
+        # gen_eval_check.py --host CIRCUIT OUT.cpp [BUDGET]
+        src = emit(sys.argv[2], None, int(sys.argv[4]) if len(sys.argv) > 4 else 4000, host=True)
+        with open(sys.argv[3], "w") as f:
+            f.write(src)
+    else:
+        emit(sys.argv[1], sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 4000)
