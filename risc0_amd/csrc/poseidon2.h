@@ -97,6 +97,18 @@ R0_HD uint32_t mont_lazy(uint64_t t) {  // t < p*2^32 -> t*2^-32 mod p in [0, 2p
   uint32_t m = uint32_t(t) * kNegPinv;
   return uint32_t((t + uint64_t(m) * kP) >> 32);
 }
+// acc + a * b as one v_mad_u64_u32. Written as inline asm on the device so LLVM keeps
+// the multiply-accumulate: for sum(c_i * C) it otherwise factors C out and sums the
+// zero-extended c_i with a v_mov + v_lshl_add_u64 pair per cell.
+R0_HD uint64_t mad64(uint32_t a, uint32_t b, uint64_t acc) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(P2_NO_ASM)
+  uint64_t r, carry;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(carry) : "v"(a), "v"(b), "v"(acc));
+  return r;
+#else
+  return uint64_t(a) * b + acc;
+#endif
+}
 R0_HD uint32_t p2_sbox_lazy(uint32_t x) {  // x canonical -> x^7 in [0, 2p)
   uint32_t x2 = fp_mul(x, x);
   uint32_t x4 = mont_lazy(uint64_t(x2) * x2);
@@ -148,9 +160,9 @@ R0_HD void poseidon2_mix(uint32_t* c) {
     c[0] = p2_sbox_lazy(fp_add(umin(c[0], c[0] - kP), kP2Partial[r]));
     uint64_t s0 = 0, s1 = 0;
 #pragma unroll
-    for (int i = 0; i < 12; i++) s0 += uint64_t(c[i]) * kFoldC;
+    for (int i = 0; i < 12; i++) s0 = mad64(c[i], kFoldC, s0);
 #pragma unroll
-    for (int i = 12; i < 24; i++) s1 += uint64_t(c[i]) * kFoldC;
+    for (int i = 12; i < 24; i++) s1 = mad64(c[i], kFoldC, s1);
     const uint64_t sf = fold64(fold64(s0) + fold64(s1));
 #pragma unroll
     for (int i = 0; i < 24; i++) c[i] = mont_lazy(uint64_t(c[i]) * kP2Diag[i] + sf);
