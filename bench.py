@@ -215,7 +215,7 @@ def cpu_baseline(args, circ):
         po2 = args.cpu_po2
         rng = np.random.default_rng(0x5249534330)
         code, data, accum, glob = synthetic_witness(rng, circ, po2)
-        suite = oracle.POSEIDON2 if args.hashfn == "poseidon2" else oracle.SHA256
+        suite = {"poseidon2": oracle.POSEIDON2, "sha-256": oracle.SHA256, "poseidon_254": oracle.POSEIDON254}[args.hashfn]
         t0 = time.perf_counter()
         oracle.prove_segment(args.circuit, suite, po2, code, data, accum, glob,
                              version=2 if args.circuit == "rv32im" else None)

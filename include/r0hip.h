@@ -13,7 +13,8 @@
  *   - every call is complete when it returns (cuda.h:77-100 semantics): results are
  *     visible to the next call and to D2H copies. Work is queued on one HIP stream
  *     per process; r0hip_prove_segment runs whole proofs without per-op syncs.
- * Suites: R0HIP_POSEIDON2 = 0, R0HIP_SHA256 = 1 (zkp/src/core/hash/mod.rs:90-100).
+ * Suites: R0HIP_POSEIDON2 = 0, R0HIP_SHA256 = 1, R0HIP_POSEIDON254 = 2 (zkp/src/core/hash/mod.rs:90-100;
+ * the CUDA HAL's CudaHashPoseidon254, zkp/src/hal/cuda.rs:179-233).
  */
 #ifndef R0HIP_H
 #define R0HIP_H
@@ -26,6 +27,7 @@ extern "C" {
 
 #define R0HIP_POSEIDON2 0
 #define R0HIP_SHA256 1
+#define R0HIP_POSEIDON254 2
 
 /* ---- device / memory (replaces the `cust` crate; zkp/src/hal/cuda.rs:235-381,397-421) ---- */
 const char* r0hip_init(int device_ordinal);                       /* sppark_init (sys/src/cuda.rs:20) */
@@ -89,7 +91,8 @@ const char* r0hip_scatter(uint32_t* d_into, const uint32_t* d_index, const uint3
                           const uint32_t* d_values, size_t cycles);
 const char* r0hip_prefix_products(uint32_t* d_io, size_t count);
 
-/* ---- hashing (sppark_poseidon2_{rows,fold}, risc0_zkp_cuda_sha_{rows,fold}) ---- */
+/* ---- hashing (sppark_poseidon2_{rows,fold}, sppark_poseidon254_{rows,fold}, risc0_zkp_cuda_sha_{rows,fold};
+ * sys/src/cuda.rs:49-72) ---- */
 /* out[row] = H(matrix[col*rows + row] for col < cols) */
 const char* r0hip_hash_rows(int suite, uint32_t* d_out, const uint32_t* d_matrix, size_t rows, size_t cols);
 /* io[output_size + i] = H(io[input_size + 2i], io[input_size + 2i + 1]) (cpu.rs:569-581) */

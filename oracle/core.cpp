@@ -346,14 +346,17 @@ Digest sha256_hash_pair(const Digest& a, const Digest& b) {
 
 Digest hash_elem_slice(int suite, const Elem* e, size_t n) {
   if (suite == SUITE_POSEIDON2) return poseidon2_hash_elems(e, n);
+  if (suite == SUITE_POSEIDON254) return poseidon254_hash_elems(e, n);
   return sha256_hash_raw_words(reinterpret_cast<const uint32_t*>(e), n);
 }
 Digest hash_ext_elem_slice(int suite, const ExtElem* e, size_t n) {
   if (suite == SUITE_POSEIDON2) return poseidon2_hash_elems(&e[0].e[0], 4 * n);
+  if (suite == SUITE_POSEIDON254) return poseidon254_hash_elems(&e[0].e[0], 4 * n);
   return sha256_hash_raw_words(reinterpret_cast<const uint32_t*>(e), 4 * n);
 }
 Digest hash_pair(int suite, const Digest& a, const Digest& b) {
   if (suite == SUITE_POSEIDON2) return poseidon2_hash_pair(a, b);
+  if (suite == SUITE_POSEIDON254) return poseidon254_hash_pair(a, b);
   return sha256_hash_pair(a, b);
 }
 
@@ -436,6 +439,7 @@ struct ShaRng : Rng {
 
 std::unique_ptr<Rng> new_rng(int suite) {
   if (suite == SUITE_POSEIDON2) return std::unique_ptr<Rng>(new Poseidon2Rng());
+  if (suite == SUITE_POSEIDON254) return new_poseidon254_rng();
   return std::unique_ptr<Rng>(new ShaRng());
 }
 

@@ -47,7 +47,11 @@ Digest sha256_hash_raw_words(const uint32_t* w, size_t n);       // cpu.rs:56-77
 Digest sha256_hash_pair(const Digest& a, const Digest& b);       // sha/mod.rs:96-98, cpu.rs:81-105
 
 // ---- HashSuite -------------------------------------------------------------
-enum Suite { SUITE_POSEIDON2 = 0, SUITE_SHA256 = 1 };
+// ---- Poseidon254: risc0/zkp/src/core/hash/poseidon_254/mod.rs (poseidon254.cpp) ----
+Digest poseidon254_hash_elems(const Elem* e, size_t n);        // mod.rs:107-133
+Digest poseidon254_hash_pair(const Digest& a, const Digest& b);  // mod.rs:136-142
+
+enum Suite { SUITE_POSEIDON2 = 0, SUITE_SHA256 = 1, SUITE_POSEIDON254 = 2 };
 Digest hash_elem_slice(int suite, const Elem* e, size_t n);
 Digest hash_ext_elem_slice(int suite, const ExtElem* e, size_t n);
 Digest hash_pair(int suite, const Digest& a, const Digest& b);
@@ -60,5 +64,6 @@ struct Rng {
   virtual ExtElem random_ext_elem() = 0;
 };
 std::unique_ptr<Rng> new_rng(int suite);
+std::unique_ptr<Rng> new_poseidon254_rng();  // mod.rs:146-209
 
 }  // namespace oracle

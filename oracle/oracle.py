@@ -18,7 +18,7 @@ REF_PATH = os.path.join(HERE, "_ref", "libref_polyfp.so")
 CIRCUITS = os.path.join(ROOT, "risc0_amd", "circuits")
 
 P = 15 * 2**27 + 1
-POSEIDON2, SHA256 = 0, 1
+POSEIDON2, SHA256, POSEIDON254 = 0, 1, 2
 
 u32p = C.POINTER(C.c_uint32)
 _lib = None

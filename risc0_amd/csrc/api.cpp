@@ -233,13 +233,13 @@ const char* r0hip_prefix_products(uint32_t* d_io, size_t count) {
 
 const char* r0hip_hash_rows(int suite, uint32_t* d_out, const uint32_t* d_matrix, size_t rows, size_t cols) {
   return wrap([&] {
-    R0_REQUIRE(suite == 0 || suite == 1, "unknown hash suite");
+    R0_REQUIRE(suite >= 0 && suite <= 2, "unknown hash suite");
     hash_rows(stream(), suite, d_out, d_matrix, rows, cols);
   });
 }
 const char* r0hip_hash_fold(int suite, uint32_t* d_io, size_t input_size, size_t output_size) {
   return wrap([&] {
-    R0_REQUIRE(suite == 0 || suite == 1, "unknown hash suite");
+    R0_REQUIRE(suite >= 0 && suite <= 2, "unknown hash suite");
     hash_fold(stream(), suite, d_io, input_size, output_size);
   });
 }

@@ -11,6 +11,7 @@
 // 24-cell state lives in VGPRs. Poseidon2 is integer-VALU bound (~1.4k modmul per
 // permutation), not HBM bound.
 #include "poseidon2.h"
+#include "poseidon254.h"
 #include "runtime.h"
 
 namespace r0 {
@@ -61,6 +62,55 @@ __global__ __launch_bounds__(kThreads) void p2_fold_kernel(uint32_t* io, uint64_
   for (int k = 16; k < 24; k++) c[k] = 0;
   poseidon2_mix(c);
   store_digest(io + (out_off + i) * 8, c);
+}
+
+// ---- Poseidon254 (BN254 Fr, poseidon_254/mod.rs) ---------------------------------
+// One lane per row as above; the 3-cell state is 27 VGPRs of 29-bit limbs. Row values are
+// decoded from Montgomery to canonical (Elem::as_u32) and packed 8 per cell.
+__device__ __forceinline__ void p254_load8(uint32_t* v, const uint32_t* __restrict__ m, uint64_t rows,
+                                           uint64_t row, uint32_t col, uint32_t cols) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) v[i] = col + i < cols ? mont_reduce(m[uint64_t(col + i) * rows + row]) : 0u;
+}
+
+__global__ __launch_bounds__(kThreads) void p254_rows_kernel(uint32_t* out, const uint32_t* __restrict__ m,
+                                                           uint64_t rows, uint32_t cols) {
+  uint64_t row = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (row >= rows) return;
+  bn::Fr c[3] = {p254_zero(), p254_zero(), p254_zero()};
+  for (uint32_t col = 0; col < cols; col += 16) {
+    uint32_t v[8];
+    p254_load8(v, m, rows, row, col, cols);
+    c[1] = p254_pack8(v);
+    if (col + 8 < cols) {
+      p254_load8(v, m, rows, row, col + 8, cols);
+      c[2] = p254_pack8(v);
+    } else {
+      c[2] = p254_zero();
+    }
+    p254_mix(c);
+  }
+  uint32_t d[8];
+  p254_to_digest(c[0], d);
+  store_digest(out + row * 8, d);
+}
+
+__device__ __forceinline__ void p254_node(const uint32_t* src, uint32_t* d) {
+  uint32_t a[8], b[8];
+  const uint4* s4 = reinterpret_cast<const uint4*>(src);
+  uint4 x0 = s4[0], x1 = s4[1], x2 = s4[2], x3 = s4[3];
+  a[0] = x0.x; a[1] = x0.y; a[2] = x0.z; a[3] = x0.w; a[4] = x1.x; a[5] = x1.y; a[6] = x1.z; a[7] = x1.w;
+  b[0] = x2.x; b[1] = x2.y; b[2] = x2.z; b[3] = x2.w; b[4] = x3.x; b[5] = x3.y; b[6] = x3.z; b[7] = x3.w;
+  p254_hash_pair(a, b, d);
+}
+
+__global__ __launch_bounds__(kThreads) void p254_fold_kernel(uint32_t* io, uint64_t in_off, uint64_t out_off,
+                                                           uint64_t n) {
+  uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (i >= n) return;
+  uint32_t d[8];
+  p254_node(io + (in_off + 2 * i) * 8, d);
+  store_digest(io + (out_off + i) * 8, d);
 }
 
 // ---- SHA-256 ------------------------------------------------------------------
@@ -149,7 +199,9 @@ __global__ __launch_bounds__(kThreads) void fold_top_kernel(uint32_t* io, uint32
     for (uint32_t i = threadIdx.x; i < out; i += kThreads) {
       const uint32_t* src = io + (uint64_t(2 * out) + 2 * i) * 8;
       uint32_t d[8];
-      if (SUITE == 0) {
+      if (SUITE == 2) {
+        p254_node(src, d);
+      } else if (SUITE == 0) {
         uint32_t c[24];
 #pragma unroll
         for (int k = 0; k < 16; k++) c[k] = src[k];
@@ -179,41 +231,49 @@ __global__ __launch_bounds__(kThreads) void fold_top_kernel(uint32_t* io, uint32
 void hash_rows(hipStream_t s, int suite, uint32_t* out, const uint32_t* matrix, size_t rows, size_t cols) {
   if (rows == 0) return;
   R0_REQUIRE(cols < (1ull << 31), "hash_rows: too many columns");
+  R0_REQUIRE(suite >= 0 && suite <= 2, "hash_rows: unknown hash suite");
   // Poseidon2 permutation = 1356 modmul (8x24 S-boxes x4, 21 partial S-boxes x4, 21x24 diagonal)
   const double perms = double(rows) * (cols ? (cols + 15) / 16 : 1);
-  KScope ks(suite == 0 ? "hash_rows_poseidon2" : "hash_rows_sha256", double(rows) * (cols * 4 + 32),
+  static const char* names[3] = {"hash_rows_poseidon2", "hash_rows_sha256", "hash_rows_poseidon254"};
+  KScope ks(names[suite], double(rows) * (cols * 4 + 32),
             suite == 0 ? perms * kP2Modmuls : 0);
+  const dim3 grid(div_up(rows, kThreads)), block(kThreads);
   if (suite == 0)
-    hipLaunchKernelGGL(p2_rows_kernel, dim3(div_up(rows, kThreads)), dim3(kThreads), 0, s, out, matrix,
-                       uint64_t(rows), uint32_t(cols));
+    hipLaunchKernelGGL(p2_rows_kernel, grid, block, 0, s, out, matrix, uint64_t(rows), uint32_t(cols));
+  else if (suite == 1)
+    hipLaunchKernelGGL(sha_rows_kernel, grid, block, 0, s, out, matrix, uint64_t(rows), uint32_t(cols));
   else
-    hipLaunchKernelGGL(sha_rows_kernel, dim3(div_up(rows, kThreads)), dim3(kThreads), 0, s, out, matrix,
-                       uint64_t(rows), uint32_t(cols));
+    hipLaunchKernelGGL(p254_rows_kernel, grid, block, 0, s, out, matrix, uint64_t(rows), uint32_t(cols));
   HIP_OK(hipGetLastError());
 }
 
 void hash_fold(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t output_size) {
   if (output_size == 0) return;
   R0_REQUIRE(input_size == 2 * output_size, "hash_fold: input_size != 2*output_size");
+  R0_REQUIRE(suite >= 0 && suite <= 2, "hash_fold: unknown hash suite");
+  const dim3 grid(div_up(output_size, kThreads)), block(kThreads);
+  const uint64_t in = input_size, out = output_size;
   if (suite == 0)
-    hipLaunchKernelGGL(p2_fold_kernel, dim3(div_up(output_size, kThreads)), dim3(kThreads), 0, s, io,
-                       uint64_t(input_size), uint64_t(output_size), uint64_t(output_size));
+    hipLaunchKernelGGL(p2_fold_kernel, grid, block, 0, s, io, in, out, out);
+  else if (suite == 1)
+    hipLaunchKernelGGL(sha_fold_kernel, grid, block, 0, s, io, in, out, out);
   else
-    hipLaunchKernelGGL(sha_fold_kernel, dim3(div_up(output_size, kThreads)), dim3(kThreads), 0, s, io,
-                       uint64_t(input_size), uint64_t(output_size), uint64_t(output_size));
+    hipLaunchKernelGGL(p254_fold_kernel, grid, block, 0, s, io, in, out, out);
   HIP_OK(hipGetLastError());
 }
 
 // MerkleTreeProver::new (risc0/zkp/src/prove/merkle.rs:54-81): leaves, then every layer.
 void merkle_tree(hipStream_t s, int suite, uint32_t* nodes, const uint32_t* matrix, size_t rows, size_t cols) {
   hash_rows(s, suite, nodes + rows * 8, matrix, rows, cols);
-  KScope ks(suite == 0 ? "merkle_fold_poseidon2" : "merkle_fold_sha256", double(rows) * 32 * 1.5,
-            suite == 0 ? double(rows - 1) * kP2Modmuls : 0);
+  static const char* names[3] = {"merkle_fold_poseidon2", "merkle_fold_sha256", "merkle_fold_poseidon254"};
+  KScope ks(names[suite], double(rows) * 32 * 1.5, suite == 0 ? double(rows - 1) * kP2Modmuls : 0);
   size_t layer = rows / 2;
   for (; layer > 512; layer /= 2) hash_fold(s, suite, nodes, 2 * layer, layer);
   if (layer >= 1) {
-    if (suite == 0) hipLaunchKernelGGL(fold_top_kernel<0>, dim3(1), dim3(kThreads), 0, s, nodes, uint32_t(layer));
-    else hipLaunchKernelGGL(fold_top_kernel<1>, dim3(1), dim3(kThreads), 0, s, nodes, uint32_t(layer));
+    const dim3 grid(1), block(kThreads);
+    if (suite == 0) hipLaunchKernelGGL(fold_top_kernel<0>, grid, block, 0, s, nodes, uint32_t(layer));
+    else if (suite == 1) hipLaunchKernelGGL(fold_top_kernel<1>, grid, block, 0, s, nodes, uint32_t(layer));
+    else hipLaunchKernelGGL(fold_top_kernel<2>, grid, block, 0, s, nodes, uint32_t(layer));
     HIP_OK(hipGetLastError());
   }
 }

@@ -499,7 +499,7 @@ std::string last_profile() { return g_last_profile; }
 std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2, const uint32_t* code,
                                     const uint32_t* data, const uint32_t* accum, uint32_t* global,
                                     bool write_version, uint32_t version, std::vector<uint32_t>* mix_out) {
-  R0_REQUIRE(suite == 0 || suite == 1, "unknown hash suite");
+  R0_REQUIRE(suite >= 0 && suite <= 2, "unknown hash suite");
   R0_REQUIRE(po2 >= 2 && po2 <= 24, "po2 out of range");
   hipStream_t s = stream();
   stage_reset();

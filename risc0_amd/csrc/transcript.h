@@ -3,6 +3,7 @@
 // the transcript RNGs. Follows
 //   poseidon2/mod.rs:47-100,221-245, poseidon2/rng.rs:50-89   (suite "poseidon2")
 //   sha/cpu.rs:36-105, sha/rng.rs:24-101                      (suite "sha-256")
+//   poseidon_254/mod.rs:107-209                                (suite "poseidon_254")
 //   prove/write_iop.rs:24-76                                   (WriteIOP)
 #pragma once
 #include <stdint.h>
@@ -13,6 +14,7 @@
 
 #include "bb31.h"
 #include "poseidon2.h"
+#include "poseidon254.h"
 
 namespace r0 {
 
@@ -115,8 +117,17 @@ inline Digest p2_hash_words(const uint32_t* e, size_t n) {
   return d;
 }
 
+// poseidon_254 unpadded_hash over Elem::as_u32 of raw Montgomery words (mod.rs:107-133)
+inline Digest p254_hash_words(const uint32_t* e, size_t n) {
+  std::vector<uint32_t> v(n);
+  for (size_t i = 0; i < n; i++) v[i] = fp_decode(e[i]);
+  Digest d;
+  p254_hash_canonical(v.data(), n, d.w);
+  return d;
+}
+
 inline Digest hash_elems(int suite, const uint32_t* e, size_t n) {
-  return suite == 0 ? p2_hash_words(e, n) : sha::hash_words(e, n);
+  return suite == 0 ? p2_hash_words(e, n) : suite == 1 ? sha::hash_words(e, n) : p254_hash_words(e, n);
 }
 
 struct Rng {
@@ -189,7 +200,33 @@ struct ShaRng : Rng {
   }
 };
 
+// poseidon_254/mod.rs:146-209: draws read the canonical value of cell 2, then permute
+struct Poseidon254Rng : Rng {
+  bn::Fr cells[3] = {p254_zero(), p254_zero(), p254_zero()};
+  void mix(const Digest& d) override {
+    cells[1] = bn::add_norm(cells[1], p254_from_digest(d.w).l);
+    p254_mix(cells);
+  }
+  void next_source(uint32_t* w) {
+    p254_to_digest(cells[2], w);
+    p254_mix(cells);
+  }
+  uint32_t random_bits(size_t bits) override {
+    uint32_t w[8];
+    next_source(w);
+    return uint32_t((uint64_t(1) << bits) - 1) & w[0];
+  }
+  uint32_t random_elem() override {  // low 160 bits of the source, mod p
+    uint32_t w[8];
+    next_source(w);
+    uint64_t v = 0;
+    for (int i = 4; i >= 0; i--) v = ((v << 32) | w[i]) % kP;
+    return fp_encode(uint32_t(v));
+  }
+};
+
 inline std::unique_ptr<Rng> make_rng(int suite) {
+  if (suite == 2) return std::unique_ptr<Rng>(new Poseidon254Rng());
   if (suite == 0) return std::unique_ptr<Rng>(new Poseidon2Rng());
   return std::unique_ptr<Rng>(new ShaRng());
 }

@@ -16,8 +16,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # R0HIP_LIB selects an alternative build of the same library (tools/ experiments only)
 LIB_PATH = os.environ.get("R0HIP_LIB") or os.path.join(_HERE, "lib", "libr0hip.so")
 
-POSEIDON2, SHA256 = 0, 1
-SUITES = {"poseidon2": POSEIDON2, "sha-256": SHA256}
+POSEIDON2, SHA256, POSEIDON254 = 0, 1, 2
+SUITES = {"poseidon2": POSEIDON2, "sha-256": SHA256, "poseidon_254": POSEIDON254, "poseidon254": POSEIDON254}
 
 _lib = None
 u32p = C.POINTER(C.c_uint32)

@@ -122,7 +122,7 @@ def test_oracle_seal_matches_golden(oracle, case):
     assert digest(code, data, accum, glob) == case["inputs_sha256"]
     if oracle.ref_lib() is None:
         pytest.skip("oracle/_ref not built (needs the reference sources)")
-    s = oracle.POSEIDON2 if case["suite"] == "poseidon2" else oracle.SHA256
+    s = {"poseidon2": oracle.POSEIDON2, "sha-256": oracle.SHA256, "poseidon_254": oracle.POSEIDON254}[case["suite"]]
     seal, mix, _ = oracle.prove_segment(circuit, s, po2, code, data, accum, glob,
                                         version=2 if circuit == "rv32im" else None)
     assert seal.size == case["seal_words"]

@@ -14,14 +14,27 @@ P = 15 * 2**27 + 1
 
 @pytest.fixture(scope="module")
 def hal():
-    import risc0_amd as r
-    return r.HipHal("poseidon2")
+    return H("poseidon2")
 
 
 @pytest.fixture(scope="module")
 def hal_sha():
+    return H("sha-256")
+
+
+_HALS = {}
+
+
+def H(suite):
+    """one HipHal per hash suite ("poseidon2", "sha-256", "poseidon_254"), made on first use"""
     import risc0_amd as r
-    return r.HipHal("sha-256")
+    if suite not in _HALS:
+        _HALS[suite] = r.HipHal(suite)
+    return _HALS[suite]
+
+
+def S(oracle, suite):
+    return {"poseidon2": oracle.POSEIDON2, "sha-256": oracle.SHA256, "poseidon_254": oracle.POSEIDON254}[suite]
 
 
 def rnd(oracle, seed, n):
@@ -195,11 +208,10 @@ def test_gather_scatter_slice_prefix(hal, oracle):
     assert np.array_equal(d.to_numpy(), io)
 
 
-@pytest.mark.parametrize("suite", ["poseidon2", "sha-256"])
+@pytest.mark.parametrize("suite", ["poseidon2", "sha-256", "poseidon_254"])
 def test_hash_rows(hal, hal_sha, oracle, suite):
     # hal/mod.rs:575-589 (rows {1,2,3,4,10} x cols {16,32,64,128}) + ragged column counts
-    h = hal if suite == "poseidon2" else hal_sha
-    s = oracle.POSEIDON2 if suite == "poseidon2" else oracle.SHA256
+    h, s = H(suite), S(oracle, suite)
     rng = np.random.default_rng(11)
     shapes = [(r, c) for r in (1, 2, 3, 4, 10) for c in (16, 32, 64, 128)]
     shapes += [(4096, 1), (4096, 211), (1000, 103), (257, 17), (1 << 16, 16)]
@@ -220,15 +232,16 @@ def test_hash_rows(hal, hal_sha, oracle, suite):
     assert np.array_equal(nodes.to_numpy()[rows * 8:], ref)
 
 
-@pytest.mark.parametrize("suite", ["poseidon2", "sha-256"])
+@pytest.mark.parametrize("suite", ["poseidon2", "sha-256", "poseidon_254"])
 def test_hash_fold(hal, hal_sha, oracle, suite):
     # hal/mod.rs:551-573 (1024 inputs; digests of reduced words for Poseidon2)
-    h = hal if suite == "poseidon2" else hal_sha
-    s = oracle.POSEIDON2 if suite == "poseidon2" else oracle.SHA256
+    h, s = H(suite), S(oracle, suite)
     rng = np.random.default_rng(12)
     inputs = 1024
     io = np.zeros(inputs * 2 * 8, np.uint32)
     io[inputs * 8:] = (rng.integers(0, 2**32, inputs * 8, dtype=np.uint64) // 3).astype(np.uint32)
+    if suite == "poseidon_254":  # digests are canonical BN254 Fr values (< r < 2^254, mod.rs:94-98)
+        io[inputs * 8 + 7::8] &= 0x0FFFFFFF
     d = h.copy_from_digest("io", io)
     layer = inputs
     while layer > 1:
@@ -304,14 +317,13 @@ def test_eval_check(hal, oracle, circuit, po2):
 
 @pytest.mark.parametrize("circuit,suite,po2", [("rv32im", "poseidon2", 8), ("rv32im", "poseidon2", 11),
                                                ("rv32im", "sha-256", 9), ("recursion", "poseidon2", 9),
-                                               ("recursion", "sha-256", 8)])
+                                               ("recursion", "sha-256", 8), ("recursion", "poseidon_254", 8)])
 def test_prove_segment_seal_identical(hal, hal_sha, oracle, circuit, suite, po2):
     """Whole-segment seals (Vec<u32>) are bit-identical to the CPU oracle's."""
     if oracle.ref_lib() is None:
         pytest.skip("oracle/_ref not built")
     import risc0_amd as r
-    h = hal if suite == "poseidon2" else hal_sha
-    s = oracle.POSEIDON2 if suite == "poseidon2" else oracle.SHA256
+    h, s = H(suite), S(oracle, suite)
     d = oracle.load_circuit_json(circuit)
     rng = np.random.default_rng(0x5249534330 + po2)
     n = 1 << po2
@@ -345,7 +357,7 @@ def test_eval_check_golden(hal, oracle, case):
 def test_prove_segment_seal_golden(hal, hal_sha, oracle, case):
     import risc0_amd as r
     circuit, po2 = case["circuit"], case["po2"]
-    h = hal if case["suite"] == "poseidon2" else hal_sha
+    h = H(case["suite"])
     code, data, accum, glob = G.seal_inputs(oracle, circuit, po2)
     seal, mix = r.prove_segment(h, circuit, po2, dev(h, code), dev(h, data), dev(h, accum), dev(h, glob),
                                 version=2 if circuit == "rv32im" else None)
@@ -363,7 +375,7 @@ def test_prove_segments_concurrently_golden(hal, hal_sha, oracle):
     cases = G.INDEX["seals"]
     inputs = []
     for case in cases:
-        h = hal if case["suite"] == "poseidon2" else hal_sha
+        h = H(case["suite"])
         code, data, accum, glob = G.seal_inputs(oracle, case["circuit"], case["po2"])
         inputs.append((h, case, [dev(h, x) for x in (code, data, accum, glob)]))
     out = [None] * len(inputs)
@@ -385,15 +397,14 @@ def test_prove_segments_concurrently_golden(hal, hal_sha, oracle):
 
 
 @pytest.mark.parametrize("circuit,suite,po2", [("rv32im", "poseidon2", 20), ("rv32im", "poseidon2", 16),
-                                               ("recursion", "sha-256", 18)])
+                                               ("recursion", "sha-256", 18), ("recursion", "poseidon_254", 18)])
 def test_full_size_seal_verifies(hal, hal_sha, oracle, circuit, suite, po2):
     """At BASELINE sizes the CPU oracle cannot prove, the HIP seal passes the reference
     verifier's checks (tests/verifier.py: transcript, all Merkle openings, DEEP-ALI
     combination, every FRI fold and the final polynomial); flipped bits are rejected."""
     import risc0_amd as r
     import verifier
-    h = hal if suite == "poseidon2" else hal_sha
-    s = oracle.POSEIDON2 if suite == "poseidon2" else oracle.SHA256
+    h, s = H(suite), S(oracle, suite)
     d = oracle.load_circuit_json(circuit)
     rng = np.random.default_rng(0x5249534330 + po2)
     n = 1 << po2

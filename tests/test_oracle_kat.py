@@ -197,3 +197,43 @@ def test_merkle_params(rows, cols, q, layers, top):
             break
         top_layer = i
     assert lay == layers and (1 << top_layer) == top
+
+
+def test_poseidon254_kat(oracle):
+    # risc0/zkp/src/core/hash/poseidon_254/mod.rs:244-268 (p254_test_vectors)
+    S = oracle.POSEIDON254
+    inp = [E(oracle, [i])[0] for i in range(1, 6)]
+    d1 = oracle.hash_elems(S, np.array(inp, np.uint32))
+    d2 = oracle.hash_pair(S, d1, d1)
+    d3 = oracle.hash_pair(S, d1, d2)
+    r = oracle.Rng(S)
+    r.mix(d3)
+    out = [r.random_bits(7), int(oracle.decode(r.random_elem()))]
+    for _ in range(23):
+        inp.append(r.random_elem())
+    r.mix(oracle.hash_elems(S, np.array(inp, np.uint32)))
+    out.append(int(oracle.decode(r.random_elem())))
+    assert out == [5, 328085114, 726238606]
+
+
+def test_poseidon254_matches_bigint_restatement(oracle):
+    # the C++ oracle (4 x u64 Montgomery) against tests/p254_ref.py (Python integers)
+    import p254_ref
+    rng = np.random.default_rng(254)
+    for n in [0, 1, 7, 8, 9, 15, 16, 17, 31, 33, 64]:
+        e = oracle.rand_elems(rng, n)
+        got = oracle.hash_elems(oracle.POSEIDON254, e)
+        assert list(got) == p254_ref.hash_elems(oracle.decode(e).tolist()), n
+        ext = oracle.rand_elems(rng, 4 * n)
+        got = oracle.hash_ext_elems(oracle.POSEIDON254, ext)
+        assert list(got) == p254_ref.hash_elems(oracle.decode(ext).tolist()), n
+    a, b = p254_ref.hash_elems([1, 2]), p254_ref.hash_elems([3])
+    got = oracle.hash_pair(oracle.POSEIDON254, np.array(a, np.uint32), np.array(b, np.uint32))
+    assert list(got) == p254_ref.hash_pair(a, b)
+    r, q = oracle.Rng(oracle.POSEIDON254), p254_ref.Rng()
+    for k in range(6):
+        d = p254_ref.hash_elems([k])
+        r.mix(np.array(d, np.uint32))
+        q.mix(d)
+        assert r.random_bits(32) == q.random_bits(32)
+        assert int(oracle.decode(r.random_elem())) == q.random_elem()

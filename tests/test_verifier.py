@@ -7,7 +7,8 @@ import test_golden as G
 import verifier
 
 CASES = [("rv32im", "poseidon2", 8), ("rv32im", "sha-256", 9), ("recursion", "poseidon2", 9),
-         ("recursion", "sha-256", 8)]
+         ("recursion", "sha-256", 8), ("recursion", "poseidon_254", 8)]
+SUITES = {"poseidon2": 0, "sha-256": 1, "poseidon_254": 2}
 
 
 @pytest.mark.parametrize("circuit,suite,po2", CASES)
@@ -15,7 +16,7 @@ def test_verifier_accepts_oracle_seals(oracle, circuit, suite, po2):
     if oracle.ref_lib() is None:
         pytest.skip("oracle/_ref not built")
     code, data, accum, glob = G.seal_inputs(oracle, circuit, po2)
-    s = oracle.POSEIDON2 if suite == "poseidon2" else oracle.SHA256
+    s = SUITES[suite]
     seal, _mix, _ = oracle.prove_segment(circuit, s, po2, code, data, accum, glob,
                                          version=2 if circuit == "rv32im" else None)
     r = verifier.verify(oracle, circuit, seal, s, check_validity=True)

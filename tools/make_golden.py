@@ -28,7 +28,8 @@ EVAL_CASES = [("rv32im", 4, 0x4543_0004), ("rv32im", 6, 0x4543_0006), ("recursio
               ("recursion", 6, 0x4543_1006)]
 # (circuit, suite, po2) — whole-segment seals, seed 0x5249534330 + po2 (as tests/test_gpu_parity.py)
 SEAL_CASES = [("rv32im", "poseidon2", 8), ("rv32im", "poseidon2", 11), ("rv32im", "sha-256", 9),
-              ("recursion", "poseidon2", 9), ("recursion", "sha-256", 8)]
+              ("recursion", "poseidon2", 9), ("recursion", "sha-256", 8), ("recursion", "poseidon_254", 8)]
+SUITE_IDS = {"poseidon2": oracle.POSEIDON2, "sha-256": oracle.SHA256, "poseidon_254": oracle.POSEIDON254}
 
 
 def eval_inputs(circuit, po2, seed):
@@ -77,7 +78,7 @@ def main():
                                     "inputs_sha256": digest(*groups, mix, glob, pm)})
     for circuit, suite, po2 in SEAL_CASES:
         code, data, accum, glob = seal_inputs(circuit, po2)
-        s = oracle.POSEIDON2 if suite == "poseidon2" else oracle.SHA256
+        s = SUITE_IDS[suite]
         seal, mix, _ = oracle.prove_segment(circuit, s, po2, code, data, accum, glob,
                                             version=2 if circuit == "rv32im" else None)
         index["seals"].append({"circuit": circuit, "suite": suite, "po2": po2,
