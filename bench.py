@@ -33,6 +33,8 @@ def parse():
     ap.add_argument("--circuit", default="rv32im")
     ap.add_argument("--hashfn", default="poseidon2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e-steps", type=int, default=6,
+                    help="segments of the end-to-end (pinned host witness -> H2D -> seal) leg; 0 = skip")
     ap.add_argument("--cpu-po2", type=int, default=16, help="segment size of the bounded CPU baseline sample")
     ap.add_argument("--inflight", type=int, default=None,
                     help="segments in flight per GPU (host threads, each with its own HIP stream); "
@@ -68,7 +70,7 @@ def main():
     code, data, accum, glob = synthetic_witness(rng, circ, args.po2)
     dc, dd, da, dg = (hal.copy_from_elem(k, v) for k, v in
                       (("code", code), ("data", data), ("accum", accum), ("global", glob)))
-    del code, data, accum
+    host_witness = (code, data, accum, glob)
 
     from risc0_amd.segments import segments_for_rank, timed_segments
     # global segment ids of this rank (segment-per-GPU, no collective on the prove path);
@@ -114,13 +116,17 @@ def main():
     # kernel-level timing of the dominant kernel + roofline (rank 0)
     roofline = None
     cpu = None
+    e2e = None
     if rank == 0:
         kt = kernel_roofline(r, hal, args, circ, dc, dd, da, dg, version)
         roofline = kt
         phases = {key: round(v / args.steps, 3) for key, v in phase_tot.items()}
         print(json.dumps({"phases_ms": phases, "seal_words": int(seal.size)}), file=sys.stderr)
+        if args.e2e_steps > 0:
+            e2e = end_to_end(r, hal, args, host_witness, k, version)
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args, circ)
+    del host_witness
 
     if rank == 0:
         line = {
@@ -144,6 +150,8 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if e2e:
+            line["end_to_end"] = e2e
         print(json.dumps(line))
     if dist:
         dist.destroy_process_group()
@@ -185,6 +193,77 @@ def kernel_roofline(r, hal, args, circ, dc, dd, da, dg, version):
         out["valu"] = {"achieved": round(mm / 1e12, 3), "peak": MODMUL_PEAK / 1e12, "unit": "T modmul-equiv/s",
                        "frac": round(mm / MODMUL_PEAK, 4), "modmuls_per_launch": int(alg_mm / calls)}
     return out
+
+
+def end_to_end(r, hal, args, witness, k, version):
+    """PCIe-inclusive leg (prove core vs end-to-end): every segment's
+    witness groups start in page-locked host memory. An upload thread copies segment
+    i+1's groups into a free device buffer set (its own HIP stream) while the k prover
+    threads work on earlier segments (r0vm's GPU_QUEUE_DEPTH); k+1 buffer
+    sets circulate. Reported beside `value`, never as it."""
+    import ctypes
+    import queue
+    import threading
+    lib = r.lib()
+    hosts = []
+    for a in witness:
+        p = ctypes.c_void_p()
+        r.check(lib.r0hip_host_alloc(ctypes.byref(p), a.size * 4))
+        np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint32)), shape=(a.size,))[:] = a
+        hosts.append((p.value, a.size))
+    h2d_bytes = sum(n * 4 for _, n in hosts)
+    sets = [[hal.alloc_elem("w", n) for _, n in hosts] for _ in range(k + 1)]
+
+    def upload(bufs):
+        for (hp, n), d in zip(hosts, bufs):
+            r.check(lib.r0hip_memcpy_h2d(d.ptr, hp, n * 4))
+
+    def run(n):
+        free, ready = queue.Queue(), queue.Queue()
+        for st in sets:
+            free.put(st)
+
+        def uploader():
+            for _ in range(n):
+                st = free.get()
+                upload(st)
+                ready.put(st)
+
+        def prover(m):
+            for _ in range(m):
+                st = ready.get()
+                c, d, a, g = st
+                r.prove_segment(hal, args.circuit, args.po2, c, d, a, g, version=version)
+                free.put(st)
+
+        share = [n // k + (1 if i < n % k else 0) for i in range(k)]
+        ts = [threading.Thread(target=uploader)] + [threading.Thread(target=prover, args=(m,)) for m in share if m]
+        for t_ in ts:
+            t_.start()
+        for t_ in ts:
+            t_.join()
+
+    try:
+        run(k)  # warm every thread's stream and pool
+        hal.synchronize()
+        t0 = time.perf_counter()
+        upload(sets[0])
+        t_up = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        run(args.e2e_steps)
+        hal.synchronize()
+        t = time.perf_counter() - t0
+    finally:
+        for st in sets:
+            for b in st:
+                b.free()
+        for hp, _ in hosts:
+            r.check(lib.r0hip_host_free(hp))
+    return {"value": round(args.e2e_steps * (1 << args.po2) / t, 1), "unit": "cycles/s",
+            "ms_per_step": round(1000.0 * t / args.e2e_steps, 3), "steps": args.e2e_steps,
+            "h2d_bytes_per_segment": int(h2d_bytes), "h2d_GBps_alone": round(h2d_bytes / t_up / 1e9, 1),
+            "note": f"witness in pinned host memory; an upload thread fills {k + 1} device buffer sets "
+                    f"ahead of {k} prover threads, so H2D overlaps proving"}
 
 
 def pmc_traffic(family, calls, args):

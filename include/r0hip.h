@@ -38,6 +38,9 @@ const char* r0hip_memset32(void* d_dst, uint32_t value, size_t count); /* alloc_
 const char* r0hip_memcpy_h2d(void* d_dst, const void* h_src, size_t bytes);
 const char* r0hip_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes);
 const char* r0hip_memcpy_d2d(void* d_dst, const void* d_src, size_t bytes);
+/* page-locked host memory for full-rate witness uploads (cust's LockedBuffer role) */
+const char* r0hip_host_alloc(void** h_ptr, size_t bytes);
+const char* r0hip_host_free(void* h_ptr);
 const char* r0hip_synchronize(void);
 void r0hip_free_error(const char* err);
 

@@ -5,8 +5,8 @@ __graft_entry__.build()): hand-written HIP kernels for gfx950 behind the C ABI
 in include/r0hip.h, plus a C++ segment prover. This package is a thin ctypes
 mirror of the reference's `Hal` trait for tests and the benchmark.
 """
-from .hal import (POSEIDON2, SHA256, Buffer, HipHal, R0HipError, check, exported_symbols, kernel_times,
+from .hal import (POSEIDON2, POSEIDON254, SHA256, Buffer, HipHal, R0HipError, check, exported_symbols, kernel_times,
                   last_profile, lib, prove_segment, set_kernel_timing)
 
-__all__ = ["POSEIDON2", "SHA256", "Buffer", "HipHal", "R0HipError", "check", "exported_symbols", "last_profile",
+__all__ = ["POSEIDON2", "POSEIDON254", "SHA256", "Buffer", "HipHal", "R0HipError", "check", "exported_symbols", "last_profile",
            "lib", "prove_segment", "kernel_times", "set_kernel_timing"]

@@ -92,6 +92,12 @@ const char* r0hip_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes) {
 const char* r0hip_memcpy_d2d(void* d_dst, const void* d_src, size_t bytes) {
   return wrap([&] { HIP_OK(hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, stream())); });
 }
+const char* r0hip_host_alloc(void** h_ptr, size_t bytes) {
+  return wrap([&] { HIP_OK(hipHostMalloc(h_ptr, bytes, hipHostMallocDefault)); });
+}
+const char* r0hip_host_free(void* h_ptr) {
+  return wrap([&] { HIP_OK(hipHostFree(h_ptr)); });
+}
 const char* r0hip_synchronize(void) {
   return wrap([] {});
 }

@@ -14,7 +14,7 @@
 // Lazy values: r < 2^254 is 2^-7 of R, so REDC(T) < T/R + r stays a hair above r for every
 // T used here; cells stay below ~2.1r and are canonicalised only when a digest is written.
 // Column bounds (products of limbs < 2^30 where an unreduced sum fed a product) are
-// documented at each use and checked by tests/native/bn254_equiv.cpp on extreme inputs.
+// documented at each use and checked by tests/native/p254_host.cpp on extreme inputs.
 #pragma once
 #include "bb31.h"
 #include "poseidon254_consts.inc"
@@ -111,6 +111,22 @@ R0_HD Fr dot3_add(const uint32_t* m0, const uint32_t* m1, const uint32_t* m2, co
         return acc;
       },
       c);
+  return o;
+}
+
+// (w * s + e*R) / R for a constant w: one product and the addend e (limbs < 2^30) in the
+// high columns.
+R0_HD Fr mul_add(const uint32_t* w, const Fr& s, const uint32_t* e) {
+  Fr o;
+  redc(
+      o,
+      [&](int k, uint64_t acc) {
+#pragma unroll
+        for (int i = 0; i < 9; i++)
+          if (k - i >= 0 && k - i <= 8) acc = mac(s.l[i], w[k - i], acc);
+        return acc;
+      },
+      e);
   return o;
 }
 

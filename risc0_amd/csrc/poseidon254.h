@@ -4,42 +4,60 @@
 //   unpadded_hash               :107-133 (8 canonical BabyBear values per Fr, base p, rate 2)
 //   hash_pair                   :136-142
 // Cells live in bn254.h's lazy Montgomery form. Each round's MDS product and the next
-// round's constants share one reduction: REDC(sum_j M_ij s_j + RC_i * R).
+// round's constants share one reduction: REDC(sum_j M_ij s_j + RC_i * R); partial rounds
+// use the equivalent sparse matrices (Poseidon paper, appendix B).
 #pragma once
 #include "bn254.h"
 
 namespace r0 {
 
 #if defined(__HIP_DEVICE_COMPILE__)
-__constant__ static const uint32_t kP254Rc[153][9] = P254_RC_L29;
-__constant__ static const uint32_t kP254Mds[9][9] = P254_MDS_L29;
-__constant__ static const uint32_t kP254Pack[8][9] = P254_PACK_L29;
+#define R0_P254_TABLE __constant__ static const
 #else
-static const uint32_t kP254Rc[153][9] = P254_RC_L29;
-static const uint32_t kP254Mds[9][9] = P254_MDS_L29;
-static const uint32_t kP254Pack[8][9] = P254_PACK_L29;
+#define R0_P254_TABLE static const
 #endif
+R0_P254_TABLE uint32_t kP254Rc0[3][9] = P254_RC0_L29;
+R0_P254_TABLE uint32_t kP254FullMat[2][9][9] = P254_FULL_MAT_L29;
+R0_P254_TABLE uint32_t kP254FullRc[8][3][9] = P254_FULL_RC_L29;
+R0_P254_TABLE uint32_t kP254Partial[42][8][9] = P254_PARTIAL_L29;
+R0_P254_TABLE uint32_t kP254Pack[8][9] = P254_PACK_L29;
+#undef R0_P254_TABLE
 
 R0_HD bn::Fr p254_sbox(const bn::Fr& x) { return bn::sqr(bn::sqr(bn::sqr(x))); }
 
-// c: Montgomery cells < 2.2r with limbs < 2^29. Rounds stay rolled (a round is ~2.7k
-// instructions; unrolled, the 50 rounds would not fit the instruction cache).
+// c: Montgomery cells, limbs < 2^29. The 42 partial rounds use the sparse equivalent
+// matrices of tools/extract_poseidon254.py: cell 0 takes a 3-term row, cells 1 and 2 take
+// w_i * s0 + cell_i, so a partial round costs 5 products instead of 9. Cells 1 and 2 are
+// not reduced there and grow by < 2.1r a round, to < 88r < 2^260.1 before the next full
+// round's S-boxes (which bring them back below 2.1r): all within bn254.h's column bounds.
+// Rounds stay rolled (one full round is ~2.7k instructions, the partial round ~1.3k).
 R0_HD void p254_mix(bn::Fr* c) {
 #pragma unroll
-  for (int i = 0; i < 3; i++) c[i] = bn::add_norm(c[i], kP254Rc[i]);
+  for (int i = 0; i < 3; i++) c[i] = bn::add_norm(c[i], kP254Rc0[i]);
 #pragma unroll 1
-  for (int r = 0; r < 50; r++) {
-    const bool full = r < 4 || r >= 46;
-    c[0] = p254_sbox(c[0]);
-    if (full) {
-      c[1] = p254_sbox(c[1]);
-      c[2] = p254_sbox(c[2]);
+  for (int f = 0; f < 8; f++) {
+    if (f == 4) {
+#pragma unroll 1
+      for (int k = 0; k < 42; k++) {
+        const uint32_t* t = &kP254Partial[k][0][0];
+        const bn::Fr s0 = p254_sbox(c[0]);
+        uint32_t e1[9], e2[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+          e1[i] = c[1].l[i] + t[54 + i];
+          e2[i] = c[2].l[i] + t[63 + i];
+        }
+        c[0] = bn::dot3_add(t, t + 9, t + 18, s0, c[1], c[2], t + 45);
+        c[1] = bn::mul_add(t + 27, s0, e1);
+        c[2] = bn::mul_add(t + 36, s0, e2);
+      }
     }
-    const bn::Fr s0 = c[0], s1 = c[1], s2 = c[2];
-    // the next round's constants (row 150 of the table is zero: nothing after round 49)
-    c[0] = bn::dot3_add(kP254Mds[0], kP254Mds[1], kP254Mds[2], s0, s1, s2, kP254Rc[3 * r + 3]);
-    c[1] = bn::dot3_add(kP254Mds[3], kP254Mds[4], kP254Mds[5], s0, s1, s2, kP254Rc[3 * r + 4]);
-    c[2] = bn::dot3_add(kP254Mds[6], kP254Mds[7], kP254Mds[8], s0, s1, s2, kP254Rc[3 * r + 5]);
+    const bn::Fr s0 = p254_sbox(c[0]), s1 = p254_sbox(c[1]), s2 = p254_sbox(c[2]);
+    const uint32_t* m = &kP254FullMat[f == 3 ? 1 : 0][0][0];
+    const uint32_t* n = &kP254FullRc[f][0][0];
+    c[0] = bn::dot3_add(m, m + 9, m + 18, s0, s1, s2, n);
+    c[1] = bn::dot3_add(m + 27, m + 36, m + 45, s0, s1, s2, n + 9);
+    c[2] = bn::dot3_add(m + 54, m + 63, m + 72, s0, s1, s2, n + 18);
   }
 }
 

@@ -67,6 +67,10 @@ def test_bn254_poseidon254_host(tmp_path):
     a, b = ref.hash_elems([7]), ref.hash_elems([8, 9])
     lines.append("pair " + " ".join(map(str, a + b)))
     checks.append(("pair", ref.hash_pair(a, b)))
+    for _ in range(300):  # random and extreme canonical digests through whole permutations
+        a, b = (ref.to_words(rnd.choice([0, r - 1, rnd.randrange(r)])) for _ in range(2))
+        lines.append("pair " + " ".join(map(str, a + b)))
+        checks.append(("pair", ref.hash_pair(a, b)))
     out = subprocess.run([str(exe)], input="\n".join(lines) + "\n", capture_output=True, text=True, check=True)
     rinv = pow(R, -1, r)
     res = out.stdout.split("\n")
