@@ -251,6 +251,9 @@ WAVES = int(os.environ.get("EC_WAVES", "2"))
 # wave cycles), not by the count of VALU instructions.
 # EC_CANON=1: every Fp/FpExt result canonical; EC_CANON=0: the lazy range analysis below
 CANON_ALL = os.environ.get("EC_CANON", "1") == "1"
+# EC_CANON_FORCE=0/1 overrides the tuned per-kernel mode (tools/tune_ec_canon.py variants)
+if "EC_CANON_FORCE" in os.environ:
+    CANON_ALL = os.environ["EC_CANON_FORCE"] == "1"
 # EC_SADDR=0: taps addressed as A.a[arg][col * domain + row] (64-bit VALU address per load);
 # EC_SADDR=1: scalar column base (A.cp) + one 32-bit lane offset per `back`
 SADDR = os.environ.get("EC_SADDR", "0") == "1"
@@ -451,6 +454,8 @@ def emit(circuit, outdir, budget, host=False):
     one, two, mone = enc(1), enc(2), enc(P - 1)
 
     for ki, items in enumerate(kernels):
+        # per-kernel arithmetic mode: tuned "canon" (1 canonical, 0 range analysis) or EC_CANON
+        kcanon = CANON_ALL if "EC_CANON_FORCE" in os.environ else bool(tune.get(ki, {}).get("canon", CANON_ALL))
         roots = []
         for it in items:
             roots += [it[3]] if it[2] == "mat" else term_roots(it[3])
@@ -519,10 +524,10 @@ def emit(circuit, outdir, budget, host=False):
             return (a, b) if a[1] >= b[1] else (b, a)
 
         def out(ty, expr, M, name=None):
-            """declare a value; CANON_ALL reduces every result (the pre-range-analysis
-            arithmetic, kept for A/B runs)"""
+            """declare a value; in canonical kernels (kcanon) every result is reduced (the
+            pre-range-analysis arithmetic), otherwise only where the range analysis needs it"""
             nm = name or fresh()
-            if CANON_ALL:
+            if kcanon:
                 r = "lred" if ty == "f" else "xred"
                 while M >= P:
                     expr, M = f"{r}({expr})", max(PM, M - P)
@@ -648,7 +653,7 @@ def emit(circuit, outdir, budget, host=False):
             if bd + U32 * P > U64 or redc_max(bd) > U32:
                 expr, bd = f"acc_fold({expr})", fold_max(bd)
             M = redc_max(bd)
-            if CANON_ALL:
+            if kcanon:
                 if bd >= RED:
                     expr = f"acc_fold({expr})"
                 w(f"  const FpExt {name} = acc_red({expr});")
@@ -662,7 +667,7 @@ def emit(circuit, outdir, budget, host=False):
             return f"acc_red({expr})"
 
         acc_state = {"n": 0, "b": 0}
-        kwaves = tune.get(ki, {}).get("waves", WAVES)
+        kwaves = int(os.environ.get("EC_WAVES_OVERRIDE", tune.get(ki, {}).get("waves", WAVES)))
         kpf = tune.get(ki, {}).get("pf", PF)
         if ORDER == "dfs":
             byid_ = pg.byid
