@@ -67,10 +67,21 @@ def main():
 
     # inputs resident in HBM before the timed region: one witness set per rank
     rng = np.random.default_rng(0x5249534330 + rank)
-    code, data, accum, glob = synthetic_witness(rng, circ, args.po2)
-    dc, dd, da, dg = (hal.copy_from_elem(k, v) for k, v in
-                      (("code", code), ("data", data), ("accum", accum), ("global", glob)))
-    host_witness = (code, data, accum, glob)
+    if args.po2 <= 22:
+        code, data, accum, glob = synthetic_witness(rng, circ, args.po2)
+        dc, dd, da, dg = (hal.copy_from_elem(k, v) for k, v in
+                          (("code", code), ("data", data), ("accum", accum), ("global", glob)))
+        host_witness = (code, data, accum, glob)
+    else:
+        # above po2=22 the host draw + upload would take minutes: draw on the device
+        # (r0hip_fill_uniform, same distribution); no end-to-end leg at these sizes
+        glob = synthetic_witness(rng, {"group_sizes": [0, 0, 0], "output_size": circ["output_size"]}, 0)[3]
+        n = 1 << args.po2
+        dc, dd, da = (hal.alloc_elem(k, circ["group_sizes"][g] * n) for k, g in (("code", 1), ("data", 2), ("accum", 0)))
+        for i, b in enumerate((dc, dd, da)):
+            r.check(r.lib().r0hip_fill_uniform(b.ptr, b.size, 0x5249534330 + rank * 8 + i))
+        dg = hal.copy_from_elem("global", glob)
+        host_witness = None
 
     from risc0_amd.segments import segments_for_rank, timed_segments
     # global segment ids of this rank (segment-per-GPU, no collective on the prove path);
@@ -122,7 +133,7 @@ def main():
         roofline = kt
         phases = {key: round(v / args.steps, 3) for key, v in phase_tot.items()}
         print(json.dumps({"phases_ms": phases, "seal_words": int(seal.size)}), file=sys.stderr)
-        if args.e2e_steps > 0:
+        if args.e2e_steps > 0 and host_witness is not None:
             e2e = end_to_end(r, hal, args, host_witness, k, version)
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args, circ)

@@ -93,6 +93,9 @@ const char* r0hip_gather_sample(uint32_t* d_dst, const uint32_t* d_src, size_t i
 const char* r0hip_scatter(uint32_t* d_into, const uint32_t* d_index, const uint32_t* d_offsets,
                           const uint32_t* d_values, size_t cycles);
 const char* r0hip_prefix_products(uint32_t* d_io, size_t count);
+/* not a reference symbol: synthetic witness words (uniform canonical BabyBear values from a
+ * counter hash of seed and index) for benches and tests at full size */
+const char* r0hip_fill_uniform(uint32_t* d_out, size_t count, uint64_t seed);
 
 /* ---- hashing (sppark_poseidon2_{rows,fold}, sppark_poseidon254_{rows,fold}, risc0_zkp_cuda_sha_{rows,fold};
  * sys/src/cuda.rs:49-72) ---- */

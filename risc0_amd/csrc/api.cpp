@@ -236,6 +236,9 @@ const char* r0hip_scatter(uint32_t* d_into, const uint32_t* d_index, const uint3
 const char* r0hip_prefix_products(uint32_t* d_io, size_t count) {
   return wrap([&] { prefix_products(stream(), d_io, count); });
 }
+const char* r0hip_fill_uniform(uint32_t* d_out, size_t count, uint64_t seed) {
+  return wrap([&] { fill_uniform(stream(), d_out, count, seed); });
+}
 
 const char* r0hip_hash_rows(int suite, uint32_t* d_out, const uint32_t* d_matrix, size_t rows, size_t cols) {
   return wrap([&] {

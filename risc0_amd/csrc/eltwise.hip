@@ -33,6 +33,18 @@ __global__ void zeroize_kernel(uint32_t* io, uint64_t n) {
   uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (i < n && io[i] == 0xffffffffu) io[i] = 0;
 }
+// synthetic witness words (uniform canonical BabyBear values): a
+// splitmix64 counter hash of (seed, index), reduced mod p — for benches and tests at sizes
+// whose host generation and upload would dominate
+__global__ void fill_uniform_kernel(uint32_t* o, uint64_t n, uint64_t seed) {
+  uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (i >= n) return;
+  uint64_t z = seed + (i + 1) * 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  z ^= z >> 31;
+  o[i] = uint32_t(z % kP);
+}
 // cpu.rs:475-500: out[k*count + idx] = (sum_i in[i*count + idx])[k]
 __global__ void sum_extelem_kernel(uint32_t* out, const uint32_t* in, uint64_t count, uint32_t to_add) {
   uint64_t idx = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
@@ -379,6 +391,11 @@ void eltwise_copy(hipStream_t s, uint32_t* out, const uint32_t* in, size_t n) {
 void eltwise_zeroize(hipStream_t s, uint32_t* io, size_t n) {
   if (!n) return;
   hipLaunchKernelGGL(zeroize_kernel, dim3(div_up(n, kThreads)), dim3(kThreads), 0, s, io, uint64_t(n));
+  HIP_OK(hipGetLastError());
+}
+void fill_uniform(hipStream_t s, uint32_t* out, size_t n, uint64_t seed) {
+  if (!n) return;
+  hipLaunchKernelGGL(fill_uniform_kernel, dim3(div_up(n, kThreads)), dim3(kThreads), 0, s, out, uint64_t(n), seed);
   HIP_OK(hipGetLastError());
 }
 void eltwise_sum_extelem(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count, size_t to_add) {

@@ -78,6 +78,7 @@ void merkle_tree(hipStream_t s, int suite, uint32_t* nodes, const uint32_t* matr
 void eltwise_add(hipStream_t s, uint32_t* out, const uint32_t* a, const uint32_t* b, size_t n);
 void eltwise_copy(hipStream_t s, uint32_t* out, const uint32_t* in, size_t n);
 void eltwise_zeroize(hipStream_t s, uint32_t* io, size_t n);
+void fill_uniform(hipStream_t s, uint32_t* out, size_t n, uint64_t seed);
 void eltwise_sum_extelem(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count, size_t to_add);
 void fri_fold(hipStream_t s, uint32_t* out, const uint32_t* in, FpExt mix, size_t count);
 void gather_sample(hipStream_t s, uint32_t* dst, const uint32_t* src, size_t idx, size_t size, size_t stride);

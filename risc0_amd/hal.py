@@ -53,6 +53,7 @@ def _declare(L):
         "r0hip_memcpy_d2d": [vp, vp, sz],
         "r0hip_host_alloc": [C.POINTER(vp), sz],
         "r0hip_host_free": [vp],
+        "r0hip_fill_uniform": [vp, sz, C.c_uint64],
         "r0hip_synchronize": [],
         "r0hip_batch_expand_into_evaluate_ntt": [vp, vp, sz, C.c_uint32, C.c_uint32],
         "r0hip_batch_interpolate_ntt": [vp, sz, C.c_uint32],

@@ -396,12 +396,52 @@ def test_prove_segments_concurrently_golden(hal, hal_sha, oracle):
         assert [int(x) for x in mix] == case["mix"]
 
 
+def test_prove_segment_from_pinned_host(oracle):
+    """The end-to-end path of bench.py's `end_to_end` leg: witness groups in page-locked
+    host memory (r0hip_host_alloc), uploaded with r0hip_memcpy_h2d, then proved; the seal
+    matches its golden fixture."""
+    import ctypes
+
+    import risc0_amd as r
+    case = G.INDEX["seals"][0]
+    h = H(case["suite"])
+    lib = r.lib()
+    bufs, hosts = [], []
+    try:
+        for a in G.seal_inputs(oracle, case["circuit"], case["po2"]):
+            p = ctypes.c_void_p()
+            r.check(lib.r0hip_host_alloc(ctypes.byref(p), a.size * 4))
+            hosts.append(p.value)
+            np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint32)), shape=(a.size,))[:] = a
+            b = h.alloc_elem("w", a.size)
+            r.check(lib.r0hip_memcpy_h2d(b.ptr, p.value, a.size * 4))
+            bufs.append(b)
+        seal, mix = r.prove_segment(h, case["circuit"], case["po2"], *bufs,
+                                    version=2 if case["circuit"] == "rv32im" else None)
+    finally:
+        for p in hosts:
+            r.check(lib.r0hip_host_free(p))
+    assert G.digest(seal) == case["seal_sha256"]
+    assert [int(x) for x in mix] == case["mix"]
+
+
+def device_witness(h, n, seed):
+    """Uniform canonical BabyBear words generated on the device (r0hip_fill_uniform) for
+    sizes whose host generation would take minutes."""
+    import risc0_amd as r
+    b = h.alloc_elem("w", n)
+    r.check(r.lib().r0hip_fill_uniform(b.ptr, n, seed))
+    return b
+
+
 @pytest.mark.parametrize("circuit,suite,po2", [("rv32im", "poseidon2", 20), ("rv32im", "poseidon2", 16),
-                                               ("recursion", "sha-256", 18), ("recursion", "poseidon_254", 18)])
+                                               ("recursion", "sha-256", 18), ("recursion", "poseidon_254", 18),
+                                               ("rv32im", "poseidon2", 24)])
 def test_full_size_seal_verifies(hal, hal_sha, oracle, circuit, suite, po2):
-    """At BASELINE sizes the CPU oracle cannot prove, the HIP seal passes the reference
-    verifier's checks (tests/verifier.py: transcript, all Merkle openings, DEEP-ALI
-    combination, every FRI fold and the final polynomial); flipped bits are rejected."""
+    """At BASELINE sizes the CPU oracle cannot prove (configs[1] po2=20 and configs[2] po2=24,
+    the maximum segment), the HIP seal passes the reference verifier's checks
+    (tests/verifier.py: transcript, all Merkle openings, DEEP-ALI combination, every FRI
+    fold and the final polynomial); flipped bits are rejected."""
     import risc0_amd as r
     import verifier
     h, s = H(suite), S(oracle, suite)
@@ -409,9 +449,14 @@ def test_full_size_seal_verifies(hal, hal_sha, oracle, circuit, suite, po2):
     rng = np.random.default_rng(0x5249534330 + po2)
     n = 1 << po2
     gs = d["group_sizes"]
-    bufs = [dev(h, oracle.rand_elems(rng, gs[g] * n)) for g in (1, 2, 0)]
+    if po2 >= 22:
+        bufs = [device_witness(h, gs[g] * n, 0x5249534330 + po2 + g) for g in (1, 2, 0)]
+    else:
+        bufs = [dev(h, oracle.rand_elems(rng, gs[g] * n)) for g in (1, 2, 0)]
     glob = dev(h, oracle.rand_elems(rng, d["output_size"]))
     seal, _mix = r.prove_segment(h, circuit, po2, *bufs, glob, version=2 if circuit == "rv32im" else None)
+    for b in bufs:
+        b.free()
     res = verifier.verify(oracle, circuit, seal, s)
     assert res["po2"] == po2
     for where in (seal.size // 3, seal.size - 5):
