@@ -207,74 +207,37 @@ def kernel_roofline(r, hal, args, circ, dc, dd, da, dg, version):
 
 
 def end_to_end(r, hal, args, witness, k, version):
-    """PCIe-inclusive leg (prove core vs end-to-end): every segment's
-    witness groups start in page-locked host memory. An upload thread copies segment
-    i+1's groups into a free device buffer set (its own HIP stream) while the k prover
-    threads work on earlier segments (r0vm's GPU_QUEUE_DEPTH); k+1 buffer
-    sets circulate. Reported beside `value`, never as it."""
+    """PCIe-inclusive leg (prove core vs end-to-end) through the native
+    segment pipeline (r0hip_prove_segments): every segment's witness groups start in
+    page-locked host memory; an uploader thread fills one of k+1 device buffer sets while
+    k prover threads run (r0vm's GPU_QUEUE_DEPTH). Reported beside
+    `value`, never as it."""
     import ctypes
-    import queue
-    import threading
     lib = r.lib()
     hosts = []
-    for a in witness:
-        p = ctypes.c_void_p()
-        r.check(lib.r0hip_host_alloc(ctypes.byref(p), a.size * 4))
-        np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint32)), shape=(a.size,))[:] = a
-        hosts.append((p.value, a.size))
-    h2d_bytes = sum(n * 4 for _, n in hosts)
-    sets = [[hal.alloc_elem("w", n) for _, n in hosts] for _ in range(k + 1)]
-
-    def upload(bufs):
-        for (hp, n), d in zip(hosts, bufs):
-            r.check(lib.r0hip_memcpy_h2d(d.ptr, hp, n * 4))
-
-    def run(n):
-        free, ready = queue.Queue(), queue.Queue()
-        for st in sets:
-            free.put(st)
-
-        def uploader():
-            for _ in range(n):
-                st = free.get()
-                upload(st)
-                ready.put(st)
-
-        def prover(m):
-            for _ in range(m):
-                st = ready.get()
-                c, d, a, g = st
-                r.prove_segment(hal, args.circuit, args.po2, c, d, a, g, version=version)
-                free.put(st)
-
-        share = [n // k + (1 if i < n % k else 0) for i in range(k)]
-        ts = [threading.Thread(target=uploader)] + [threading.Thread(target=prover, args=(m,)) for m in share if m]
-        for t_ in ts:
-            t_.start()
-        for t_ in ts:
-            t_.join()
-
     try:
-        run(k)  # warm every thread's stream and pool
-        hal.synchronize()
+        for a in witness:
+            p = ctypes.c_void_p()
+            r.check(lib.r0hip_host_alloc(ctypes.byref(p), a.size * 4))
+            hosts.append(p.value)
+            np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint32)), shape=(a.size,))[:] = a
+        h2d_bytes = sum(a.size * 4 for a in witness)
+        jobs = lambda n: [tuple(hosts)] * n
+        r.prove_segments(hal, args.circuit, args.po2, jobs(k), version=version, in_flight=k)  # warm
         t0 = time.perf_counter()
-        upload(sets[0])
-        t_up = time.perf_counter() - t0
+        r.prove_segments(hal, args.circuit, args.po2, jobs(1), version=version, in_flight=1)
+        t_one = time.perf_counter() - t0
         t0 = time.perf_counter()
-        run(args.e2e_steps)
-        hal.synchronize()
+        r.prove_segments(hal, args.circuit, args.po2, jobs(args.e2e_steps), version=version, in_flight=k)
         t = time.perf_counter() - t0
     finally:
-        for st in sets:
-            for b in st:
-                b.free()
-        for hp, _ in hosts:
+        for hp in hosts:
             r.check(lib.r0hip_host_free(hp))
     return {"value": round(args.e2e_steps * (1 << args.po2) / t, 1), "unit": "cycles/s",
             "ms_per_step": round(1000.0 * t / args.e2e_steps, 3), "steps": args.e2e_steps,
-            "h2d_bytes_per_segment": int(h2d_bytes), "h2d_GBps_alone": round(h2d_bytes / t_up / 1e9, 1),
-            "note": f"witness in pinned host memory; an upload thread fills {k + 1} device buffer sets "
-                    f"ahead of {k} prover threads, so H2D overlaps proving"}
+            "h2d_bytes_per_segment": int(h2d_bytes), "ms_one_segment_unpipelined": round(1000.0 * t_one, 1),
+            "note": f"witness in pinned host memory; native pipeline (r0hip_prove_segments): an uploader fills "
+                    f"{k + 1} device buffer sets ahead of {k} prover threads, so H2D overlaps proving"}
 
 
 def pmc_traffic(family, calls, args):

@@ -120,6 +120,28 @@ const char* r0hip_prove_segment(const char* circuit, int suite, uint32_t po2, co
                                 const uint32_t* d_data, const uint32_t* d_accum, uint32_t* d_global,
                                 int write_version, uint32_t version, uint32_t* h_seal, size_t seal_cap,
                                 size_t* seal_len, uint32_t* h_mix_out);
+/* ---- segment pipeline (r0vm's per-GPU worker queue, r0vm/src/actors/worker.rs:75-76, over the
+ * zkvm's per-segment prove loop, zkvm/src/host/server/prove/prover_impl.rs:84-94) ----
+ * Proves njobs segments of one (circuit, suite, po2) from HOST witness buffers: an uploader
+ * thread copies the next job's groups into one of in_flight+1 device buffer sets while
+ * in_flight prover threads run r0hip_prove_segment's core on their own streams. Host
+ * buffers should be page-locked (r0hip_host_alloc) for full PCIe rate. Per job: seal into
+ * h_seal (seal_cap words), its length in seal_len, mix values into h_mix_out (optional),
+ * and error = NULL or a malloc'd message (free() it). Returns NULL when every job succeeded. */
+typedef struct r0hip_segment_job {
+  const uint32_t* h_code;
+  const uint32_t* h_data;
+  const uint32_t* h_accum;
+  const uint32_t* h_global; /* output_size words; zeroized on the device copy only */
+  uint32_t* h_seal;
+  size_t seal_cap;
+  size_t seal_len;
+  uint32_t* h_mix_out;
+  const char* error;
+} r0hip_segment_job;
+const char* r0hip_prove_segments(const char* circuit, int suite, uint32_t po2, int write_version, uint32_t version,
+                                 r0hip_segment_job* jobs, size_t njobs, uint32_t in_flight);
+
 /* kernel-level timing with HIP events on the library stream: enable, run, then read
  * "name=total_ms:calls:alg_bytes;..." (alg_bytes = algorithmic HBM bytes) */
 const char* r0hip_set_kernel_timing(int on);

@@ -1,0 +1,157 @@
+// Segment pipeline: many segments through one GPU with the witness upload of the next
+// segment overlapped with the proofs in flight — the queue r0vm's GPU worker keeps
+// (GPU_QUEUE_DEPTH=2, risc0/r0vm/src/actors/worker.rs:75-76) and the per-segment loop of
+// the zkvm prover (risc0/zkvm/src/host/server/prove/prover_impl.rs:84-94), native here.
+//
+// One uploader thread copies a job's witness groups from host memory (page-locked for
+// full PCIe rate) into a free device buffer set on its own stream; `in_flight` prover
+// threads each take a filled set, run the whole-segment prover on their own stream
+// (runtime.cpp gives every host thread its own stream, pool and staging), write the
+// seal, and hand the set back. in_flight + 1 sets circulate, so an upload is always
+// running ahead while the GPU proves. Each job reports its own error.
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/r0hip.h"
+#include "circuit.h"
+#include "devmem.h"
+#include "runtime.h"
+
+namespace r0 {
+std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2, const uint32_t* code,
+                                    const uint32_t* data, const uint32_t* accum, uint32_t* global,
+                                    bool write_version, uint32_t version, std::vector<uint32_t>* mix_out);
+
+namespace {
+
+struct BufSet {
+  DevBuf g[4];  // code, data, accum, global
+  size_t job = 0;
+};
+
+// a bounded queue of set indices
+struct Queue {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<long> q;
+  void put(long v) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      q.push_back(v);
+    }
+    cv.notify_one();
+  }
+  long get() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return !q.empty(); });
+    long v = q.front();
+    q.pop_front();
+    return v;
+  }
+};
+
+char* dup_msg(const char* m) {
+  size_t n = strlen(m) + 1;
+  char* p = static_cast<char*>(malloc(n));
+  if (p) memcpy(p, m, n);
+  return p;
+}
+
+}  // namespace
+}  // namespace r0
+
+using namespace r0;
+
+extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint32_t po2, int write_version,
+                                            uint32_t version, r0hip_segment_job* jobs, size_t njobs,
+                                            uint32_t in_flight) {
+  try {
+    const CircuitDef* c = find_circuit(circuit ? circuit : "");
+    R0_REQUIRE(c, std::string("unknown circuit ") + (circuit ? circuit : "(null)"));
+    R0_REQUIRE(suite >= 0 && suite <= 2, "unknown hash suite");
+    R0_REQUIRE(po2 >= 1 && po2 <= 24, "po2 out of range");
+    R0_REQUIRE(njobs == 0 || jobs, "jobs is NULL");
+    ensure_init();
+    if (njobs == 0) return nullptr;
+    const size_t k = std::max<size_t>(1, std::min<size_t>(in_flight ? in_flight : 2, njobs));
+    const size_t n = size_t(1) << po2;
+    // group_sizes: accum 0, code 1, data 2 (the reference's register-group order)
+    const size_t words[4] = {c->group_sizes[1] * n, c->group_sizes[2] * n, c->group_sizes[0] * n, c->output_size};
+    std::vector<BufSet> sets(k + 1);
+    for (auto& s : sets)
+      for (int g = 0; g < 4; g++) s.g[g] = DevBuf(words[g]);
+    HIP_OK(hipDeviceSynchronize());  // allocations complete before other streams use them
+    for (size_t i = 0; i < njobs; i++) {
+      jobs[i].error = nullptr;
+      jobs[i].seal_len = 0;
+    }
+
+    Queue free_q, ready_q;
+    for (size_t s = 0; s < sets.size(); s++) free_q.put(long(s));
+
+    std::thread uploader([&] {
+      for (size_t i = 0; i < njobs; i++) {
+        long s = free_q.get();
+        BufSet& b = sets[s];
+        b.job = i;
+        try {
+          ensure_init();
+          const uint32_t* src[4] = {jobs[i].h_code, jobs[i].h_data, jobs[i].h_accum, jobs[i].h_global};
+          for (int g = 0; g < 4; g++) {
+            R0_REQUIRE(src[g], "witness group pointer is NULL");
+            HIP_OK(hipMemcpyAsync(b.g[g].p, src[g], words[g] * 4, hipMemcpyHostToDevice, stream()));
+          }
+          HIP_OK(hipStreamSynchronize(stream()));
+        } catch (const std::exception& e) {
+          jobs[i].error = dup_msg(e.what());
+        }
+        ready_q.put(s);
+      }
+      for (size_t t = 0; t < k; t++) ready_q.put(-1);  // one stop token per prover
+    });
+
+    std::vector<std::thread> provers;
+    for (size_t t = 0; t < k; t++) {
+      provers.emplace_back([&] {
+        for (;;) {
+          long s = ready_q.get();
+          if (s < 0) return;
+          BufSet& b = sets[s];
+          r0hip_segment_job& j = jobs[b.job];
+          if (!j.error) {
+            try {
+              ensure_init();
+              std::vector<uint32_t> mix;
+              std::vector<uint32_t> seal = prove_segment(*c, suite, po2, b.g[0].p, b.g[1].p, b.g[2].p, b.g[3].p,
+                                                         write_version != 0, version, &mix);
+              HIP_OK(hipStreamSynchronize(stream()));
+              j.seal_len = seal.size();
+              if (j.h_mix_out) memcpy(j.h_mix_out, mix.data(), mix.size() * 4);
+              R0_REQUIRE(!j.h_seal || seal.size() <= j.seal_cap, "seal buffer too small");
+              if (j.h_seal) memcpy(j.h_seal, seal.data(), seal.size() * 4);
+            } catch (const std::exception& e) {
+              j.error = dup_msg(e.what());
+            }
+          }
+          free_q.put(s);
+        }
+      });
+    }
+    uploader.join();
+    for (auto& t : provers) t.join();
+    for (size_t i = 0; i < njobs; i++)
+      if (jobs[i].error) return dup_msg((std::string("segment ") + std::to_string(i) + ": " + jobs[i].error).c_str());
+    return nullptr;
+  } catch (const std::exception& e) {
+    return dup_msg(e.what());
+  } catch (...) {
+    return dup_msg("r0hip: unknown error");
+  }
+}

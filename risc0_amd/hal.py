@@ -54,6 +54,7 @@ def _declare(L):
         "r0hip_host_alloc": [C.POINTER(vp), sz],
         "r0hip_host_free": [vp],
         "r0hip_fill_uniform": [vp, sz, C.c_uint64],
+        "r0hip_prove_segments": [C.c_char_p, C.c_int, C.c_uint32, C.c_int, C.c_uint32, C.c_void_p, sz, C.c_uint32],
         "r0hip_synchronize": [],
         "r0hip_batch_expand_into_evaluate_ntt": [vp, vp, sz, C.c_uint32, C.c_uint32],
         "r0hip_batch_interpolate_ntt": [vp, sz, C.c_uint32],
@@ -320,6 +321,48 @@ def prove_segment(hal, circuit, po2, code, data, accum, glob, version=None, seal
                                     int(version is not None), version or 0, seal.ctypes.data_as(u32p), seal_cap,
                                     C.byref(n), mix.ctypes.data_as(u32p)))
     return seal[: n.value].copy(), mix
+
+
+class SegmentJob(C.Structure):
+    """struct r0hip_segment_job (include/r0hip.h)"""
+    _fields_ = [("h_code", C.c_void_p), ("h_data", C.c_void_p), ("h_accum", C.c_void_p), ("h_global", C.c_void_p),
+                ("h_seal", C.c_void_p),
+                ("seal_cap", C.c_size_t), ("seal_len", C.c_size_t), ("h_mix_out", C.c_void_p), ("error", C.c_void_p)]
+
+
+def prove_segments(hal, circuit, po2, witnesses, version=None, in_flight=2, seal_cap=1 << 24):
+    """The native segment pipeline (r0hip_prove_segments): `witnesses` is a list of
+    (code, data, accum, global) host arrays (numpy uint32, ideally views of page-locked
+    memory) or raw host pointers; returns [(seal, mix)] in job order."""
+    from json import load
+    with open(os.path.join(_HERE, "circuits", circuit + ".taps.json")) as f:
+        mix_size = load(f)["mix_size"]
+    jobs = (SegmentJob * len(witnesses))()
+    keep, seals, mixes = [], [], []
+    for j, w in zip(jobs, witnesses):
+        ptrs = []
+        for a in w:
+            if isinstance(a, np.ndarray):
+                a = np.ascontiguousarray(a, dtype=np.uint32)
+                keep.append(a)
+                ptrs.append(a.ctypes.data)
+            else:
+                ptrs.append(int(a))
+        j.h_code, j.h_data, j.h_accum, j.h_global = ptrs
+        seals.append(np.zeros(seal_cap, dtype=np.uint32))
+        mixes.append(np.zeros(mix_size, dtype=np.uint32))
+        j.h_seal, j.seal_cap, j.h_mix_out = seals[-1].ctypes.data, seal_cap, mixes[-1].ctypes.data
+    err = lib().r0hip_prove_segments(circuit.encode(), hal.suite, po2, int(version is not None), version or 0,
+                                     C.cast(jobs, C.c_void_p), len(witnesses), in_flight)
+    for j in jobs:
+        if j.error:
+            libc_free(j.error)
+    check(err)
+    return [(seal[: j.seal_len].copy(), mix) for j, seal, mix in zip(jobs, seals, mixes)]
+
+
+def libc_free(p):
+    C.CDLL(None).free(C.c_void_p(p))
 
 
 def last_profile():

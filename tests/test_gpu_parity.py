@@ -425,6 +425,21 @@ def test_prove_segment_from_pinned_host(oracle):
     assert [int(x) for x in mix] == case["mix"]
 
 
+def test_prove_segments_pipeline_golden(oracle):
+    """The native segment pipeline (r0hip_prove_segments): uploader + 2 provers over 5
+    jobs from host witnesses; every seal matches its golden fixture."""
+    import risc0_amd as r
+    case = G.INDEX["seals"][0]
+    h = H(case["suite"])
+    w = G.seal_inputs(oracle, case["circuit"], case["po2"])
+    out = r.prove_segments(h, case["circuit"], case["po2"], [w] * 5,
+                           version=2 if case["circuit"] == "rv32im" else None, in_flight=2)
+    assert len(out) == 5
+    for seal, mix in out:
+        assert G.digest(seal) == case["seal_sha256"]
+        assert [int(x) for x in mix] == case["mix"]
+
+
 def device_witness(h, n, seed):
     """Uniform canonical BabyBear words generated on the device (r0hip_fill_uniform) for
     sizes whose host generation would take minutes."""
