@@ -120,6 +120,13 @@ const char* r0hip_prove_segment(const char* circuit, int suite, uint32_t po2, co
                                 const uint32_t* d_data, const uint32_t* d_accum, uint32_t* d_global,
                                 int write_version, uint32_t version, uint32_t* h_seal, size_t seal_cap,
                                 size_t* seal_len, uint32_t* h_mix_out);
+/* ---- rv32im witness side: accumulation phases 2-3 (risc0_circuit_rv32im_cuda_accum after its
+ * stepAccum kernel, rv32im-sys/kernels/cuda/ffi.cu:480-509; CPU ffi.cpp:326-360): inclusive
+ * prefix sums of the last 4 accum columns over rows [0, last_cycle), then every row adds the
+ * previous row's prefix values to the machine columns [23, cols - 4). d_accum is the accum
+ * group, column-major with `rows` rows (the per-cycle stepAccum phase stays the caller's). */
+const char* r0hip_rv32im_accum_finalize(uint32_t* d_accum, size_t rows, size_t cols, size_t last_cycle);
+
 /* ---- segment pipeline (r0vm's per-GPU worker queue, r0vm/src/actors/worker.rs:75-76, over the
  * zkvm's per-segment prove loop, zkvm/src/host/server/prove/prover_impl.rs:84-94) ----
  * Proves njobs segments of one (circuit, suite, po2) from HOST witness buffers: an uploader

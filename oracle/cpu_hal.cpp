@@ -198,6 +198,29 @@ void oracle_eltwise_copy_elem_slice(uint32_t* into, const uint32_t* from, size_t
 }
 
 // cpu.rs:637-642
+// rv32im accumulation, phases 2 and 3 of risc0_circuit_rv32im_cpu_accum
+// (risc0/circuit/rv32im-sys/kernels/cxx/ffi.cpp:326-360): inclusive prefix sums of the
+// last 4 accum columns over rows [0, last_cycle), then every row adds the previous row's
+// (cyclically) prefix values to the machine columns [split, cols - 4), 4 at a time.
+void oracle_rv32im_accum_finalize(uint32_t* accum, size_t rows, size_t cols, size_t split, size_t last_cycle) {
+  Elem* a = E(accum);
+  for (size_t j = 0; j < 4; j++) {
+    Elem* c = a + (cols - 4 + j) * rows;
+    for (size_t i = 1; i < last_cycle; i++) c[i] = c[i] + c[i - 1];
+  }
+  size_t machine_columns = (cols - split) / 4;
+  for (size_t row = 0; row < last_cycle; row++) {
+    size_t back1 = (row + last_cycle - 1) % last_cycle;
+    Elem prev[4];
+    for (size_t k = 0; k < 4; k++) prev[k] = a[(cols - 4 + k) * rows + back1];
+    for (size_t j = 0; j + 1 < machine_columns; j++)
+      for (size_t k = 0; k < 4; k++) {
+        size_t col = split + j * 4 + k;
+        a[col * rows + row] = a[col * rows + row] + prev[k];
+      }
+  }
+}
+
 void oracle_prefix_products(uint32_t* io, size_t n) {
   for (size_t i = 1; i < n; i++) X(io)[i] = X(io)[i] * X(io)[i - 1];
 }

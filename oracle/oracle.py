@@ -157,6 +157,10 @@ def eltwise_copy_elem_slice(into, frm, from_rows, from_cols, from_offset, from_s
                                          sz(from_stride), sz(into_offset), sz(into_stride))
 
 
+def rv32im_accum_finalize(accum, rows, cols, split, last_cycle):
+    lib().oracle_rv32im_accum_finalize(ptr(accum), sz(rows), sz(cols), sz(split), sz(last_cycle))
+
+
 def prefix_products(io):
     lib().oracle_prefix_products(ptr(io), sz(io.size // 4))
 

@@ -236,6 +236,11 @@ const char* r0hip_scatter(uint32_t* d_into, const uint32_t* d_index, const uint3
 const char* r0hip_prefix_products(uint32_t* d_io, size_t count) {
   return wrap([&] { prefix_products(stream(), d_io, count); });
 }
+const char* r0hip_rv32im_accum_finalize(uint32_t* d_accum, size_t rows, size_t cols, size_t last_cycle) {
+  // kUserAccumSplit = kLayout_TopAccum.columns[0].col (rv32im-sys/kernels/cxx/ffi.cpp:52,
+  // layout.cpp.inc:6993-6999): the first machine accumulator column
+  return wrap([&] { rv32im_accum_finalize(stream(), d_accum, rows, cols, 23, last_cycle); });
+}
 const char* r0hip_fill_uniform(uint32_t* d_out, size_t count, uint64_t seed) {
   return wrap([&] { fill_uniform(stream(), d_out, count, seed); });
 }

@@ -54,6 +54,7 @@ def _declare(L):
         "r0hip_host_alloc": [C.POINTER(vp), sz],
         "r0hip_host_free": [vp],
         "r0hip_fill_uniform": [vp, sz, C.c_uint64],
+        "r0hip_rv32im_accum_finalize": [vp, sz, sz, sz],
         "r0hip_prove_segments": [C.c_char_p, C.c_int, C.c_uint32, C.c_int, C.c_uint32, C.c_void_p, sz, C.c_uint32],
         "r0hip_synchronize": [],
         "r0hip_batch_expand_into_evaluate_ntt": [vp, vp, sz, C.c_uint32, C.c_uint32],
@@ -282,6 +283,10 @@ class HipHal:
         di, dof, dv = (self.copy_from_u32("index", index), self.copy_from_u32("offsets", offsets),
                        self.copy_from_elem("values", values))
         check(lib().r0hip_scatter(into.ptr, di.ptr, dof.ptr, dv.ptr, index.size - 1))
+
+    def rv32im_accum_finalize(self, accum, rows, cols, last_cycle):
+        """accumulation phases 2-3 of risc0_circuit_rv32im_cuda_accum (ffi.cu:480-509)"""
+        check(lib().r0hip_rv32im_accum_finalize(accum.ptr, rows, cols, last_cycle))
 
     def prefix_products(self, io):
         check(lib().r0hip_prefix_products(io.ptr, io.size))

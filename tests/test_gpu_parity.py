@@ -251,6 +251,19 @@ def test_hash_fold(hal, hal_sha, oracle, suite):
     assert np.array_equal(d.to_numpy(), io)
 
 
+@pytest.mark.parametrize("po2,last", [(4, 16), (10, 1000), (12, 4096), (20, (1 << 20) - 7), (16, 1), (13, 4097)])
+def test_rv32im_accum_finalize(hal, oracle, po2, last):
+    # accumulation phases 2-3 (rv32im-sys/kernels/cxx/ffi.cpp:326-360): 103 accum columns,
+    # prefix sums over [0, last) including ragged tiles and a single row; rows past `last` untouched
+    rows, cols = 1 << po2, 103
+    a = rnd(oracle, 40 + po2, rows * cols)
+    d = dev(hal, a)
+    hal.rv32im_accum_finalize(d, rows, cols, last)
+    ref = a.copy()
+    oracle.rv32im_accum_finalize(ref, rows, cols, 23, last)
+    assert np.array_equal(d.to_numpy(), ref)
+
+
 def test_combos_prepare_and_divide(hal, oracle):
     # hal/mod.rs:202-257: prepare, then divide by (x - z*w^-back); remainders must vanish.
     # Build combos whose rows have the required roots by construction.

@@ -237,3 +237,19 @@ def test_poseidon254_matches_bigint_restatement(oracle):
         q.mix(d)
         assert r.random_bits(32) == q.random_bits(32)
         assert int(oracle.decode(r.random_elem())) == q.random_elem()
+
+
+def test_rv32im_accum_finalize_restatement(oracle):
+    # no reference KAT covers accumulation phases 2-3 (ffi.cpp:326-360) in isolation (phase 1
+    # needs a real preflight trace): the oracle is checked against a direct numpy reading
+    rows, cols, last, split = 64, 103, 50, 23
+    a = oracle.rand_elems(np.random.default_rng(7), rows * cols)
+    ref = a.copy()
+    oracle.rv32im_accum_finalize(ref, rows, cols, split, last)
+    x = a.reshape(cols, rows).astype(np.int64)
+    for j in range(4):
+        x[cols - 4 + j, :last] = np.cumsum(x[cols - 4 + j, :last]) % P
+    prev = x[cols - 4:, (np.arange(last) + last - 1) % last]
+    for j in range((cols - split) // 4 - 1):
+        x[split + 4 * j:split + 4 * j + 4, :last] = (x[split + 4 * j:split + 4 * j + 4, :last] + prev) % P
+    assert np.array_equal(x.reshape(-1).astype(np.uint32), ref)
