@@ -20,8 +20,9 @@ def main():
     rng = np.random.default_rng(1)
     if "ec" in which:
         import json
-        circ = json.load(open(os.path.join(ROOT, "risc0_amd", "circuits", "rv32im.taps.json")))
-        po2 = 20
+        name = os.environ.get("R0_EC_CIRCUIT", "rv32im")
+        circ = json.load(open(os.path.join(ROOT, "risc0_amd", "circuits", name + ".taps.json")))
+        po2 = 20 if name == "rv32im" else 18
         D = 4 << po2
         gs = circ["group_sizes"]
         groups = [hal.copy_from_elem("g", rng.integers(0, P, gs[g] * D, dtype=np.uint64).astype(np.uint32))
@@ -30,11 +31,11 @@ def main():
         glob = hal.copy_from_elem("glob", rng.integers(0, P, circ["output_size"], dtype=np.uint64).astype(np.uint32))
         out = hal.alloc_elem("check", 4 * D)
         pm = rng.integers(0, P, 4, dtype=np.uint64).astype(np.uint32)
-        hal.eval_check("rv32im", out, groups, mix, glob, pm, po2)
+        hal.eval_check(name, out, groups, mix, glob, pm, po2)
         hal.synchronize()
         r.set_kernel_timing(True)
         for _ in range(3):
-            hal.eval_check("rv32im", out, groups, mix, glob, pm, po2)
+            hal.eval_check(name, out, groups, mix, glob, pm, po2)
         hal.synchronize()
         for k, v in sorted(r.kernel_times().items()):
             print(f"{os.environ.get('R0HIP_LIB', 'default')}: {k} {v[0] / v[1]:.3f} ms/launch")

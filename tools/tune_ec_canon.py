@@ -24,6 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "risc0_amd", "csrc")
 VAR = os.path.join(ROOT, "risc0_amd", "lib_variants")
 OUT = os.path.join(ROOT, "gpurun_out", "tune_canon")
+CIRCUIT = "rv32im"
 VARIANTS = {"canon": {"EC_CANON_FORCE": "1"}, "lazy": {"EC_CANON_FORCE": "0"},
             "lazyw1": {"EC_CANON_FORCE": "0", "EC_WAVES_OVERRIDE": "1"}}
 
@@ -45,7 +46,7 @@ def measure():
     os.makedirs(OUT, exist_ok=True)
     for name in VARIANTS:
         lib = os.path.join(VAR, f"libr0hip_{name}.so")
-        env = dict(os.environ, R0HIP_LIB=lib, TMPDIR="/tmp")
+        env = dict(os.environ, R0HIP_LIB=lib, TMPDIR="/tmp", R0_EC_CIRCUIT=CIRCUIT)
         subprocess.run(["timeout", "-k", "10", "200", "rocprofv3", "--kernel-trace", "--stats", "-d",
                         os.path.join(OUT, name), "-o", "run", "--output-format", "csv", "--", sys.executable,
                         os.path.join(ROOT, "tools", "bench_kernels.py"), "ec"], env=env, check=True,
@@ -83,5 +84,5 @@ def pick(circuit):
 
 if __name__ == "__main__":
     cmd = sys.argv[1]
-    c = sys.argv[2] if len(sys.argv) > 2 else "rv32im"
+    c = CIRCUIT = sys.argv[2] if len(sys.argv) > 2 else "rv32im"
     {"build": lambda: build(c), "measure": measure, "pick": lambda: pick(c)}[cmd]()

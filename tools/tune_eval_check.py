@@ -23,6 +23,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "risc0_amd", "csrc")
 VAR = os.path.join(ROOT, "risc0_amd", "lib_variants")
 OUT = os.path.join(ROOT, "gpurun_out", "tune")
+CIRCUIT = "rv32im"
 GRID = [(w, pf) for w in (1, 2) for pf in (128, 256, 384, 512, 640, 768, 1024)]
 BUDGET = 4000
 
@@ -47,7 +48,7 @@ def measure():
     os.makedirs(OUT, exist_ok=True)
     for lib in sorted(glob.glob(os.path.join(VAR, "libr0hip_tune_*.so"))):
         tag = os.path.basename(lib)[len("libr0hip_tune_"):-3]
-        env = dict(os.environ, R0HIP_LIB=lib, TMPDIR="/tmp")
+        env = dict(os.environ, R0HIP_LIB=lib, TMPDIR="/tmp", R0_EC_CIRCUIT=CIRCUIT)
         subprocess.run(["timeout", "-k", "10", "200", "rocprofv3", "--kernel-trace", "--stats", "-d",
                         os.path.join(OUT, tag), "-o", "run", "--output-format", "csv", "--", sys.executable,
                         os.path.join(ROOT, "tools", "bench_kernels.py"), "ec"], env=env, check=True,
@@ -78,5 +79,5 @@ def pick(circuit):
 
 if __name__ == "__main__":
     cmd = sys.argv[1]
-    c = sys.argv[2] if len(sys.argv) > 2 else "rv32im"
+    c = CIRCUIT = sys.argv[2] if len(sys.argv) > 2 else "rv32im"
     {"build": lambda: build(c), "measure": measure, "pick": lambda: pick(c)}[cmd]()
