@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--cpu-po2", type=int, default=16, help="segment size of the bounded CPU baseline sample")
     ap.add_argument("--inflight", type=int, default=None,
                     help="segments in flight per GPU (host threads, each with its own HIP stream); "
-                         "default 2, or 1 above po2=22 where one segment needs ~150 GB of HBM")
+                         "default 6 up to po2=18, 2 up to po2=22, 1 above (one po2=24 segment needs ~150 GB)")
     return ap.parse_args()
 
 
@@ -90,7 +90,9 @@ def main():
     phase_tot = {}
     last = {}
     import threading
-    inflight = args.inflight if args.inflight is not None else (2 if args.po2 <= 22 else 1)
+    # segments in flight per GPU: small segments are latency-bound (6 at po2<=18 measured
+    # 5.32 -> 4.67 ms for recursion po2=18), po2=20 gains nothing past 2, po2>22 fits one
+    inflight = args.inflight if args.inflight is not None else (6 if args.po2 <= 18 else 2 if args.po2 <= 22 else 1)
     k = max(1, min(inflight, len(segs) or 1))
     # per-thread globals buffer: prove_segment zeroizes it in place; the witness
     # groups are only read and are shared
