@@ -75,8 +75,9 @@ def run_host(lib, circuit, args_plain_words, poly_mix, po2):
     w = rou_fwd()[po2 + 2]
     vinv = enc([pow((pow(3 * pow(w, q, P) % P, 1 << po2, P) - 1) % P, P - 2, P) for q in range(4)])
     acc = np.zeros(4 * D, np.uint32)
-    mf = np.zeros(16, np.uint32)
-    me = np.zeros(16, np.uint32)
+    # materialised sub-expressions (tools/pick_ec_mat.py): up to 64 Fp and 64 FpExt slots
+    mf = np.zeros(64 * D, np.uint32)
+    me = np.zeros(64 * 4 * D, np.uint32)
     check = np.zeros(4 * D, np.uint32)
     arrs = [np.ascontiguousarray(a, dtype=np.uint32) for a in args_plain_words]
     argv = (u32p * len(arrs))(*[ptr(a) for a in arrs])

@@ -313,8 +313,25 @@ def emul_ok(ma, mb):
     return 4 * ma * max(mb, P - 1) <= U64
 
 
+def mat_config(circuit, budget):
+    """Sub-expressions materialised to HBM across kernels (tools/pick_ec_mat.py, committed in
+    <circuit>.ectune.json as "mat"), so kernels read them instead of recomputing their cones.
+    Applies whatever EC_WAVES/EC_PF say, since tuning variants must share the partition;
+    EC_NOMAT=1 disables it."""
+    path = os.path.join(ROOT, "risc0_amd", "circuits", circuit + ".ectune.json")
+    if os.environ.get("EC_NOMAT") == "1" or not os.path.exists(path):
+        return []
+    import json
+    with open(path) as f:
+        t = json.load(f)
+    if t.get("budget") != budget:
+        return []
+    return [int(v) for v in t.get("mat", [])]
+
+
 def emit(circuit, outdir, budget, host=False):
     pg = Program(circuit)
+    pg.mat = set(mat_config(circuit, budget))
     terms, kernels = schedule(pg, budget)
     tune = kernel_config(circuit, budget)
     prog, types = pg.prog, pg.types

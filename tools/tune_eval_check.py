@@ -69,9 +69,12 @@ def pick(circuit):
             if k not in best or t < best[k][0]:
                 best[k] = (t, w, pf)
     tot = sum(v[0] for v in best.values())
+    path = os.path.join(ROOT, "risc0_amd", "circuits", circuit + ".ectune.json")
+    prev = json.load(open(path)) if os.path.exists(path) else {}
     out = {"budget": BUDGET, "order": "dfs", "measured_total_us": round(tot, 1),
            "kernels": {str(k): {"waves": v[1], "pf": v[2], "us": round(v[0], 1)} for k, v in sorted(best.items())}}
-    path = os.path.join(ROOT, "risc0_amd", "circuits", circuit + ".ectune.json")
+    if prev.get("mat"):
+        out["mat"] = prev["mat"]  # the partition these kernels belong to
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print(f"wrote {path}: {len(best)} kernels, sum of best {tot / 1e3:.2f} ms")
