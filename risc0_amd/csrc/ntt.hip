@@ -60,7 +60,7 @@ constexpr uint32_t lds_words() {
 // One group of NST (1..3) radix-2 stages [s0, s0+NST) in registers: a lane owns blocks
 // of 2^NST elements t_base + m*h (h = 2^(s0-1)), so a group costs one LDS read and
 // write per element instead of NST. Twiddles come from the LDS copy of the table.
-template <bool INV, bool COLS, int B, int C, int NST, int FROM_EB = 0>
+template <bool INV, bool COLS, int B, int C, int NST, int FROM_EB = 0, int NT = kThreads>
 __device__ __forceinline__ void stage_group(uint32_t* lds, const uint32_t* tw, uint32_t s0,
                                             const uint32_t* csrc = nullptr) {
   if constexpr (NST > B) return;  // never reached; keeps the shifts below well-formed
@@ -69,9 +69,9 @@ __device__ __forceinline__ void stage_group(uint32_t* lds, const uint32_t* tw, u
   constexpr uint32_t nrb = 1u << (B >= NST ? B - NST : 0);  // blocks per column/row
   constexpr uint32_t nblk = nrb << C;
 #pragma unroll
-  for (uint32_t it = 0; it < (nblk + kThreads - 1) / kThreads; it++) {
-    const uint32_t blk = it * kThreads + threadIdx.x;
-    if (nblk % kThreads != 0 && blk >= nblk) break;
+  for (uint32_t it = 0; it < (nblk + NT - 1) / NT; it++) {
+    const uint32_t blk = it * NT + threadIdx.x;
+    if (nblk % NT != 0 && blk >= nblk) break;
     uint32_t j, r;
     if (COLS) {
       j = blk & ((1u << C) - 1);
@@ -122,7 +122,7 @@ __device__ __forceinline__ void stage_group(uint32_t* lds, const uint32_t* tw, u
 }
 
 // stages [first, B] ascending (DIT) or [1, B] descending (DIF), radix-8 groups first
-template <bool INV, bool COLS, int B, int C, int EB = 0>
+template <bool INV, bool COLS, int B, int C, int EB = 0, int NT = kThreads>
 __device__ __forceinline__ void stages(uint32_t* lds, const uint32_t* tw, const uint32_t* csrc = nullptr) {
   if (!INV) {
     // DIT stages EB+1 .. B; the first group reads the compact (unreplicated) input
@@ -131,16 +131,16 @@ __device__ __forceinline__ void stages(uint32_t* lds, const uint32_t* tw, const 
       const uint32_t n = uint32_t(B) - s + 1;
       const bool first = s == EB + 1 && EB > 0;
       if (n >= 3) {
-        if (first) stage_group<INV, COLS, B, C, 3, EB>(lds, tw, s, csrc);
-        else stage_group<INV, COLS, B, C, 3>(lds, tw, s);
+        if (first) stage_group<INV, COLS, B, C, 3, EB, NT>(lds, tw, s, csrc);
+        else stage_group<INV, COLS, B, C, 3, 0, NT>(lds, tw, s);
         s += 3;
       } else if (n == 2) {
-        if (first) stage_group<INV, COLS, B, C, 2, EB>(lds, tw, s, csrc);
-        else stage_group<INV, COLS, B, C, 2>(lds, tw, s);
+        if (first) stage_group<INV, COLS, B, C, 2, EB, NT>(lds, tw, s, csrc);
+        else stage_group<INV, COLS, B, C, 2, 0, NT>(lds, tw, s);
         s += 2;
       } else {
-        if (first) stage_group<INV, COLS, B, C, 1, EB>(lds, tw, s, csrc);
-        else stage_group<INV, COLS, B, C, 1>(lds, tw, s);
+        if (first) stage_group<INV, COLS, B, C, 1, EB, NT>(lds, tw, s, csrc);
+        else stage_group<INV, COLS, B, C, 1, 0, NT>(lds, tw, s);
         s += 1;
       }
     }
@@ -148,13 +148,13 @@ __device__ __forceinline__ void stages(uint32_t* lds, const uint32_t* tw, const 
 #pragma unroll
     for (int s = B; s >= 1;) {
       if (s >= 3) {
-        stage_group<INV, COLS, B, C, 3>(lds, tw, uint32_t(s - 2));
+        stage_group<INV, COLS, B, C, 3, 0, NT>(lds, tw, uint32_t(s - 2));
         s -= 3;
       } else if (s == 2) {
-        stage_group<INV, COLS, B, C, 2>(lds, tw, uint32_t(s - 1));
+        stage_group<INV, COLS, B, C, 2, 0, NT>(lds, tw, uint32_t(s - 1));
         s -= 2;
       } else {
-        stage_group<INV, COLS, B, C, 1>(lds, tw, uint32_t(s));
+        stage_group<INV, COLS, B, C, 1, 0, NT>(lds, tw, uint32_t(s));
         s -= 1;
       }
     }
@@ -198,8 +198,9 @@ __device__ __forceinline__ uint64_t col_block(uint64_t b) {
   return grp * (8 * H) + (r % 8) * H + r / 8;
 }
 
-template <bool INV, bool EXPAND, bool LAST, bool COLS, int B, int C, int EB>
-__global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
+template <bool INV, bool EXPAND, bool LAST, bool COLS, int B, int C, int EB, int NT>
+__global__ __launch_bounds__(NT) void ntt_pass_kernel(PassArgs p) {
+  static_assert(!COLS || NT == kThreads, "column passes assume 256 lanes (ColTwiddles)");
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* tw = lds + lds_words<COLS, B, C>();
   const uint32_t tid = threadIdx.x;
@@ -208,8 +209,8 @@ __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
   const uint64_t wg = COLS ? col_block<C>(blockIdx.x) : uint64_t(blockIdx.x);
   // stage twiddles -> LDS (entries 1 .. 2^B - 1)
 #pragma unroll
-  for (uint32_t i = 0; i < (nb + kThreads - 1) / kThreads; i++) {
-    uint32_t q = i * kThreads + tid;
+  for (uint32_t i = 0; i < (nb + NT - 1) / NT; i++) {
+    uint32_t q = i * NT + tid;
     if (q < nb) tw[q] = p.local_tw[q];
   }
   uint64_t g_hi = 0;
@@ -226,21 +227,21 @@ __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
     // rows [wg*2^C, +2^C): a contiguous run of 2^(B+C-EB) source words (expand: each
     // stands for 2^EB replicated slots, which the first stage group reads in place)
     constexpr uint32_t NIN = total >> EB;
-    constexpr uint32_t EIN = (NIN + kThreads - 1) / kThreads;
+    constexpr uint32_t EIN = (NIN + NT - 1) / NT;
     const uint32_t* src = p.in;
     const uint64_t base = wg << (B + C - EB);
     const uint64_t limit = p.groups << (B - EB);
     uint32_t r[EIN];
 #pragma unroll
     for (uint32_t i = 0; i < EIN; i++) {
-      const uint32_t q = i * kThreads + tid;
+      const uint32_t q = i * NT + tid;
       r[i] = 0;
-      if ((NIN % kThreads == 0 || q < NIN) && base + q < limit) r[i] = src[base + q];
+      if ((NIN % NT == 0 || q < NIN) && base + q < limit) r[i] = src[base + q];
     }
 #pragma unroll
     for (uint32_t i = 0; i < EIN; i++) {
-      const uint32_t q = i * kThreads + tid;
-      if (NIN % kThreads != 0 && q >= NIN) continue;
+      const uint32_t q = i * NT + tid;
+      if (NIN % NT != 0 && q >= NIN) continue;
       if (EB == 0) lds[lidx<COLS, B, C>(q >> B, q & (nb - 1))] = r[i];
       else if (EB >= B) {
 #pragma unroll
@@ -252,11 +253,11 @@ __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
     }
   } else if constexpr (B < 8 - C) {
     // tiny column passes: plain mapping, table twiddles
-    constexpr uint32_t E = (total + kThreads - 1) / kThreads;
+    constexpr uint32_t E = (total + NT - 1) / NT;
 #pragma unroll
     for (uint32_t i = 0; i < E; i++) {
-      const uint32_t idx = i * kThreads + tid;
-      if (total % kThreads != 0 && idx >= total) continue;
+      const uint32_t idx = i * NT + tid;
+      if (total % NT != 0 && idx >= total) continue;
       const uint32_t j = idx & ((1u << C) - 1), t = idx >> C;
       uint32_t v = p.in[(g_hi << (p.a + B)) + (uint64_t(t) << p.a) + low0 + j];
       if (!INV) {
@@ -269,8 +270,8 @@ __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
     // 2^C adjacent columns x 2^B rows of stride 2^a. Lane (j, r0) owns the rows t with
     // rev_B(t) = u = r0*E + i, i < E, so its forward pre-scale factors
     // w_{2^(a+B)}^{(low0+j)*u} are one running product (c^i) — no table loads.
-    constexpr uint32_t E = total / kThreads;
-    constexpr uint32_t R = kThreads >> C;  // rows per i
+    constexpr uint32_t E = total / NT;
+    constexpr uint32_t R = NT >> C;  // rows per i
     const uint32_t j = tid & ((1u << C) - 1), t0 = tid >> C;
     uint32_t r[E];
 #pragma unroll
@@ -286,12 +287,12 @@ __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
     for (uint32_t i = 0; i < E; i++) lds[lidx<COLS, B, C>(j, R * i + t0)] = r[i];
   }
   __syncthreads();
-  if (!INV) stages<false, COLS, B, C, (EB < B ? EB : 0)>(lds, tw, compact);
-  else stages<true, COLS, B, C>(lds, tw);
+  if (!INV) stages<false, COLS, B, C, (EB < B ? EB : 0), NT>(lds, tw, compact);
+  else stages<true, COLS, B, C, 0, NT>(lds, tw);
   // ---- store (inverse column passes post-scale; last inverse pass normalises) ----
   if constexpr (COLS && B >= 8 - C) {
-    constexpr uint32_t E = total / kThreads;
-    constexpr uint32_t R = kThreads >> C;
+    constexpr uint32_t E = total / NT;
+    constexpr uint32_t R = NT >> C;
     const uint32_t j = tid & ((1u << C) - 1), t0 = tid >> C;
     ColTwiddles<B, C> tf;
     if (INV) tf.init(p, low0 + j, t0);
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(kThreads) void ntt_pass_kernel(PassArgs p) {
     return;
   }
 #pragma unroll 4
-  for (uint32_t idx = tid; idx < total; idx += kThreads) {
+  for (uint32_t idx = tid; idx < total; idx += NT) {
     uint32_t t, j;
     uint64_t e;
     if (!COLS) {
@@ -458,7 +459,10 @@ void launch_pass_be(hipStream_t s, const PassArgs& p) {
       4 * (size_t(lds_words<COLS, B, C>()) + (size_t(1) << B) + (EB > 0 && EB < B ? (size_t(1) << (B + C - EB)) : 0));
   uint64_t nwg = COLS ? (p.groups >> C) : ((p.groups + (uint64_t(1) << C) - 1) >> C);
   R0_REQUIRE(nwg < (1ull << 31), "ntt grid too large");
-  hipLaunchKernelGGL((ntt_pass_kernel<INV, EXPAND, LAST, COLS, B, C, EB>), dim3(unsigned(nwg)), dim3(kThreads), lds,
+  // 13-bit row passes hold ~74 KB of LDS (data + stage twiddles), so only two workgroups
+  // fit a CU: 512 lanes per workgroup double the waves that hide their loads
+  constexpr int NT = (!COLS && B >= 13) ? 512 : kThreads;
+  hipLaunchKernelGGL((ntt_pass_kernel<INV, EXPAND, LAST, COLS, B, C, EB, NT>), dim3(unsigned(nwg)), dim3(NT), lds,
                      s, p);
   HIP_OK(hipGetLastError());
 }
