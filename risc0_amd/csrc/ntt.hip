@@ -461,7 +461,7 @@ void launch_pass_be(hipStream_t s, const PassArgs& p) {
   R0_REQUIRE(nwg < (1ull << 31), "ntt grid too large");
   // 13-bit row passes hold ~74 KB of LDS (data + stage twiddles), so only two workgroups
   // fit a CU: 512 lanes per workgroup double the waves that hide their loads
-  constexpr int NT = (!COLS && B >= 13) ? 512 : kThreads;
+  constexpr int NT = (!COLS && B >= 13) ? (INV ? 1024 : 512) : kThreads;
   hipLaunchKernelGGL((ntt_pass_kernel<INV, EXPAND, LAST, COLS, B, C, EB, NT>), dim3(unsigned(nwg)), dim3(NT), lds,
                      s, p);
   HIP_OK(hipGetLastError());
