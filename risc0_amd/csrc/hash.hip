@@ -173,12 +173,18 @@ __global__ __launch_bounds__(kThreads) void sha_rows_kernel(uint32_t* out, const
                                                           uint64_t rows, uint32_t cols) {
   uint64_t row = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (row >= rows) return;
-  uint32_t s[8], w[16];
+  uint32_t s[8], w[16], nxt[16];
   sha_init(s);
+  // the next block's loads are in flight during the current compression
+  auto load = [&](uint32_t col) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) nxt[i] = (col + i < cols) ? m[uint64_t(col + i) * rows + row] : 0u;
+  };
+  if (cols) load(0);
   for (uint32_t col = 0; col < cols; col += 16) {
 #pragma unroll
-    for (int i = 0; i < 16; i++)
-      w[i] = (col + i < cols) ? __builtin_bswap32(m[uint64_t(col + i) * rows + row]) : 0u;
+    for (int i = 0; i < 16; i++) w[i] = __builtin_bswap32(nxt[i]);
+    if (col + 16 < cols) load(col + 16);
     sha_compress(s, w);
   }
   uint32_t d[8];
