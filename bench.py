@@ -204,8 +204,42 @@ def kernel_roofline(r, hal, args, circ, dc, dd, da, dg, version):
     if alg_mm:
         mm = alg_mm / calls / avg_s
         out["valu"] = {"achieved": round(mm / 1e12, 3), "peak": MODMUL_PEAK / 1e12, "unit": "T modmul-equiv/s",
-                       "frac": round(mm / MODMUL_PEAK, 4), "modmuls_per_launch": int(alg_mm / calls)}
+                       "frac": round(mm / MODMUL_PEAK, 4), "modmuls_per_launch": int(alg_mm / calls),
+                       "note": "field multiplications of the restated algorithm per second against a canonical "
+                               "Montgomery multiply's rate; lazy reductions make one cost less, so frac can exceed 1"}
+        busy, src = pmc_valu_busy(name, args)
+        if busy is not None:
+            out["valu"]["issue_busy_frac"] = busy
+            out["valu"]["issue_source"] = src
     return out
+
+
+def pmc_valu_busy(family, args):
+    """Time-weighted share of cycles the SIMDs issue VALU instructions in `family`'s kernels,
+    from the newest committed SQ_ACTIVE_INST_VALU summary (profiles/r*_pmc_valu.txt, made by
+    tools/pmc_summary.py from a rocprofv3 --pmc pass of this bench)."""
+    import glob
+    if args.circuit != "rv32im" or args.po2 != 20 or args.hashfn != "poseidon2":
+        return None, None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_valu.txt")))
+    if not files:
+        return None, None
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from rocprof_families import family as fam_of
+    tot = busy = 0.0
+    for line in open(files[-1]).read().splitlines()[1:]:
+        f = line.split()
+        try:
+            ms, pct = float(f[-6]), float(f[-3])
+        except (ValueError, IndexError):
+            continue
+        name = " ".join(f[:-6])
+        if fam_of(name) == family.split("_poseidon2")[0]:
+            tot += ms
+            busy += ms * min(pct, 100.0) / 100.0
+    if tot == 0:
+        return None, None
+    return round(busy / tot, 3), os.path.relpath(files[-1], ROOT)
 
 
 def end_to_end(r, hal, args, witness, k, version):
