@@ -264,6 +264,8 @@ const char* r0hip_eval_check(const char* circuit, uint32_t* d_check, const uint3
   return wrap([&] {
     const CircuitDef* c = find_circuit(circuit ? circuit : "");
     R0_REQUIRE(c, std::string("unknown circuit ") + (circuit ? circuit : "(null)"));
+    R0_REQUIRE(d_check && d_groups && h_poly_mix, "eval_check: null argument");
+    for (int g = 0; g < 3; g++) R0_REQUIRE(d_groups[g], "eval_check: null register group");
     stage_reset();
     run_eval_check(*c, d_check, d_groups, d_mix, d_global, fe(h_poly_mix), po2);
   });

@@ -492,3 +492,37 @@ def test_full_size_seal_verifies(hal, hal_sha, oracle, circuit, suite, po2):
         bad[where] ^= np.uint32(1 << 9)
         with pytest.raises(verifier.VerificationError):
             verifier.verify(oracle, circuit, bad, s)
+
+
+def test_abi_errors_are_reported_not_fatal(hal, oracle):
+    """The C ABI's error contract (risc0/sys/src/lib.rs:53-75): bad arguments come back as
+    messages, the library stays usable, and the pipeline reports the failing job."""
+    import ctypes
+
+    import risc0_amd as r
+    L = r.lib()
+    d = hal.alloc_digest("d", 8)
+    m = hal.alloc_elem("m", 8 * 16)
+    with pytest.raises(r.R0HipError, match="suite"):
+        r.check(L.r0hip_hash_rows(7, d.ptr, m.ptr, 8, 16))
+    with pytest.raises(r.R0HipError, match="input_size"):
+        r.check(L.r0hip_hash_fold(0, d.ptr, 6, 4))
+    with pytest.raises(r.R0HipError, match="NTT size"):
+        r.check(L.r0hip_batch_interpolate_ntt(m.ptr, 1, 40))
+    with pytest.raises(r.R0HipError, match="circuit"):
+        r.check(L.r0hip_eval_check(b"keccak", m.ptr, None, m.ptr, m.ptr, None, 4))
+    case = G.INDEX["seals"][0]
+    code, data, accum, glob = (dev(hal, x) for x in G.seal_inputs(oracle, case["circuit"], case["po2"]))
+    with pytest.raises(r.R0HipError, match="seal buffer too small"):
+        r.prove_segment(hal, case["circuit"], case["po2"], code, data, accum, glob, version=2, seal_cap=16)
+    w = G.seal_inputs(oracle, case["circuit"], case["po2"])
+    with pytest.raises(r.R0HipError, match="segment 1"):
+        r.prove_segments(hal, case["circuit"], case["po2"], [w, (w[0], 0, w[2], w[3])], version=2)
+    # still healthy afterwards
+    h_ok = hal.alloc_elem("ok", 8 * 16)
+    h_ok.copy_from(oracle.rand_elems(np.random.default_rng(3), 8 * 16))
+    out = hal.alloc_digest("o", 8)
+    hal.hash_rows(out, h_ok)
+    ref = np.zeros(8 * 8, np.uint32)
+    oracle.hash_rows(oracle.POSEIDON2, ref, h_ok.to_numpy())
+    assert np.array_equal(out.to_numpy(), ref)
