@@ -149,6 +149,16 @@ typedef struct r0hip_segment_job {
 const char* r0hip_prove_segments(const char* circuit, int suite, uint32_t po2, int write_version, uint32_t version,
                                  r0hip_segment_job* jobs, size_t njobs, uint32_t in_flight);
 
+/* ---- seal verification (risc0/zkp/src/verify/mod.rs:500-560 `verify`, with merkle.rs:79-186,
+ * fri.rs:36-155, read_iop.rs:20-84; rv32im seals lead with the version word 2,
+ * circuit/rv32im/src/lib.rs:78-92) ----
+ * Replays the transcript and checks every Merkle opening, every FRI fold, the final FRI
+ * polynomial and the seal length; the constraint validity equation (mod.rs:356-394) is not
+ * evaluated. Host-only: needs no GPU and no r0hip_init. Returns NULL when the
+ * seal verifies (po2 of the segment in *po2_out, if non-NULL), else the failed check. */
+const char* r0hip_verify_seal(const char* circuit, int suite, const uint32_t* seal, size_t seal_len,
+                              uint32_t* po2_out);
+
 /* kernel-level timing with HIP events on the library stream: enable, run, then read
  * "name=total_ms:calls:alg_bytes;..." (alg_bytes = algorithmic HBM bytes) */
 const char* r0hip_set_kernel_timing(int on);

@@ -56,6 +56,7 @@ def _declare(L):
         "r0hip_fill_uniform": [vp, sz, C.c_uint64],
         "r0hip_rv32im_accum_finalize": [vp, sz, sz, sz],
         "r0hip_prove_segments": [C.c_char_p, C.c_int, C.c_uint32, C.c_int, C.c_uint32, C.c_void_p, sz, C.c_uint32],
+        "r0hip_verify_seal": [C.c_char_p, C.c_int, u32p, sz, C.POINTER(C.c_uint32)],
         "r0hip_synchronize": [],
         "r0hip_batch_expand_into_evaluate_ntt": [vp, vp, sz, C.c_uint32, C.c_uint32],
         "r0hip_batch_interpolate_ntt": [vp, sz, C.c_uint32],
@@ -364,6 +365,16 @@ def prove_segments(hal, circuit, po2, witnesses, version=None, in_flight=2, seal
             libc_free(j.error)
     check(err)
     return [(seal[: j.seal_len].copy(), mix) for j, seal, mix in zip(jobs, seals, mixes)]
+
+
+def verify_seal(circuit, suite, seal):
+    """r0hip_verify_seal: the native seal verifier (host-only, no GPU); returns the
+    segment po2, raises R0HipError naming the failed check."""
+    seal = np.ascontiguousarray(seal, dtype=np.uint32)
+    po2 = C.c_uint32(0)
+    check(lib().r0hip_verify_seal(circuit.encode(), SUITES[suite] if isinstance(suite, str) else suite,
+                                  seal.ctypes.data_as(u32p), seal.size, C.byref(po2)))
+    return po2.value
 
 
 def libc_free(p):

@@ -487,11 +487,14 @@ def test_full_size_seal_verifies(hal, hal_sha, oracle, circuit, suite, po2):
         b.free()
     res = verifier.verify(oracle, circuit, seal, s)
     assert res["po2"] == po2
+    assert r.verify_seal(circuit, s, seal) == po2  # the native verifier agrees
     for where in (seal.size // 3, seal.size - 5):
         bad = seal.copy()
         bad[where] ^= np.uint32(1 << 9)
         with pytest.raises(verifier.VerificationError):
             verifier.verify(oracle, circuit, bad, s)
+        with pytest.raises(r.R0HipError):
+            r.verify_seal(circuit, s, bad)
 
 
 def test_abi_errors_are_reported_not_fatal(hal, oracle):

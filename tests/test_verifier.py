@@ -29,3 +29,34 @@ def test_verifier_accepts_oracle_seals(oracle, circuit, suite, po2):
         bad[where] ^= np.uint32(1 << 7)
         with pytest.raises(verifier.VerificationError):
             verifier.verify(oracle, circuit, bad, s)
+
+
+@pytest.mark.parametrize("circuit,suite,po2", CASES)
+def test_native_verifier_matches_restatement(oracle, circuit, suite, po2):
+    """r0hip_verify_seal (risc0_amd/csrc/verify.cpp) — host code, no GPU — accepts what the
+    restatement accepts and rejects the same tampered, truncated and padded seals."""
+    import os
+    import risc0_amd as r
+    from risc0_amd.hal import LIB_PATH
+    if oracle.ref_lib() is None or not os.path.exists(LIB_PATH):
+        pytest.skip("oracle/_ref or libr0hip.so not built")
+    code, data, accum, glob = G.seal_inputs(oracle, circuit, po2)
+    s = SUITES[suite]
+    seal, _mix, _ = oracle.prove_segment(circuit, s, po2, code, data, accum, glob,
+                                         version=2 if circuit == "rv32im" else None)
+    assert r.verify_seal(circuit, s, seal) == po2
+    rng = np.random.default_rng(po2 * 7 + s)
+    for where in [1, 2, 9, seal.size // 4, seal.size // 2, seal.size - 3] + list(rng.integers(0, seal.size, 6)):
+        bad = seal.copy()
+        bad[where] ^= np.uint32(1 << int(rng.integers(0, 31)))
+        with pytest.raises(verifier.VerificationError):
+            verifier.verify(oracle, circuit, bad, s)
+        with pytest.raises(r.R0HipError):
+            r.verify_seal(circuit, s, bad)
+    for bad, msg in ((seal[:-1], "seal too short"), (np.append(seal, np.uint32(0)), "trailing words")):
+        with pytest.raises(r.R0HipError, match=msg):
+            r.verify_seal(circuit, s, bad)
+    with pytest.raises(r.R0HipError):  # another suite's transcript
+        r.verify_seal(circuit, (s + 1) % 3, seal)
+    with pytest.raises(r.R0HipError, match="unknown circuit"):
+        r.verify_seal("nope", s, seal)
