@@ -152,12 +152,19 @@ const char* r0hip_prove_segments(const char* circuit, int suite, uint32_t po2, i
 /* ---- seal verification (risc0/zkp/src/verify/mod.rs:500-560 `verify`, with merkle.rs:79-186,
  * fri.rs:36-155, read_iop.rs:20-84; rv32im seals lead with the version word 2,
  * circuit/rv32im/src/lib.rs:78-92) ----
- * Replays the transcript and checks every Merkle opening, every FRI fold, the final FRI
- * polynomial and the seal length; the constraint validity equation (mod.rs:356-394) is not
- * evaluated. Host-only: needs no GPU and no r0hip_init. Returns NULL when the
- * seal verifies (po2 of the segment in *po2_out, if non-NULL), else the failed check. */
+ * Replays the transcript and checks the constraint validity equation poly_ext(z) ==
+ * check(z) * ((3z)^N - 1) (mod.rs:340-394; skipped when check_validity == 0, for seals of
+ * synthetic witnesses), every Merkle opening, every FRI fold, the final FRI polynomial and
+ * the seal length. Host-only: needs no GPU and no r0hip_init. Returns NULL when the seal
+ * verifies (po2 of the segment in *po2_out, if non-NULL), else the failed check. */
 const char* r0hip_verify_seal(const char* circuit, int suite, const uint32_t* seal, size_t seal_len,
-                              uint32_t* po2_out);
+                              int check_validity, uint32_t* po2_out);
+/* PolyExt::poly_ext of the circuit (its generated poly_ext.rs, called at mod.rs:356-386): the
+ * constraint polynomial at the out-of-domain point. h_mix (mix_size) and h_global
+ * (output_size) are Montgomery words, h_eval_u one FpExt (4 words) per tap in tap order,
+ * h_poly_mix one FpExt; the result FpExt goes to h_out. Host-only. */
+const char* r0hip_poly_ext(const char* circuit, const uint32_t* h_mix, const uint32_t* h_global,
+                           const uint32_t* h_eval_u, const uint32_t* h_poly_mix, uint32_t* h_out);
 
 /* kernel-level timing with HIP events on the library stream: enable, run, then read
  * "name=total_ms:calls:alg_bytes;..." (alg_bytes = algorithmic HBM bytes) */

@@ -7,8 +7,8 @@ mirror of the reference's `Hal` trait for tests and the benchmark.
 """
 from .hal import (POSEIDON2, POSEIDON254, SHA256, Buffer, HipHal, R0HipError, check, exported_symbols, kernel_times,
                   last_profile, lib, prove_segment, prove_segments, set_kernel_timing,
-                  verify_seal)
+                  poly_ext, verify_seal)
 
 __all__ = ["POSEIDON2", "POSEIDON254", "SHA256", "Buffer", "HipHal", "R0HipError", "check", "exported_symbols", "last_profile",
            "lib", "prove_segment", "prove_segments", "kernel_times", "set_kernel_timing",
-           "verify_seal"]
+           "poly_ext", "verify_seal"]

@@ -31,6 +31,10 @@ struct CircuitDef {
   size_t n_eval_args;
   void (*eval_check)(hipStream_t, const EvalCheckArgs&);
   void (*info)(EvalCheckInfo*);
+  // the constraint program for the host poly_ext (verify.cpp): n_ir records of
+  // {op, dst, a, b, c, d}, op index into "celg+-*abr", dst dense 0..n_ir-1
+  const uint32_t* ir;
+  size_t n_ir;
 
   struct Tap {
     uint32_t offset, back, group, combo, skip;

@@ -7,10 +7,11 @@
 //   DEEP-ALI taps     mod.rs:246-290 (fri_eval_taps)
 //   Merkle openings   risc0/zkp/src/verify/merkle.rs:79-186 with zkp/src/merkle.rs:36-66 params
 //   FRI               risc0/zkp/src/verify/fri.rs:36-155
-// Everything the reference checks is checked except the constraint validity equation
-// (mod.rs:356-394), which needs the circuit's compiled poly_ext: transcript replay, every
-// Merkle path, every FRI fold, the final polynomial and the seal length. Host code only —
-// no HIP call, so it runs without a GPU.
+// Everything the reference checks is checked: transcript replay, the validity equation
+// (mod.rs:340-394, with poly_ext run from the circuit's constraint program), every Merkle
+// path, every FRI fold, the final polynomial and the seal length. The validity check can be
+// switched off for seals of synthetic witnesses, which do not satisfy the constraints.
+// Host code only — no HIP call, so it runs without a GPU.
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -119,6 +120,40 @@ struct MerkleVerifier {
 
 FpExt load_ext(const uint32_t* w) { return FpExt{{w[0], w[1], w[2], w[3]}}; }
 
+}  // namespace
+
+// PolyExt::poly_ext (the circuits' generated poly_ext.rs, e.g. circuit/recursion/src/poly_ext.rs,
+// as called by verify_validity, zkp/src/verify/mod.rs:356-386): the constraint polynomial at
+// the out-of-domain point from the tap evaluations, by running the circuit's flattened program
+// (CircuitDef::ir, from <c>.poly.ir) over FpExt. mix/global are Montgomery words; eval_u holds
+// one value per tap in tap order.
+FpExt poly_ext(const CircuitDef& c, const uint32_t* mix, const uint32_t* global, const FpExt* eval_u,
+               FpExt poly_mix) {
+  std::vector<FpExt> pows(c.n_poly_mix);
+  for (size_t k = 0; k < c.n_poly_mix; k++) pows[k] = fe_pow(poly_mix, c.poly_mix_powers[k]);
+  std::vector<FpExt> val(c.n_ir);
+  for (size_t k = 0; k < c.n_ir; k++) {
+    const uint32_t* r = c.ir + 6 * k;
+    FpExt& v = val[r[1]];
+    switch (r[0]) {
+      case 0: v = fe_from_fp(r[2]); break;                              // c: constant
+      case 1: v = FpExt{{r[2], r[3], r[4], r[5]}}; break;               // e: extension constant
+      case 2: v = eval_u[r[2]]; break;                                   // l: tap
+      case 3: v = fe_from_fp((r[2] ? global : mix)[r[3]]); break;        // g: mix / global word
+      case 4: v = fe_add(val[r[2]], val[r[3]]); break;
+      case 5: v = fe_sub(val[r[2]], val[r[3]]); break;
+      case 6: v = fe_mul(val[r[2]], val[r[3]]); break;
+      case 7: v = fe_add(val[r[2]], fe_mul(val[r[3]], pows[r[4]])); break;  // a: acc + x * mix^k
+      case 8: v = fe_add(val[r[2]], fe_mul(fe_mul(val[r[3]], val[r[4]]), pows[r[5]])); break;
+      case 9: return v;  // r: result (the record names the value in its dst slot)
+      default: throw std::runtime_error("r0hip: bad constraint program record");
+    }
+  }
+  throw std::runtime_error("r0hip: constraint program has no result");
+}
+
+namespace {
+
 FpExt poly_eval(const FpExt* coeffs, size_t n, FpExt x) {
   FpExt tot = fe_zero();
   for (size_t i = n; i-- > 0;) tot = fe_add(fe_mul(tot, x), coeffs[i]);
@@ -180,7 +215,7 @@ void fri_verify(ReadIOP& iop, size_t degree, Inner inner) {
   }
 }
 
-uint32_t verify_seal(const CircuitDef& c, int suite, const uint32_t* seal, size_t len) {
+uint32_t verify_seal(const CircuitDef& c, int suite, const uint32_t* seal, size_t len, bool check_validity) {
   if (c.name == std::string("rv32im")) {  // rv32im/src/lib.rs:78-92: a version word leads the seal
     if (len < 1 || seal[0] != 2) throw VerifyError("bad rv32im seal version");
     seal++;
@@ -202,11 +237,12 @@ uint32_t verify_seal(const CircuitDef& c, int suite, const uint32_t* seal, size_
   // groups in commit order: code, data, then (after the mix draw) accum (mod.rs:215-244)
   MerkleVerifier code(iop, domain, c.group_sizes[1]);
   MerkleVerifier data(iop, domain, c.group_sizes[2]);
-  for (size_t i = 0; i < c.mix_size; i++) (void)iop.rng->random_elem();
+  std::vector<uint32_t> mix(c.mix_size);
+  for (auto& m : mix) m = iop.rng->random_elem();
   MerkleVerifier accum(iop, domain, c.group_sizes[0]);
   const MerkleVerifier* groups[3] = {&accum, &code, &data};
-  // verify_validity (mod.rs:292-474) up to the validity equation
-  (void)iop.rng->random_ext_elem();  // poly_mix
+  // verify_validity (mod.rs:292-474)
+  const FpExt poly_mix = iop.rng->random_ext_elem();
   MerkleVerifier check(iop, domain, CHECK_SIZE);
   const FpExt z = iop.rng->random_ext_elem();
   const uint32_t back_one = fp_encode(kRouRev[po2]);
@@ -215,6 +251,31 @@ uint32_t verify_seal(const CircuitDef& c, int suite, const uint32_t* seal, size_
   iop.commit(hash_elems(suite, coeff_words, (nt + CHECK_SIZE) * 4));
   std::vector<FpExt> coeff_u(nt + CHECK_SIZE);
   for (size_t i = 0; i < coeff_u.size(); i++) coeff_u[i] = load_ext(coeff_words + 4 * i);
+  if (check_validity) {  // mod.rs:340-394: poly_ext(z) == check(z) * ((3z)^N - 1)
+    std::vector<FpExt> eval_u;
+    size_t pos = 0;
+    c.regs(0, nt, [&](size_t cur) {
+      const size_t size = c.tap(cur).skip;
+      for (size_t i = 0; i < size; i++) {
+        const FpExt x = fe_mul_fp(z, fp_pow(back_one, c.tap(cur + i).back));
+        eval_u.push_back(poly_eval(&coeff_u[pos], size, x));
+      }
+      pos += size;
+    });
+    FpExt check = fe_zero();
+    const size_t remap[4] = {0, 2, 1, 3};
+    for (size_t i = 0; i < 4; i++) {
+      const FpExt zi = fe_pow(z, i);
+      for (size_t k = 0; k < 4; k++) {
+        FpExt unit = fe_zero();
+        unit.c[k] = kOne;
+        check = fe_add(check, fe_mul(fe_mul(coeff_u[nt + remap[i] + 4 * k], zi), unit));
+      }
+    }
+    check = fe_mul(check, fe_sub(fe_pow(fe_mul_fp(z, fp_encode(3)), n), fe_one()));
+    if (!fe_eq(check, poly_ext(c, mix.data(), header, eval_u.data(), poly_mix)))
+      throw VerifyError("verification indicates proof is invalid");
+  }
 
   // DEEP-ALI mixing (mod.rs:396-440)
   const FpExt fri_mix = iop.rng->random_ext_elem();
@@ -280,14 +341,32 @@ uint32_t verify_seal(const CircuitDef& c, int suite, const uint32_t* seal, size_
 using namespace r0;
 
 extern "C" const char* r0hip_verify_seal(const char* circuit, int suite, const uint32_t* seal, size_t seal_len,
-                                         uint32_t* po2_out) {
+                                         int check_validity, uint32_t* po2_out) {
   try {
     const CircuitDef* c = find_circuit(circuit ? circuit : "");
     R0_REQUIRE(c, std::string("unknown circuit ") + (circuit ? circuit : "(null)"));
     R0_REQUIRE(suite >= 0 && suite <= 2, "unknown hash suite");
     R0_REQUIRE(seal || seal_len == 0, "seal is NULL");
-    uint32_t po2 = verify_seal(*c, suite, seal, seal_len);
+    uint32_t po2 = verify_seal(*c, suite, seal, seal_len, check_validity != 0);
     if (po2_out) *po2_out = po2;
+    return nullptr;
+  } catch (const std::exception& e) {
+    return strdup(e.what());
+  } catch (...) {
+    return strdup("r0hip: unknown error");
+  }
+}
+
+extern "C" const char* r0hip_poly_ext(const char* circuit, const uint32_t* h_mix, const uint32_t* h_global,
+                                      const uint32_t* h_eval_u, const uint32_t* h_poly_mix, uint32_t* h_out) {
+  try {
+    const CircuitDef* c = find_circuit(circuit ? circuit : "");
+    R0_REQUIRE(c, std::string("unknown circuit ") + (circuit ? circuit : "(null)"));
+    R0_REQUIRE(h_mix && h_global && h_eval_u && h_poly_mix && h_out, "poly_ext: null argument");
+    std::vector<FpExt> eval_u(c->n_taps);
+    for (size_t i = 0; i < c->n_taps; i++) eval_u[i] = load_ext(h_eval_u + 4 * i);
+    FpExt r = poly_ext(*c, h_mix, h_global, eval_u.data(), load_ext(h_poly_mix));
+    memcpy(h_out, r.c, 16);
     return nullptr;
   } catch (const std::exception& e) {
     return strdup(e.what());

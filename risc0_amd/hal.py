@@ -56,7 +56,8 @@ def _declare(L):
         "r0hip_fill_uniform": [vp, sz, C.c_uint64],
         "r0hip_rv32im_accum_finalize": [vp, sz, sz, sz],
         "r0hip_prove_segments": [C.c_char_p, C.c_int, C.c_uint32, C.c_int, C.c_uint32, C.c_void_p, sz, C.c_uint32],
-        "r0hip_verify_seal": [C.c_char_p, C.c_int, u32p, sz, C.POINTER(C.c_uint32)],
+        "r0hip_verify_seal": [C.c_char_p, C.c_int, u32p, sz, C.c_int, C.POINTER(C.c_uint32)],
+        "r0hip_poly_ext": [C.c_char_p, u32p, u32p, u32p, u32p, u32p],
         "r0hip_synchronize": [],
         "r0hip_batch_expand_into_evaluate_ntt": [vp, vp, sz, C.c_uint32, C.c_uint32],
         "r0hip_batch_interpolate_ntt": [vp, sz, C.c_uint32],
@@ -367,14 +368,23 @@ def prove_segments(hal, circuit, po2, witnesses, version=None, in_flight=2, seal
     return [(seal[: j.seal_len].copy(), mix) for j, seal, mix in zip(jobs, seals, mixes)]
 
 
-def verify_seal(circuit, suite, seal):
+def verify_seal(circuit, suite, seal, check_validity=True):
     """r0hip_verify_seal: the native seal verifier (host-only, no GPU); returns the
-    segment po2, raises R0HipError naming the failed check."""
+    segment po2, raises R0HipError naming the failed check. check_validity=False skips the
+    constraint equation, for seals of synthetic witnesses."""
     seal = np.ascontiguousarray(seal, dtype=np.uint32)
     po2 = C.c_uint32(0)
     check(lib().r0hip_verify_seal(circuit.encode(), SUITES[suite] if isinstance(suite, str) else suite,
-                                  seal.ctypes.data_as(u32p), seal.size, C.byref(po2)))
+                                  seal.ctypes.data_as(u32p), seal.size, int(bool(check_validity)), C.byref(po2)))
     return po2.value
+
+
+def poly_ext(circuit, mix, glob, eval_u, poly_mix):
+    """r0hip_poly_ext (host-only): Montgomery words in, the FpExt result as 4 Montgomery words."""
+    arrs = [np.ascontiguousarray(a, dtype=np.uint32) for a in (mix, glob, eval_u, poly_mix)]
+    out = np.zeros(4, np.uint32)
+    check(lib().r0hip_poly_ext(circuit.encode(), *(a.ctypes.data_as(u32p) for a in arrs), out.ctypes.data_as(u32p)))
+    return out
 
 
 def libc_free(p):

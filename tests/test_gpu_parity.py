@@ -487,14 +487,34 @@ def test_full_size_seal_verifies(hal, hal_sha, oracle, circuit, suite, po2):
         b.free()
     res = verifier.verify(oracle, circuit, seal, s)
     assert res["po2"] == po2
-    assert r.verify_seal(circuit, s, seal) == po2  # the native verifier agrees
+    assert r.verify_seal(circuit, s, seal, check_validity=False) == po2  # the native verifier agrees
     for where in (seal.size // 3, seal.size - 5):
         bad = seal.copy()
         bad[where] ^= np.uint32(1 << 9)
         with pytest.raises(verifier.VerificationError):
             verifier.verify(oracle, circuit, bad, s)
         with pytest.raises(r.R0HipError):
-            r.verify_seal(circuit, s, bad)
+            r.verify_seal(circuit, s, bad, check_validity=False)
+
+
+@pytest.mark.parametrize("suite,po2", [("poseidon2", 20), ("sha-256", 16), ("poseidon_254", 16)])
+def test_valid_witness_seal_passes_validity(hal, hal_sha, oracle, suite, po2):
+    """A witness that satisfies the recursion circuit (all-zero code/data/accum; its
+    constraints hold for any globals and mix) proved on the GPU passes every check of the
+    reference verifier including the validity equation (mod.rs:340-394), in the native
+    verifier and in the restatement."""
+    import risc0_amd as r
+    import verifier
+    h, s = H(suite), S(oracle, suite)
+    d = oracle.load_circuit_json("recursion")
+    n, gs = 1 << po2, d["group_sizes"]
+    bufs = [dev(h, np.zeros(gs[g] * n, np.uint32)) for g in (1, 2, 0)]
+    glob = dev(h, oracle.rand_elems(np.random.default_rng(po2), d["output_size"]))
+    seal, _mix = r.prove_segment(h, "recursion", po2, *bufs, glob)
+    for b in bufs:
+        b.free()
+    assert r.verify_seal("recursion", s, seal) == po2
+    assert verifier.verify(oracle, "recursion", seal, s, check_validity=True)["validity"] is True
 
 
 def test_abi_errors_are_reported_not_fatal(hal, oracle):

@@ -44,7 +44,10 @@ def test_native_verifier_matches_restatement(oracle, circuit, suite, po2):
     s = SUITES[suite]
     seal, _mix, _ = oracle.prove_segment(circuit, s, po2, code, data, accum, glob,
                                          version=2 if circuit == "rv32im" else None)
-    assert r.verify_seal(circuit, s, seal) == po2
+    assert r.verify_seal(circuit, s, seal, check_validity=False) == po2
+    # synthetic witnesses break the constraints: both verifiers see it
+    with pytest.raises(r.R0HipError, match="proof is invalid"):
+        r.verify_seal(circuit, s, seal)
     rng = np.random.default_rng(po2 * 7 + s)
     for where in [1, 2, 9, seal.size // 4, seal.size // 2, seal.size - 3] + list(rng.integers(0, seal.size, 6)):
         bad = seal.copy()
@@ -52,11 +55,55 @@ def test_native_verifier_matches_restatement(oracle, circuit, suite, po2):
         with pytest.raises(verifier.VerificationError):
             verifier.verify(oracle, circuit, bad, s)
         with pytest.raises(r.R0HipError):
-            r.verify_seal(circuit, s, bad)
+            r.verify_seal(circuit, s, bad, check_validity=False)
     for bad, msg in ((seal[:-1], "seal too short"), (np.append(seal, np.uint32(0)), "trailing words")):
         with pytest.raises(r.R0HipError, match=msg):
-            r.verify_seal(circuit, s, bad)
+            r.verify_seal(circuit, s, bad, check_validity=False)
     with pytest.raises(r.R0HipError):  # another suite's transcript
-        r.verify_seal(circuit, (s + 1) % 3, seal)
+        r.verify_seal(circuit, (s + 1) % 3, seal, check_validity=False)
     with pytest.raises(r.R0HipError, match="unknown circuit"):
         r.verify_seal("nope", s, seal)
+
+
+def _native_lib_or_skip(oracle):
+    import os
+    from risc0_amd.hal import LIB_PATH
+    if oracle.ref_lib() is None or not os.path.exists(LIB_PATH):
+        pytest.skip("oracle/_ref or libr0hip.so not built")
+
+
+@pytest.mark.parametrize("circuit", ["rv32im", "recursion"])
+def test_native_poly_ext_matches_restatement(oracle, circuit):
+    """r0hip_poly_ext (the constraint program run over FpExt on the host) equals the
+    Python IR interpretation on random out-of-domain inputs."""
+    import risc0_amd as r
+    _native_lib_or_skip(oracle)
+    taps = verifier.Taps(circuit)
+    d = taps.d
+    rng = np.random.default_rng(11)
+    for _ in range(3):
+        mix = oracle.rand_elems(rng, d["mix_size"])
+        glob = oracle.rand_elems(rng, d["output_size"])
+        eval_u = oracle.rand_elems(rng, 4 * taps.num_taps)
+        pm = oracle.rand_elems(rng, 4)
+        got = tuple(verifier.dec(w) for w in r.poly_ext(circuit, mix, glob, eval_u, pm))
+        want = verifier.poly_ext(circuit, taps, tuple(verifier.dec(w) for w in pm),
+                                 verifier.ext_words(eval_u), glob, mix)
+        assert got == want
+
+
+@pytest.mark.parametrize("suite", ["poseidon2", "sha-256", "poseidon_254"])
+def test_valid_recursion_seal_passes_validity(oracle, suite):
+    """A witness that satisfies the recursion circuit (all-zero code/data/accum; the
+    constraints hold for any globals and mix) gives a seal whose validity equation holds in
+    the restatement and in the native verifier; a flipped coefficient breaks it."""
+    import risc0_amd as r
+    _native_lib_or_skip(oracle)
+    po2, s = 8, SUITES[suite]
+    d = oracle.load_circuit_json("recursion")
+    n, gs = 1 << po2, d["group_sizes"]
+    code, data, accum = (np.zeros(gs[g] * n, np.uint32) for g in (1, 2, 0))
+    glob = oracle.rand_elems(np.random.default_rng(5), d["output_size"])
+    seal, _mix, _ = oracle.prove_segment("recursion", s, po2, code, data, accum, glob, version=None)
+    assert verifier.verify(oracle, "recursion", seal, s, check_validity=True)["validity"] is True
+    assert r.verify_seal("recursion", s, seal) == po2
