@@ -107,3 +107,30 @@ def test_valid_recursion_seal_passes_validity(oracle, suite):
     seal, _mix, _ = oracle.prove_segment("recursion", s, po2, code, data, accum, glob, version=None)
     assert verifier.verify(oracle, "recursion", seal, s, check_validity=True)["validity"] is True
     assert r.verify_seal("recursion", s, seal) == po2
+
+
+def test_native_verifier_rejects_garbage(oracle):
+    """Malformed seals (empty, random words, a valid prefix with a tampered po2 or cut
+    anywhere) come back as errors, never as a crash or an out-of-bounds read."""
+    import risc0_amd as r
+    _native_lib_or_skip(oracle)
+    rng = np.random.default_rng(99)
+    for circuit in ("rv32im", "recursion"):
+        for s in (0, 1, 2):
+            for n in (0, 1, 5, 64, 4096):
+                junk = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+                if circuit == "rv32im" and n:
+                    junk[0] = 2
+                with pytest.raises(r.R0HipError):
+                    r.verify_seal(circuit, s, junk, check_validity=False)
+    code, data, accum, glob = G.seal_inputs(oracle, "recursion", 8)
+    seal, _mix, _ = oracle.prove_segment("recursion", 0, 8, code, data, accum, glob)
+    po2_at = verifier.Taps("recursion").d["output_size"]
+    for po2 in (0, 1, 9, 25, 2**31):
+        bad = seal.copy()
+        bad[po2_at] = po2
+        with pytest.raises(r.R0HipError):
+            r.verify_seal("recursion", 0, bad, check_validity=False)
+    for cut in rng.integers(1, seal.size, 20):
+        with pytest.raises(r.R0HipError, match="seal too short"):
+            r.verify_seal("recursion", 0, seal[:cut], check_validity=False)
