@@ -82,9 +82,8 @@ R0_HD void poseidon2_mix_simple(uint32_t* c) {
 //  * sbox: x^2 canonical, then three REDCs without the final umin: each product has
 //    one factor < p and one < 2p, so t < 2p^2 < p*2^32 and the result is < 2p;
 //  * M_EXT runs in 64-bit on those lazy (< 2p) cells: every output is a combination
-//    with coefficient sum <= 112, so y < 224p < 2^39, and one Barrett step
-//    (q = ((y >> 7) * 273) >> 32 is floor(y/p) or one less) plus a umin gives the
-//    canonical cell — the next round constant is added in 64-bit before it;
+//    with coefficient sum <= 112, so y < 224p < 2^39; the next round constant is
+//    added in 64-bit and one lazy REDC feeds the S-box (scaled rounds, below);
 //  * M_INT: c_i*d_i + S = REDC(c_i*d_i + S*2^32) and S*2^32 is congruent to
 //    fold64(sum c_i * (2^32 mod p)) < 2^60, so multiply, add and reduce are one
 //    v_mad_u64_u32 plus one REDC (t < p^2 + 2^60 < p*2^32).
@@ -139,6 +138,55 @@ R0_HD void p2_m_ext64(const uint32_t* x, uint64_t* y) {
   }
 }
 
+// Full rounds without Barrett steps. A full round's M_EXT output y (< 224p + p with the
+// next round constant) goes straight into a lazy REDC, which returns y * 2^-32 mod p in
+// [0, p + 106) in two instructions instead of p2_red39's seven; that is small enough for
+// the S-box's first Montgomery square. The REDC leaves the state scaled by 2^-32, so in
+// round r the stored cells are X * sigma_r (X the true value, R = 2^32 mod p):
+//   sigma_{r+1} = (sigma_r R^-1)^7 R^-6      (one REDC, then the S-box's four)
+// and the round constants are stored pre-multiplied by sigma_r R^-1. One Montgomery
+// multiply by R^3 / sigma restores the Montgomery form (X * R) before the partial rounds
+// and at the end. Rounds 0 and 5 start from sigma = R, so their constants are unchanged.
+struct P2Scaled {
+  uint32_t rc[8 * 24];  // rounds 0-3 and 5-7 (round 4 uses kP2Full as it is)
+  uint32_t k_mid, k_end;
+};
+constexpr uint32_t p2c_mul(uint32_t a, uint32_t b) { return uint32_t(uint64_t(a) * b % kP); }
+constexpr uint32_t p2c_pow(uint32_t a, uint64_t e) {
+  uint32_t r = 1;
+  while (e) {
+    if (e & 1) r = p2c_mul(r, a);
+    a = p2c_mul(a, a);
+    e >>= 1;
+  }
+  return r;
+}
+constexpr P2Scaled p2_make_scaled() {
+  P2Scaled t{};
+  const uint32_t full[8 * 24] = P2_FULL_RC_MONT;
+  const uint32_t R = uint32_t((uint64_t(1) << 32) % kP), Rinv = p2c_pow(R, kP - 2);
+  const uint32_t R3 = p2c_pow(R, 3), Rm6 = p2c_pow(Rinv, 6);
+  for (int half = 0; half < 2; half++) {
+    const int r0 = half ? 5 : 0, r1 = half ? 8 : 4;
+    uint32_t sigma = R;
+    for (int r = r0; r < r1; r++) {
+      const uint32_t s = p2c_mul(sigma, Rinv);
+      for (int i = 0; i < 24; i++) t.rc[r * 24 + i] = p2c_mul(full[r * 24 + i], s);
+      sigma = p2c_mul(p2c_pow(s, 7), Rm6);
+    }
+    const uint32_t k = p2c_mul(R3, p2c_pow(sigma, kP - 2));
+    if (half) t.k_end = k;
+    else t.k_mid = k;
+  }
+  for (int i = 0; i < 24; i++) t.rc[4 * 24 + i] = full[4 * 24 + i];
+  return t;
+}
+#if defined(__HIP_DEVICE_COMPILE__)
+__constant__ static const P2Scaled kP2S = p2_make_scaled();
+#else
+static constexpr P2Scaled kP2S = p2_make_scaled();
+#endif
+
 R0_HD void poseidon2_mix(uint32_t* c) {
   uint64_t y[24];
   uint32_t x[24];
@@ -146,11 +194,11 @@ R0_HD void poseidon2_mix(uint32_t* c) {
 #pragma unroll
   for (int r = 0; r < 4; r++) {
 #pragma unroll
-    for (int i = 0; i < 24; i++) x[i] = p2_sbox_lazy(p2_red39(y[i] + kP2Full[r * 24 + i]));
+    for (int i = 0; i < 24; i++) x[i] = p2_sbox_lazy(mont_lazy(y[i] + kP2S.rc[r * 24 + i]));
     p2_m_ext64(x, y);
   }
 #pragma unroll
-  for (int i = 0; i < 24; i++) c[i] = p2_red39(y[i]);
+  for (int i = 0; i < 24; i++) c[i] = fp_mul(mont_lazy(y[i]), kP2S.k_mid);
 #pragma unroll
   // Partial rounds keep every cell lazy in [0, 2p): with cells c < X the M_INT output
   // REDC(c*d + sf) < 0.469 X + sf/2^32 + p, whose fixed point (sf < 2^57 + 2^32 after
@@ -170,13 +218,16 @@ R0_HD void poseidon2_mix(uint32_t* c) {
 #pragma unroll
   for (int i = 0; i < 24; i++) c[i] = umin(c[i], c[i] - kP);
 #pragma unroll
-  for (int r = 4; r < 8; r++) {
+  for (int i = 0; i < 24; i++) x[i] = p2_sbox_lazy(fp_add(c[i], kP2Full[4 * 24 + i]));
+  p2_m_ext64(x, y);
 #pragma unroll
-    for (int i = 0; i < 24; i++) x[i] = p2_sbox_lazy(fp_add(c[i], kP2Full[r * 24 + i]));
+  for (int r = 5; r < 8; r++) {
+#pragma unroll
+    for (int i = 0; i < 24; i++) x[i] = p2_sbox_lazy(mont_lazy(y[i] + kP2S.rc[r * 24 + i]));
     p2_m_ext64(x, y);
-#pragma unroll
-    for (int i = 0; i < 24; i++) c[i] = p2_red39(y[i]);
   }
+#pragma unroll
+  for (int i = 0; i < 24; i++) c[i] = fp_mul(mont_lazy(y[i]), kP2S.k_end);
 }
 
 }  // namespace r0
