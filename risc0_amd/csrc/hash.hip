@@ -33,29 +33,25 @@ __global__ __launch_bounds__(kThreads) void p2_rows_kernel(uint32_t* out, const 
   uint32_t c[24];
 #pragma unroll
   for (int i = 0; i < 24; i++) c[i] = 0;
-  // full blocks of 16 columns, software-pipelined: the next block's 16 loads are in
-  // flight while the current block is permuted
-  const uint32_t full = cols / 16;
+  // blocks of 16 columns (the last one zero-padded; cols == 0 is one all-zero block),
+  // software-pipelined: the next block's loads are in flight while the current block is
+  // permuted. One permutation call site keeps the kernel small for the instruction cache.
+  const uint32_t nblk = cols ? (cols + 15) / 16 : 1;
   uint32_t nxt[16];
-  if (full) {
-#pragma unroll
-    for (int i = 0; i < 16; i++) nxt[i] = m[uint64_t(i) * rows + row];
-  }
-  for (uint32_t b = 0; b < full; b++) {
-#pragma unroll
-    for (int i = 0; i < 16; i++) c[i] = nxt[i];
-    if (b + 1 < full) {
-      const uint32_t col = (b + 1) * 16;
+  auto load = [&](uint32_t col) {
+    if (col + 16 <= cols) {
 #pragma unroll
       for (int i = 0; i < 16; i++) nxt[i] = m[uint64_t(col + i) * rows + row];
-    }
-    poseidon2_mix(c);
-  }
-  const uint32_t col = full * 16;
-  if (col < cols || cols == 0) {
-    uint32_t rem = cols - col;
+    } else {
 #pragma unroll
-    for (int i = 0; i < 16; i++) c[i] = (uint32_t)i < rem ? m[uint64_t(col + i) * rows + row] : 0u;
+      for (int i = 0; i < 16; i++) nxt[i] = col + i < cols ? m[uint64_t(col + i) * rows + row] : 0u;
+    }
+  };
+  load(0);
+  for (uint32_t b = 0; b < nblk; b++) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) c[i] = nxt[i];
+    if (b + 1 < nblk) load((b + 1) * 16);
     poseidon2_mix(c);
   }
   store_digest(out + row * 8, c);

@@ -191,7 +191,9 @@ R0_HD void poseidon2_mix(uint32_t* c) {
   uint64_t y[24];
   uint32_t x[24];
   p2_m_ext64(c, y);
-#pragma unroll
+  // rolled: each round's 24 constants are loaded at the top of its iteration instead of
+  // all 168 living in SGPRs (which spill to VGPR lanes in hash_rows)
+#pragma unroll 1
   for (int r = 0; r < 4; r++) {
 #pragma unroll
     for (int i = 0; i < 24; i++) x[i] = p2_sbox_lazy(mont_lazy(y[i] + kP2S.rc[r * 24 + i]));
@@ -220,7 +222,7 @@ R0_HD void poseidon2_mix(uint32_t* c) {
 #pragma unroll
   for (int i = 0; i < 24; i++) x[i] = p2_sbox_lazy(fp_add(c[i], kP2Full[4 * 24 + i]));
   p2_m_ext64(x, y);
-#pragma unroll
+#pragma unroll 1
   for (int r = 5; r < 8; r++) {
 #pragma unroll
     for (int i = 0; i < 24; i++) x[i] = p2_sbox_lazy(mont_lazy(y[i] + kP2S.rc[r * 24 + i]));
