@@ -136,7 +136,22 @@ void* scratch(size_t bytes, int slot) {
       HIP_OK(hipFree(s.p));
     }
     size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
-    HIP_OK(hipMalloc(&s.p, want));
+    s.p = nullptr;
+    {
+      // a block left by an exited thread (bench and pipeline threads come and go; each
+      // new one would otherwise hipMalloc its eval_check scratch again, GBs at po2 >= 20)
+      std::lock_guard<std::mutex> lk(g_mu);
+      auto ot = g_orphans.lower_bound(bytes);
+      if (ot != g_orphans.end() && ot->first <= 2 * want) {
+        s.p = ot->second;
+        want = ot->first;
+        g_orphans.erase(ot);
+      }
+    }
+    if (!s.p && hipMalloc(&s.p, want) != hipSuccess) {
+      dev_trim();
+      HIP_OK(hipMalloc(&s.p, want));
+    }
     s.bytes = want;
   }
   return s.p;
