@@ -5,8 +5,11 @@ A step proves one rv32im segment of 2^po2 cycles on one GPU: from the witness
 groups already resident in HBM (code 1 / data 211 / accum 103 columns, synthetic,
 seeded per segment) to the seal (Vec<u32>) on the host, through the whole STARK
 prover (commit code/data/accum, eval_check, DEEP-ALI, FRI, query openings).
-Multi-GPU: one process per GPU (torch.distributed.run), whole segments sharded per
-rank, no data-path collective (gloo only for the barrier and the max-time reduce).
+Multi-GPU: one process per GPU, whole segments sharded per rank, no data-path
+collective (gloo only for the barriers, the max-time reduce and the host-side gather of
+seal digests). The ranks come from torch.distributed.run, or — when `--gpus N` is given
+without a launcher — from risc0_amd.segments.launch_local, which starts N rank processes
+(rank r on device r) before anything touches a GPU, as r0vm spawns one worker per GPU.
 
 Prints ONE JSON line (rank 0). Extra diagnostics go to stderr.
 """
@@ -52,6 +55,8 @@ def synthetic_witness(rng, circuit, po2):
 
 def main():
     args = parse()
+    from risc0_amd.segments import maybe_launch
+    maybe_launch(args.gpus, os.path.abspath(__file__))  # no WORLD_SIZE and --gpus > 1: spawn the ranks
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -122,6 +127,10 @@ def main():
     phase_tot.clear()
     _t, t = timed_segments(prove_batch, [segs], 0, hal.synchronize, dist)
     seal = last["seal"]
+    # host-side gather of one seal digest per rank (the receipts stay on their hosts)
+    from risc0_amd.segments import gather_results
+    import hashlib
+    digests = gather_results({rank: hashlib.sha256(seal.tobytes()).hexdigest()[:16]}, dist)
     cycles_total = world * args.steps * (1 << args.po2)
     value = cycles_total / t
     ms_per_step = 1000.0 * t / args.steps
@@ -159,7 +168,8 @@ def main():
                                    "witness resident in HBM -> seal on host",
                        "circuit": args.circuit, "po2": args.po2, "hashfn": args.hashfn,
                        "segments_per_gpu": args.steps, "segments_in_flight_per_gpu": k,
-                       "parallelism": f"segment-per-gpu x{world}"},
+                       "parallelism": f"segment-per-gpu x{world}",
+                       "seal_sha256_by_rank": [digests[i] for i in range(world)]},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

@@ -153,12 +153,22 @@ const char* r0hip_prove_segments(const char* circuit, int suite, uint32_t po2, i
  * fri.rs:36-155, read_iop.rs:20-84; rv32im seals lead with the version word 2,
  * circuit/rv32im/src/lib.rs:78-92) ----
  * Replays the transcript and checks the constraint validity equation poly_ext(z) ==
- * check(z) * ((3z)^N - 1) (mod.rs:340-394; skipped when check_validity == 0, for seals of
- * synthetic witnesses), every Merkle opening, every FRI fold, the final FRI polynomial and
- * the seal length. Host-only: needs no GPU and no r0hip_init. Returns NULL when the seal
- * verifies (po2 of the segment in *po2_out, if non-NULL), else the failed check. */
+ * check(z) * ((3z)^N - 1) (mod.rs:340-394), every Merkle opening, every FRI fold, the final
+ * FRI polynomial, that every field word read is canonical (read_field_elem_slice,
+ * read_iop.rs:45-48) and the seal length. check_code (mod.rs:531): the code/control root is
+ * written to h_code_root_out (8 words, if non-NULL), and when n_code_roots > 0 it must equal
+ * one of the n_code_roots digests at h_code_roots (8 words each) — the recursion circuit's
+ * control-id allow-list (zkvm/src/receipt/succinct.rs:143-157). Host-only: needs no GPU and
+ * no r0hip_init. Returns NULL when the seal verifies (po2 of the segment in *po2_out, if
+ * non-NULL), else the failed check. */
 const char* r0hip_verify_seal(const char* circuit, int suite, const uint32_t* seal, size_t seal_len,
-                              int check_validity, uint32_t* po2_out);
+                              const uint32_t* h_code_roots, size_t n_code_roots, uint32_t* h_code_root_out,
+                              uint32_t* po2_out);
+/* TESTING ONLY — never use it to accept a receipt. r0hip_verify_seal without the validity
+ * equation and without a code-root check, for seals of synthetic witnesses (which do not
+ * satisfy the constraints) in the parity tests. */
+const char* r0hip_testing_verify_seal_structure(const char* circuit, int suite, const uint32_t* seal,
+                                                size_t seal_len, uint32_t* po2_out);
 /* PolyExt::poly_ext of the circuit (its generated poly_ext.rs, called at mod.rs:356-386): the
  * constraint polynomial at the out-of-domain point. h_mix (mix_size) and h_global
  * (output_size) are Montgomery words, h_eval_u one FpExt (4 words) per tap in tap order,

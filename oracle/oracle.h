@@ -53,6 +53,13 @@ const char* oracle_eval_check(const oracle_circuit_t* c, uint32_t* check, const 
                               const uint32_t* mix, const uint32_t* global,
                               const uint32_t* poly_mix, uint32_t po2);
 
+// eval_check of groups filled by r0hip_fill_uniform(group_seeds[g]) at po2, evaluated only
+// at the n given cycles (out: n x 4 words, point-major), for full-size parity tests.
+const char* oracle_eval_check_sampled(const oracle_circuit_t* c, const uint64_t* group_seeds,
+                                      const uint32_t* mix, const uint32_t* global,
+                                      const uint32_t* poly_mix, uint32_t po2, const uint64_t* cycles,
+                                      size_t n, uint32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

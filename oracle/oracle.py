@@ -40,6 +40,7 @@ def lib():
         _lib = C.CDLL(LIB_PATH)
         _lib.oracle_prove_segment.restype = C.c_void_p
         _lib.oracle_eval_check.restype = C.c_void_p
+        _lib.oracle_eval_check_sampled.restype = C.c_void_p
         _lib.oracle_combos_divide.restype = C.c_long
         _lib.oracle_rng_new.restype = C.c_void_p
         for f in ("oracle_rng_free", "oracle_rng_mix", "oracle_rng_random_bits", "oracle_rng_random_elem"):
@@ -294,6 +295,31 @@ def eval_check(name, check, groups, mix, glob, poly_mix, po2):
     arr = (u32p * len(groups))(*[ptr(g) for g in groups])
     _check(lib().oracle_eval_check(C.byref(c), ptr(check), arr, ptr(mix), ptr(glob), ptr(poly_mix),
                                    C.c_uint32(po2)))
+
+
+def splitmix_fill(seed, n, start=0):
+    """The synthetic words r0hip_fill_uniform writes (splitmix64 of (seed, index) mod p),
+    for indices [start, start + n)."""
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + (np.arange(start, start + n, dtype=np.uint64) + np.uint64(1)) * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    return (z % np.uint64(P)).astype(np.uint32)
+
+
+def eval_check_sampled(name, group_seeds, mix, glob, poly_mix, po2, cycles):
+    """eval_check over groups filled by r0hip_fill_uniform(group_seeds[g]) (group ids:
+    accum 0, code 1, data 2), evaluated only at `cycles`; returns (len(cycles), 4)."""
+    c, keep, _ = make_circuit(name)
+    seeds = np.ascontiguousarray(group_seeds, dtype=np.uint64)
+    cyc = np.ascontiguousarray(cycles, dtype=np.uint64)
+    out = np.zeros(4 * cyc.size, np.uint32)
+    u64p = C.POINTER(C.c_uint64)
+    _check(lib().oracle_eval_check_sampled(C.byref(c), seeds.ctypes.data_as(u64p), ptr(mix), ptr(glob),
+                                           ptr(poly_mix), C.c_uint32(po2), cyc.ctypes.data_as(u64p),
+                                           sz(cyc.size), ptr(out)))
+    return out.reshape(-1, 4)
 
 
 def prove_segment(name, suite, po2, code, data, accum, glob, version=None):

@@ -8,6 +8,7 @@
 //   risc0/zkp/src/prove/write_iop.rs:24-76
 //   risc0/zkp/src/core/poly.rs:23-89
 //   risc0/circuit/rv32im/src/prove/hal/mod.rs:143-224 (segment header / group order)
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -227,6 +228,67 @@ void eval_check(const oracle_circuit_t* c, uint32_t* check, const uint32_t** gro
   });
 }
 
+// Full-size eval_check at sampled cycles (test infrastructure). The evaluated groups are
+// the device's synthetic words (r0hip_fill_uniform: splitmix64 of (seed, index) mod p), so
+// any tap value is recomputed here from its index instead of copying GB-sized buffers to
+// the host. The reference poly_fp reads a tap only as args[col*steps + ((cycle - 4*back) &
+// (steps-1))] (rv32im-sys/kernels/cxx/rust_poly_fp_*.cpp), so each sampled cycle is
+// evaluated on a small window domain holding, for every column, the values at
+// cycle - 4*back of the full domain; the result is multiplied by the full-size
+// ((3*w^cycle)^N - 1)^-1 exactly as eval_check above (cpu.rs:145-207).
+static uint32_t splitmix_word(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + (i + 1) * 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  z ^= z >> 31;
+  return uint32_t(z % P);
+}
+
+void eval_check_sampled(const oracle_circuit_t* c, const uint64_t* group_seeds, const uint32_t* mix,
+                        const uint32_t* global, ExtElem poly_mix, uint32_t po2, const uint64_t* cycles,
+                        size_t n, uint32_t* out) {
+  if (!c->poly_fp) throw std::runtime_error("circuit has no poly_fp (oracle/_ref not built?)");
+  TapSet taps{c};
+  uint32_t max_back = 0;
+  for (size_t i = 0; i < c->n_taps; i++) max_back = std::max(max_back, taps.tap(i)->back);
+  size_t win = 1;
+  while (win < INV_RATE * (max_back + 2)) win <<= 1;
+  const size_t steps = size_t(1) << po2, domain = steps * INV_RATE;
+  std::vector<ExtElem> pows = map_pow(poly_mix, c->poly_mix_powers, c->n_poly_mix);
+  Elem rou = rou_fwd(po2 + 2);
+  for (size_t s = 0; s < n; s++)
+    if (cycles[s] >= domain) throw std::runtime_error("sampled cycle out of range");
+  parallel_for(n, [&](size_t b, size_t e) {
+    std::vector<Buf> w(c->n_groups);
+    for (size_t g = 0; g < c->n_groups; g++) w[g].assign(taps.group_size(g) * win, 0);
+    std::vector<const uint32_t*> args(c->n_eval_args);
+    for (size_t s = b; s < e; s++) {
+      uint64_t cyc = cycles[s];
+      size_t local = INV_RATE * (max_back + 1) + (cyc & 3);  // same coset, every back in range
+      for (size_t g = 0; g < c->n_groups; g++) {
+        size_t gs = taps.group_size(g);
+        for (size_t col = 0; col < gs; col++)
+          for (uint32_t bk = 0; bk <= max_back; bk++) {
+            uint64_t full = (cyc - INV_RATE * bk) & (domain - 1);
+            w[g][col * win + ((local - INV_RATE * bk) & (win - 1))] =
+                splitmix_word(group_seeds[g], col * domain + full);
+          }
+      }
+      for (size_t i = 0; i < c->n_eval_args; i++) {
+        int a = c->eval_args[i];
+        args[i] = a >= 0 ? w[a].data() : (a == -1 ? mix : global);
+      }
+      uint32_t tot_w[4];
+      const char* err = c->poly_fp(local, win, &pows[0].e[0].v, args.data(), tot_w);
+      if (err) abort();
+      ExtElem tot = ExtElem::raw(tot_w);
+      Elem y = (Elem::from(3) * rou.pow(cyc)).pow(steps);
+      ExtElem ret = tot * (y - Elem::one()).inv();
+      for (size_t i = 0; i < 4; i++) out[s * 4 + i] = ret.e[i].v;
+    }
+  });
+}
+
 struct Prover {
   const oracle_circuit_t* c;
   TapSet taps;
@@ -406,6 +468,18 @@ extern "C" const char* oracle_eval_check(const oracle_circuit_t* c, uint32_t* ch
                                          uint32_t po2) {
   try {
     eval_check(c, check, groups, mix, global, ExtElem::raw(poly_mix), po2);
+  } catch (const std::exception& e) {
+    return strdup(e.what());
+  }
+  return nullptr;
+}
+
+extern "C" const char* oracle_eval_check_sampled(const oracle_circuit_t* c, const uint64_t* group_seeds,
+                                                 const uint32_t* mix, const uint32_t* global,
+                                                 const uint32_t* poly_mix, uint32_t po2, const uint64_t* cycles,
+                                                 size_t n, uint32_t* out) {
+  try {
+    eval_check_sampled(c, group_seeds, mix, global, ExtElem::raw(poly_mix), po2, cycles, n, out);
   } catch (const std::exception& e) {
     return strdup(e.what());
   }

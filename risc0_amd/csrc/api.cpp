@@ -34,8 +34,10 @@ const char* wrap(F f) {
     f();
     HIP_OK(hipStreamSynchronize(stream()));
   } catch (const std::exception& e) {
+    drain_after_error();
     return strdup(e.what());
   } catch (...) {
+    drain_after_error();
     return strdup("r0hip: unknown error");
   }
   return nullptr;

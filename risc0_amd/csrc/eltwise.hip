@@ -25,25 +25,25 @@ __device__ __forceinline__ void st_fe(uint32_t* p, FpExt a) {
 
 // ---- element-wise ---------------------------------------------------------------
 __global__ void add_kernel(uint32_t* o, const uint32_t* a, const uint32_t* b, uint64_t n) {
-  uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
-  if (i < n) o[i] = fp_add(a[i], b[i]);
+  for (uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x; i < n; i += uint64_t(gridDim.x) * kThreads)
+    o[i] = fp_add(a[i], b[i]);
 }
 // cpu.rs:518-522: INVALID (0xffffffff) -> 0
 __global__ void zeroize_kernel(uint32_t* io, uint64_t n) {
-  uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
-  if (i < n && io[i] == 0xffffffffu) io[i] = 0;
+  for (uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x; i < n; i += uint64_t(gridDim.x) * kThreads)
+    if (io[i] == 0xffffffffu) io[i] = 0;
 }
 // synthetic witness words (uniform canonical BabyBear values): a
 // splitmix64 counter hash of (seed, index), reduced mod p — for benches and tests at sizes
 // whose host generation and upload would dominate
 __global__ void fill_uniform_kernel(uint32_t* o, uint64_t n, uint64_t seed) {
-  uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
-  if (i >= n) return;
-  uint64_t z = seed + (i + 1) * 0x9e3779b97f4a7c15ull;
-  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-  z ^= z >> 31;
-  o[i] = uint32_t(z % kP);
+  for (uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x; i < n; i += uint64_t(gridDim.x) * kThreads) {
+    uint64_t z = seed + (i + 1) * 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    z ^= z >> 31;
+    o[i] = uint32_t(z % kP);
+  }
 }
 // cpu.rs:475-500: out[k*count + idx] = (sum_i in[i*count + idx])[k]
 __global__ void sum_extelem_kernel(uint32_t* out, const uint32_t* in, uint64_t count, uint32_t to_add) {
@@ -87,10 +87,11 @@ __global__ void scatter_kernel(uint32_t* into, const uint32_t* index, const uint
 __global__ void copy_slice_kernel(uint32_t* into, const uint32_t* from, uint64_t rows, uint64_t cols,
                                   uint64_t from_offset, uint64_t from_stride, uint64_t into_offset,
                                   uint64_t into_stride) {
-  uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
-  if (i >= rows * cols) return;
-  uint64_t r = i / cols, c = i % cols;
-  into[into_offset + r * into_stride + c] = from[from_offset + r * from_stride + c];
+  for (uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x; i < rows * cols;
+       i += uint64_t(gridDim.x) * kThreads) {
+    uint64_t r = i / cols, c = i % cols;
+    into[into_offset + r * into_stride + c] = from[from_offset + r * from_stride + c];
+  }
 }
 
 // ---- mix_poly_coeffs (cpu.rs:410-455) ---------------------------------------------
@@ -381,7 +382,7 @@ __global__ void gather_words_kernel(uint32_t* dst, const uint32_t* const* bases,
 
 void eltwise_add(hipStream_t s, uint32_t* out, const uint32_t* a, const uint32_t* b, size_t n) {
   if (!n) return;
-  hipLaunchKernelGGL(add_kernel, dim3(div_up(n, kThreads)), dim3(kThreads), 0, s, out, a, b, uint64_t(n));
+  hipLaunchKernelGGL(add_kernel, dim3(grid_stride(n, kThreads)), dim3(kThreads), 0, s, out, a, b, uint64_t(n));
   HIP_OK(hipGetLastError());
 }
 void eltwise_copy(hipStream_t s, uint32_t* out, const uint32_t* in, size_t n) {
@@ -390,12 +391,12 @@ void eltwise_copy(hipStream_t s, uint32_t* out, const uint32_t* in, size_t n) {
 }
 void eltwise_zeroize(hipStream_t s, uint32_t* io, size_t n) {
   if (!n) return;
-  hipLaunchKernelGGL(zeroize_kernel, dim3(div_up(n, kThreads)), dim3(kThreads), 0, s, io, uint64_t(n));
+  hipLaunchKernelGGL(zeroize_kernel, dim3(grid_stride(n, kThreads)), dim3(kThreads), 0, s, io, uint64_t(n));
   HIP_OK(hipGetLastError());
 }
 void fill_uniform(hipStream_t s, uint32_t* out, size_t n, uint64_t seed) {
   if (!n) return;
-  hipLaunchKernelGGL(fill_uniform_kernel, dim3(div_up(n, kThreads)), dim3(kThreads), 0, s, out, uint64_t(n), seed);
+  hipLaunchKernelGGL(fill_uniform_kernel, dim3(grid_stride(n, kThreads)), dim3(kThreads), 0, s, out, uint64_t(n), seed);
   HIP_OK(hipGetLastError());
 }
 void eltwise_sum_extelem(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count, size_t to_add) {
@@ -428,7 +429,7 @@ void scatter(hipStream_t s, uint32_t* into, const uint32_t* index, const uint32_
 void copy_elem_slice(hipStream_t s, uint32_t* into, const uint32_t* from, size_t rows, size_t cols,
                      size_t from_offset, size_t from_stride, size_t into_offset, size_t into_stride) {
   if (!rows || !cols) return;
-  hipLaunchKernelGGL(copy_slice_kernel, dim3(div_up(rows * cols, kThreads)), dim3(kThreads), 0, s, into, from,
+  hipLaunchKernelGGL(copy_slice_kernel, dim3(grid_stride(rows * cols, kThreads)), dim3(kThreads), 0, s, into, from,
                      uint64_t(rows), uint64_t(cols), uint64_t(from_offset), uint64_t(from_stride),
                      uint64_t(into_offset), uint64_t(into_stride));
   HIP_OK(hipGetLastError());

@@ -373,11 +373,11 @@ __global__ __launch_bounds__(kThreads) void bit_reverse_tiles(uint32_t* io, uint
 // cpu.rs:395-408. 3^{rev(i)} = A[rev_h(lo)] * B[rev_{L-h}(hi)], i = hi*2^h + lo.
 __global__ __launch_bounds__(kThreads) void zk_shift_kernel(uint32_t* io, uint64_t n, uint32_t L, uint32_t h,
                                                           const uint32_t* A, const uint32_t* B) {
-  uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
-  if (i >= n) return;
-  uint32_t pos = uint32_t(i & ((uint64_t(1) << L) - 1));
-  uint32_t lo = pos & ((1u << h) - 1), hi = pos >> h;
-  io[i] = fp_mul(io[i], fp_mul(A[bitrev_n(lo, h)], B[bitrev_n(hi, L - h)]));
+  for (uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x; i < n; i += uint64_t(gridDim.x) * kThreads) {
+    uint32_t pos = uint32_t(i & ((uint64_t(1) << L) - 1));
+    uint32_t lo = pos & ((1u << h) - 1), hi = pos >> h;
+    io[i] = fp_mul(io[i], fp_mul(A[bitrev_n(lo, h)], B[bitrev_n(hi, L - h)]));
+  }
 }
 
 // ---- host-side table generation ---------------------------------------------
@@ -614,7 +614,7 @@ void zk_shift(hipStream_t s, uint32_t* io, size_t count, uint32_t L) {
     }
     return t;
   });
-  hipLaunchKernelGGL(zk_shift_kernel, dim3(div_up(n, kThreads)), dim3(kThreads), 0, s, io, n, L, h, A, B);
+  hipLaunchKernelGGL(zk_shift_kernel, dim3(grid_stride(n, kThreads)), dim3(kThreads), 0, s, io, n, L, h, A, B);
   HIP_OK(hipGetLastError());
 }
 

@@ -138,6 +138,9 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
               if (j.h_seal) memcpy(j.h_seal, seal.data(), seal.size() * 4);
             } catch (const std::exception& e) {
               j.error = dup_msg(e.what());
+              // kernels queued before the throw may still read this buffer set: drain
+              // them before the uploader refills it
+              drain_after_error();
             }
           }
           free_q.put(s);

@@ -106,6 +106,10 @@ hipStream_t stream() {
   return t_ctx.stream;
 }
 
+void drain_after_error() noexcept {
+  if (t_ctx.stream) (void)hipStreamSynchronize(t_ctx.stream);
+}
+
 const uint32_t* dev_table(const std::string& key, const std::function<std::vector<uint32_t>()>& gen) {
   ensure_init();
   {

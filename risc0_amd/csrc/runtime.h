@@ -38,6 +38,10 @@ const uint32_t* dev_table(const std::string& key, const std::function<std::vecto
 
 // Scratch buffer reused across calls (grown on demand; stream-ordered use only).
 void* scratch(size_t bytes, int slot = 0);
+// After an error: wait for whatever this thread already queued on its stream (ignoring the
+// status), so no buffer is reused or handed to another thread while kernels still use it.
+// Only a thread that has a stream drains; it never creates one.
+void drain_after_error() noexcept;
 
 // Stream-ordered host->device upload through a pinned bump arena, so the caller's
 // host data may die immediately. The arena is recycled by stage_reset() (call only
@@ -56,7 +60,20 @@ struct KScope {
 void ktimer_enable(bool on);
 std::string ktimer_report();  // "name=total_ms:calls:alg_bytes:alg_modmuls;..." (synchronises)
 
-inline unsigned div_up(size_t a, size_t b) { return unsigned((a + b - 1) / b); }
+// Workgroups for a 1-D launch of a lanes at b per workgroup. An AQL dispatch counts
+// work-items in 32 bits, so a grid of 2^32 or more lanes cannot launch; such sizes go
+// through grid_stride() instead.
+inline unsigned div_up(size_t a, size_t b) {
+  const size_t g = (a + b - 1) / b;
+  R0_REQUIRE(g * b < (size_t(1) << 32), "1-D launch of " + std::to_string(a) + " lanes exceeds the 32-bit grid");
+  return unsigned(g);
+}
+// Grid for element-wise kernels that stride over n elements (for (i = gid; i < n; i += lanes)):
+// at most 2^20 workgroups (every CU stays busy), never above the 32-bit grid.
+inline unsigned grid_stride(size_t n, size_t b) {
+  const size_t g = (n + b - 1) / b;
+  return unsigned(g < (size_t(1) << 20) ? g : (size_t(1) << 20));
+}
 
 // ---- launchers (all asynchronous on `s`) -----------------------------------
 // NTT family (ntt.hip). Sizes are log2 of the per-polynomial length.

@@ -6,8 +6,11 @@
 //   the rest          verify_core.h (read IOP, Merkle, verify_validity, FRI)
 // Everything the reference checks is checked: transcript replay, the validity equation
 // (mod.rs:340-394, with poly_ext run from the circuit's constraint program), every Merkle
-// path, every FRI fold, the final polynomial and the seal length. The validity check can be
-// switched off for seals of synthetic witnesses, which do not satisfy the constraints.
+// path, every FRI fold, the final polynomial and the seal length, plus the check_code hook
+// (mod.rs:531): the code (control) root is returned, and when the caller passes an allow-list
+// the root must be in it. Field words in the seal must be canonical (read_field_elem_slice).
+// r0hip_testing_verify_seal_structure skips the validity equation for seals of synthetic
+// witnesses, which do not satisfy the constraints; it is for tests, never for receipts.
 // Host code only — no HIP call, so it runs without a GPU.
 #include <cstdlib>
 #include <cstring>
@@ -55,7 +58,8 @@ FpExt poly_ext(const CircuitDef& c, const uint32_t* mix, const uint32_t* global,
 namespace {
 using namespace vfy;
 
-uint32_t verify_seal(const CircuitDef& c, int suite, const uint32_t* seal, size_t len, bool check_validity) {
+uint32_t verify_seal(const CircuitDef& c, int suite, const uint32_t* seal, size_t len, bool check_validity,
+                     const uint32_t* code_roots, size_t n_code_roots, uint32_t* code_root_out) {
   if (c.name == std::string("rv32im")) {  // rv32im/src/lib.rs:78-92: a version word leads the seal
     if (len < 1 || seal[0] != 2) throw VerifyError("bad rv32im seal version");
     seal++;
@@ -69,13 +73,21 @@ uint32_t verify_seal(const CircuitDef& c, int suite, const uint32_t* seal, size_
   }
   iop.commit(hash_elems(suite, psi, 16));
   iop.commit(hash_elems(suite, ci, 16));
-  const uint32_t* header = iop.read(c.output_size + 1);
+  const uint32_t* header = iop.read_elems(c.output_size + 1);
   iop.commit(hash_elems(suite, header, c.output_size + 1));
   const uint32_t po2 = header[c.output_size];
   if (po2 < 2 || po2 > 24) throw VerifyError("po2 out of range");
   const size_t domain = INV_RATE * (size_t(1) << po2);
   // groups in commit order: code, data, then (after the mix draw) accum (mod.rs:215-244)
   MerkleVerifier code(iop, domain, c.group_sizes[1]);
+  // check_code(po2, code_root) (mod.rs:531): e.g. the recursion control-id inclusion check
+  // (zkvm/src/receipt/succinct.rs:143-157) is made against the allow-list the caller passes
+  if (code_root_out) memcpy(code_root_out, code.root.w, 32);
+  if (n_code_roots) {
+    bool found = false;
+    for (size_t i = 0; i < n_code_roots && !found; i++) found = same(digest_of(code_roots + 8 * i), code.root);
+    if (!found) throw VerifyError("code root is not in the allowed set");
+  }
   MerkleVerifier data(iop, domain, c.group_sizes[2]);
   std::vector<uint32_t> mix(c.mix_size);
   for (auto& m : mix) m = iop.rng->random_elem();
@@ -93,14 +105,16 @@ uint32_t verify_seal(const CircuitDef& c, int suite, const uint32_t* seal, size_
 
 using namespace r0;
 
-extern "C" const char* r0hip_verify_seal(const char* circuit, int suite, const uint32_t* seal, size_t seal_len,
-                                         int check_validity, uint32_t* po2_out) {
+static const char* verify_entry(const char* circuit, int suite, const uint32_t* seal, size_t seal_len,
+                                bool check_validity, const uint32_t* code_roots, size_t n_code_roots,
+                                uint32_t* code_root_out, uint32_t* po2_out) {
   try {
     const CircuitDef* c = find_circuit(circuit ? circuit : "");
     R0_REQUIRE(c, std::string("unknown circuit ") + (circuit ? circuit : "(null)"));
     R0_REQUIRE(suite >= 0 && suite <= 2, "unknown hash suite");
     R0_REQUIRE(seal || seal_len == 0, "seal is NULL");
-    uint32_t po2 = verify_seal(*c, suite, seal, seal_len, check_validity != 0);
+    R0_REQUIRE(code_roots || n_code_roots == 0, "code_roots is NULL");
+    uint32_t po2 = verify_seal(*c, suite, seal, seal_len, check_validity, code_roots, n_code_roots, code_root_out);
     if (po2_out) *po2_out = po2;
     return nullptr;
   } catch (const std::exception& e) {
@@ -108,6 +122,17 @@ extern "C" const char* r0hip_verify_seal(const char* circuit, int suite, const u
   } catch (...) {
     return strdup("r0hip: unknown error");
   }
+}
+
+extern "C" const char* r0hip_verify_seal(const char* circuit, int suite, const uint32_t* seal, size_t seal_len,
+                                         const uint32_t* h_code_roots, size_t n_code_roots,
+                                         uint32_t* h_code_root_out, uint32_t* po2_out) {
+  return verify_entry(circuit, suite, seal, seal_len, true, h_code_roots, n_code_roots, h_code_root_out, po2_out);
+}
+
+extern "C" const char* r0hip_testing_verify_seal_structure(const char* circuit, int suite, const uint32_t* seal,
+                                                           size_t seal_len, uint32_t* po2_out) {
+  return verify_entry(circuit, suite, seal, seal_len, false, nullptr, 0, nullptr, po2_out);
 }
 
 extern "C" const char* r0hip_poly_ext(const char* circuit, const uint32_t* h_mix, const uint32_t* h_global,

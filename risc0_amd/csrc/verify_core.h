@@ -51,6 +51,10 @@ Digest hash_pair(int suite, const Digest& a, const Digest& b) {
   uint32_t both[16];  // poseidon2: the unpadded hash of a || b (poseidon2/mod.rs:247-255)
   memcpy(both, a.w, 32);
   memcpy(both + 8, b.w, 32);
+  // the reference asserts every word is reduced (poseidon2/mod.rs:47-59): a seal whose
+  // digests carry words >= p is rejected there, so it is rejected here
+  for (uint32_t w : both)
+    if (w >= kP) throw VerifyError("non-canonical Poseidon2 digest word in seal");
   return p2_hash_words(both, 16);
 }
 
@@ -65,6 +69,14 @@ struct ReadIOP {
     if (n > size - pos) throw VerifyError("seal too short");
     const uint32_t* p = words + pos;
     pos += n;
+    return p;
+  }
+  // read_field_elem_slice (read_iop.rs:45-48): field words must be canonical (< p), as the
+  // reference's checked cast of the seal words into BabyBearElem enforces
+  const uint32_t* read_elems(size_t n) {
+    const uint32_t* p = read(n);
+    for (size_t i = 0; i < n; i++)
+      if (p[i] >= kP) throw VerifyError("non-canonical field element in seal");
     return p;
   }
   void commit(const Digest& d) { rng->mix(d); }
@@ -97,7 +109,7 @@ struct MerkleVerifier {
   // opens row `idx`: the column values, checked against the committed tree
   const uint32_t* verify(ReadIOP& iop, size_t idx) const {
     if (idx >= rows) throw VerifyError("merkle query out of range");
-    const uint32_t* out = iop.read(cols);
+    const uint32_t* out = iop.read_elems(cols);
     Digest cur = hash_elems(iop.suite, out, cols);
     idx += rows;
     while (idx >= 2 * top_size) {
@@ -157,7 +169,7 @@ void fri_verify(ReadIOP& iop, size_t degree, Inner inner) {
     domain = d;
     degree /= FRI_FOLD;
   }
-  const uint32_t* final_words = iop.read(4 * degree);
+  const uint32_t* final_words = iop.read_elems(4 * degree);
   iop.commit(hash_elems(iop.suite, final_words, 4 * degree));
   std::vector<FpExt> final_poly(degree);
   for (size_t i = 0; i < degree; i++)
@@ -206,7 +218,7 @@ void verify_validity_and_fri(ReadIOP& iop, const TapView& t, uint32_t po2, const
   const FpExt z = iop.rng->random_ext_elem();
   const uint32_t back_one = fp_encode(kRouRev[po2]);
   const size_t nt = t.n_taps;
-  const uint32_t* coeff_words = iop.read((nt + CHECK_SIZE) * 4);
+  const uint32_t* coeff_words = iop.read_elems((nt + CHECK_SIZE) * 4);
   iop.commit(hash_elems(iop.suite, coeff_words, (nt + CHECK_SIZE) * 4));
   std::vector<FpExt> coeff_u(nt + CHECK_SIZE);
   for (size_t i = 0; i < coeff_u.size(); i++) coeff_u[i] = load_ext(coeff_words + 4 * i);

@@ -56,7 +56,8 @@ def _declare(L):
         "r0hip_fill_uniform": [vp, sz, C.c_uint64],
         "r0hip_rv32im_accum_finalize": [vp, sz, sz, sz],
         "r0hip_prove_segments": [C.c_char_p, C.c_int, C.c_uint32, C.c_int, C.c_uint32, C.c_void_p, sz, C.c_uint32],
-        "r0hip_verify_seal": [C.c_char_p, C.c_int, u32p, sz, C.c_int, C.POINTER(C.c_uint32)],
+        "r0hip_verify_seal": [C.c_char_p, C.c_int, u32p, sz, u32p, sz, u32p, C.POINTER(C.c_uint32)],
+        "r0hip_testing_verify_seal_structure": [C.c_char_p, C.c_int, u32p, sz, C.POINTER(C.c_uint32)],
         "r0hip_poly_ext": [C.c_char_p, u32p, u32p, u32p, u32p, u32p],
         "r0hip_synchronize": [],
         "r0hip_batch_expand_into_evaluate_ntt": [vp, vp, sz, C.c_uint32, C.c_uint32],
@@ -368,15 +369,28 @@ def prove_segments(hal, circuit, po2, witnesses, version=None, in_flight=2, seal
     return [(seal[: j.seal_len].copy(), mix) for j, seal, mix in zip(jobs, seals, mixes)]
 
 
-def verify_seal(circuit, suite, seal, check_validity=True):
+def verify_seal(circuit, suite, seal, check_validity=True, code_roots=None, return_code_root=False):
     """r0hip_verify_seal: the native seal verifier (host-only, no GPU); returns the
-    segment po2, raises R0HipError naming the failed check. check_validity=False skips the
-    constraint equation, for seals of synthetic witnesses."""
+    segment po2 (and the code root, 8 words, with return_code_root), raises R0HipError
+    naming the failed check. code_roots: allowed code/control roots (check_code,
+    zkp/src/verify/mod.rs:531). check_validity=False calls the test-only
+    r0hip_testing_verify_seal_structure instead (no constraint equation, no code-root check),
+    for seals of synthetic witnesses."""
     seal = np.ascontiguousarray(seal, dtype=np.uint32)
     po2 = C.c_uint32(0)
-    check(lib().r0hip_verify_seal(circuit.encode(), SUITES[suite] if isinstance(suite, str) else suite,
-                                  seal.ctypes.data_as(u32p), seal.size, int(bool(check_validity)), C.byref(po2)))
-    return po2.value
+    sid = SUITES[suite] if isinstance(suite, str) else suite
+    if not check_validity:
+        assert code_roots is None and not return_code_root, "the structure check binds no code root"
+        check(lib().r0hip_testing_verify_seal_structure(circuit.encode(), sid, seal.ctypes.data_as(u32p), seal.size,
+                                                        C.byref(po2)))
+        return po2.value
+    roots = np.ascontiguousarray(np.zeros(0, np.uint32) if code_roots is None else code_roots, dtype=np.uint32)
+    assert roots.size % 8 == 0
+    root_out = np.zeros(8, np.uint32)
+    check(lib().r0hip_verify_seal(circuit.encode(), sid, seal.ctypes.data_as(u32p), seal.size,
+                                  roots.ctypes.data_as(u32p), roots.size // 8, root_out.ctypes.data_as(u32p),
+                                  C.byref(po2)))
+    return (po2.value, root_out) if return_code_root else po2.value
 
 
 def poly_ext(circuit, mix, glob, eval_u, poly_mix):

@@ -462,6 +462,53 @@ def device_witness(h, n, seed):
     return b
 
 
+def ec_sample_cycles(po2, rng, n_random=4096):
+    """Cycles for the full-size eval_check checks: the domain's ends, the back-wrap
+    region (taps reach back 4*68 points), every cycle & 3 coset, 256-point launch-block
+    edges, the 2^k boundaries, and random points."""
+    D = 4 << po2
+    s = set(range(8)) | set(range(D - 8, D)) | set(range(4 * 68 - 4, 4 * 68 + 8))
+    s |= set(range(D - 4 * 68 - 4, D - 4 * 68 + 4))
+    for k in range(8, po2 + 2):
+        s |= {(1 << k) - 1, 1 << k, (1 << k) + 1}
+    for b in rng.integers(1, D // 256, 64):
+        s |= {int(b) * 256 - 1, int(b) * 256}
+    s |= {int(x) for x in rng.integers(0, D, n_random)}
+    return np.array(sorted(x for x in s if 0 <= x < D), np.uint64)
+
+
+@pytest.mark.parametrize("circuit,po2", [("rv32im", 20), ("rv32im", 24), ("recursion", 18)])
+def test_eval_check_full_size(hal, oracle, circuit, po2):
+    """eval_check at the BASELINE sizes (configs[1] po2=20, configs[2] po2=24, configs[4]
+    recursion po2=18) equals the reference's compiled poly_fp x inv((3x)^N - 1)
+    (rv32im/src/prove/hal/cpu.rs:145-207) word for word at >= 4096 sampled cycles. The
+    evaluated groups are drawn on the device; the checker recomputes any tap from its
+    index (oracle.eval_check_sampled)."""
+    import risc0_amd as r
+    if oracle.ref_lib() is None:
+        pytest.skip("oracle/_ref not built")
+    d = oracle.load_circuit_json(circuit)
+    D = 4 << po2
+    gs = d["group_sizes"]
+    seeds = [0x45430000 + 16 * po2 + g for g in range(3)]
+    rng = np.random.default_rng(0x4543 + po2)
+    bufs = [device_witness(hal, gs[g] * D, seeds[g]) for g in range(3)]
+    mix = oracle.rand_elems(rng, d["mix_size"])
+    glob = oracle.rand_elems(rng, d["output_size"])
+    pm = oracle.rand_elems(rng, 4)
+    out = hal.alloc_elem("check", 4 * D)
+    hal.eval_check(circuit, out, bufs, dev(hal, mix), dev(hal, glob), pm, po2)
+    for b in bufs:
+        b.free()
+    got = out.to_numpy().reshape(4, D)
+    out.free()
+    cycles = ec_sample_cycles(po2, rng)
+    assert cycles.size >= 4096
+    ref = oracle.eval_check_sampled(circuit, seeds, mix, glob, pm, po2, cycles)
+    bad = np.nonzero((got[:, cycles.astype(np.int64)].T != ref).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} of {cycles.size} cycles differ, first at {cycles[bad[:8]]}"
+
+
 @pytest.mark.parametrize("circuit,suite,po2", [("rv32im", "poseidon2", 20), ("rv32im", "poseidon2", 16),
                                                ("recursion", "sha-256", 18), ("recursion", "poseidon_254", 18),
                                                ("rv32im", "poseidon2", 24)])

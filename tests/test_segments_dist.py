@@ -1,36 +1,17 @@
-"""World-size-2 gloo run of the segment-per-GPU harness (risc0_amd/segments.py) on
-the CPU: sharding covers every segment exactly once, ranks never exchange segment
-data, and the reported time is the max over ranks."""
+"""World-size-2 CPU rehearsal of the segment-per-GPU path (risc0_amd/segments.py, SURVEY.md
+§8e): the local launcher (what `bench.py --gpus N` uses without torch.distributed.run)
+starts 2 gloo ranks; each proves its round-robin share of the golden seal cases with the
+CPU oracle; rank 0 gathers the seal digests host-side and they equal the golden fixtures
+(tests/golden/index.json), with the reported time the max over ranks."""
+import json
 import os
-import socket
+import sys
 
 import pytest
-import torch.multiprocessing as mp
 
-from risc0_amd.segments import segments_for_rank, timed_segments
+from risc0_amd.segments import launch_local, rank_env, segments_for_rank
 
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-def _worker(rank, world, port, n_segments, q):
-    import time
-
-    import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    done = []
-    # rank 1 is made slower so the max-over-ranks is observable
-    segs = segments_for_rank(rank, world, n_segments)
-    t, tmax = timed_segments(lambda s: (done.append(s), time.sleep(0.02 * (1 + rank))), segs, warmup=1,
-                             sync=lambda: None, dist=dist)
-    q.put((rank, segs, done[1:], t, tmax))
-    dist.destroy_process_group()
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def test_round_robin_covers_all_segments():
@@ -39,21 +20,24 @@ def test_round_robin_covers_all_segments():
         assert got == list(range(64))
 
 
-@pytest.mark.timeout(120)
-def test_two_rank_gloo_timing_is_max_over_ranks():
-    world, n = 2, 6
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
-    for p in ps:
-        p.start()
-    res = sorted(q.get(timeout=100) for _ in range(world))
-    for p in ps:
-        p.join(30)
-        assert p.exitcode == 0
-    assert sorted(s for r in res for s in r[2]) == list(range(n))
-    ts = [r[3] for r in res]
-    for r in res:
-        assert abs(r[4] - max(ts)) < 1e-9
-    assert res[1][3] > res[0][3]
+def test_rank_env_matches_torchrun():
+    e = rank_env(3, 8, 29500, base={})
+    assert (e["RANK"], e["LOCAL_RANK"], e["WORLD_SIZE"], e["MASTER_ADDR"], e["MASTER_PORT"]) == \
+        ("3", "3", "8", "127.0.0.1", "29500")
+
+
+@pytest.mark.timeout(300)
+def test_two_ranks_prove_golden_segments(oracle, tmp_path):
+    if oracle.ref_lib() is None:
+        pytest.skip("oracle/_ref not built")
+    import test_golden as G
+    out = tmp_path / "dist.json"
+    rc = launch_local(2, [sys.executable, os.path.join(HERE, "dist_worker.py"), str(out)], timeout=280)
+    assert rc == 0
+    res = json.loads(out.read_text())
+    cases = G.INDEX["seals"]
+    assert res["world"] == 2
+    assert {int(k) for k in res["digests"]} == set(range(len(cases)))
+    for k, d in res["digests"].items():
+        assert d == cases[int(k)]["seal_sha256"], f"segment {k} seal differs from its golden digest"
+    assert abs(res["tmax"] - max(res["t_by_rank"].values())) < 1e-9

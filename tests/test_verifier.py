@@ -134,3 +134,34 @@ def test_native_verifier_rejects_garbage(oracle):
     for cut in rng.integers(1, seal.size, 20):
         with pytest.raises(r.R0HipError, match="seal too short"):
             r.verify_seal("recursion", 0, seal[:cut], check_validity=False)
+
+
+def test_native_verifier_binds_code_root_and_canonical_words(oracle):
+    """check_code (zkp/src/verify/mod.rs:531): the code root comes back and an allow-list
+    is enforced; field words >= p are rejected as read_field_elem_slice's checked cast
+    rejects them (read_iop.rs:45-48), even though they are congruent to valid words."""
+    import risc0_amd as r
+    _native_lib_or_skip(oracle)
+    po2, s = 8, 0
+    d = oracle.load_circuit_json("recursion")
+    n, gs = 1 << po2, d["group_sizes"]
+    code, data, accum = (np.zeros(gs[g] * n, np.uint32) for g in (1, 2, 0))
+    glob = oracle.rand_elems(np.random.default_rng(6), d["output_size"])
+    seal, _mix, _ = oracle.prove_segment("recursion", s, po2, code, data, accum, glob, version=None)
+    got, root = r.verify_seal("recursion", s, seal, return_code_root=True)
+    assert got == po2 and root.any()
+    other = root.copy()
+    other[0] ^= 1
+    assert r.verify_seal("recursion", s, seal, code_roots=np.concatenate([other, root])) == po2
+    with pytest.raises(r.R0HipError, match="code root"):
+        r.verify_seal("recursion", s, seal, code_roots=other)
+    bad = seal.copy()
+    bad[0] += np.uint32(oracle.P)  # a header global, congruent to the original
+    with pytest.raises(r.R0HipError, match="non-canonical"):
+        r.verify_seal("recursion", s, bad, check_validity=False)
+    rng = np.random.default_rng(7)
+    for where in rng.choice(np.nonzero(seal < np.uint32(2**32 - oracle.P))[0], 60, replace=False):
+        bad = seal.copy()
+        bad[where] += np.uint32(oracle.P)
+        with pytest.raises(r.R0HipError):
+            r.verify_seal("recursion", s, bad, check_validity=False)

@@ -772,7 +772,14 @@ def emit(circuit, outdir, budget, host=False):
                 Mv[i] = PM
                 continue
             if op == "l" and not SADDR:
-                w(f"  const uint32_t v{i} = A.a[{ins[2]}][{ins[3]}u * A.domain + ((cycle - {4 * ins[4]}u) & mask)];")
+                # column base in 64-bit scalar arithmetic (211 columns x 2^26 points exceed
+                # 2^32 words at po2=24) + one 32-bit byte offset per `back`, so each load is
+                # a saddr-form global_load with no per-load VALU address arithmetic
+                back = ins[4]
+                if back not in offs:
+                    offs.add(back)
+                    w(f"  const uint32_t o{back} = ((cycle - {4 * back}u) & mask) * 4u;")
+                w(f"  const uint32_t v{i} = ldc(A.a[{ins[2]}] + uint64_t({ins[3]}u) * A.domain, o{back});")
                 Mv[i] = PM
                 continue
             if op == "l":

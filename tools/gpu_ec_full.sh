@@ -1,0 +1,15 @@
+#!/bin/bash
+# Full-size eval_check parity (rv32im po2 20/24, recursion po2 18) first, then the whole
+# GPU suite, smoke() and one default bench line.
+TAG=${1:-ecfull}
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/$TAG; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread \
+  -k test_eval_check_full_size > $O/ec_full.log 2>&1 || { tail -30 $O/ec_full.log; exit 1; }
+grep -E "PASSED|FAILED" $O/ec_full.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+cat $O/bench.json
