@@ -38,7 +38,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=6,
                     help="segments of the end-to-end (pinned host witness -> H2D -> seal) leg; 0 = skip")
-    ap.add_argument("--cpu-po2", type=int, default=16, help="segment size of the bounded CPU baseline sample")
+    ap.add_argument("--cpu-po2", type=int, default=None,
+                    help="segment size of the CPU baseline proof (default: the bench's own po2, at most 20)")
     ap.add_argument("--inflight", type=int, default=None,
                     help="segments in flight per GPU (host threads, each with its own HIP stream); "
                          "default 6 up to po2=18, 2 up to po2=22, 1 above (one po2=24 segment needs ~150 GB)")
@@ -180,17 +181,24 @@ def main():
         dist.destroy_process_group()
 
 
-# Measured on MI355X with tools/micro/modmul_bench.hip: a dependent chain of canonical
-# Montgomery multiplies (v_mad_u64_u32, v_mul_lo_u32, v_mad_u64_u32, v_add, v_min) runs
-# at 7.78e12 modmul/s over the chip — the integer-VALU roof the hash, eval_check and
-# evaluate_any kernels are quoted against.
-MODMUL_PEAK = 7.78e12
 HBM_PEAK_GBS = 8000.0
+# Chip VALU issue roof in wave64 instructions/s: 256 CUs x 4 SIMDs, one wave64 instruction
+# per 4 cycles per SIMD at 2.4 GHz. That is the measured issue cost of the 32-bit integer
+# VOP3 ops these kernels are made of (v_mad_u64_u32, v_mul_lo_u32, v_min_u32, v_lshl_add_u64:
+# 29-34 T lane-instructions/s in profiles/r1_valu_rates.txt) and the unit SQ_ACTIVE_INST_VALU
+# counts in (ACTIVE_INST_VALU x 4 = SQ_INSTS_VALU exactly, profiles/r2a_pmc_valu.json).
+VALU_PEAK_GIPS = 256 * 4 * 2.4e9 / 4 / 1e9
+# The binding resource of each launcher family: the hash, eval_check and
+# evaluate_any kernels are integer-VALU-issue bound; the NTT/eltwise ones move bytes.
+VALU_BOUND = {"eval_check", "hash_rows", "merkle_fold", "batch_evaluate_any"}
 
 
 def kernel_roofline(r, hal, args, circ, dc, dd, da, dg, version):
     """Time every kernel family of one proof with HIP events on the library stream
-    (r0hip_kernel_times) and quote the dominant one against HBM and the VALU roof."""
+    (r0hip_kernel_times) and quote the dominant one against the resource that binds it:
+    VALU instruction issue (SQ_INSTS_VALU per launch from the committed PMC pass of this
+    bench, over the measured launch time) for the integer-arithmetic kernels, HBM otherwise;
+    the HBM view is always reported beside it."""
     # the main thread has its own stream/pool: warm it first so no first-use
     # allocation lands inside a timed launcher
     r.prove_segment(hal, args.circuit, args.po2, dc, dd, da, dg, version=version)
@@ -200,56 +208,65 @@ def kernel_roofline(r, hal, args, circ, dc, dd, da, dg, version):
     r.set_kernel_timing(False)
     if not times:
         return None
-    name, (ms, calls, alg_bytes, alg_mm) = max(times.items(), key=lambda kv: kv[1][0])
+    name, (ms, calls, alg_bytes, _alg_mm) = max(times.items(), key=lambda kv: kv[1][0])
     print(json.dumps({"kernel_times_ms": {k: [round(v[0], 3), v[1]] for k, v in times.items()}}), file=sys.stderr)
     avg_s = ms / 1000.0 / calls
     per_launch = alg_bytes / calls
-    achieved = per_launch / avg_s / 1e9
-    traffic, src = pmc_traffic(name, calls, args)
-    out = {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "alg_bytes_per_launch": int(per_launch),
-           "avg_launch_ms": round(avg_s * 1000, 4)}
-    if src:
-        out["traffic_source"] = src
-    if alg_mm:
-        mm = alg_mm / calls / avg_s
-        out["valu"] = {"achieved": round(mm / 1e12, 3), "peak": MODMUL_PEAK / 1e12, "unit": "T modmul-equiv/s",
-                       "frac": round(mm / MODMUL_PEAK, 4), "modmuls_per_launch": int(alg_mm / calls),
-                       "note": "field multiplications of the restated algorithm per second against a canonical "
-                               "Montgomery multiply's rate; lazy reductions make one cost less, so frac can exceed 1"}
-        busy, src = pmc_valu_busy(name, args)
-        if busy is not None:
-            out["valu"]["issue_busy_frac"] = busy
-            out["valu"]["issue_source"] = src
+    gbs = per_launch / avg_s / 1e9
+    hbm = {"achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    traffic, tsrc = pmc_traffic(name, calls, args)
+    fam = name.split("_poseidon2")[0].split("_sha")[0]
+    insts, busy, vsrc = pmc_valu(fam, args)
+    if fam in VALU_BOUND and insts:
+        gips = insts / avg_s / 1e9
+        out = {"kernel": name, "bound": "valu", "achieved": round(gips, 1), "peak": VALU_PEAK_GIPS,
+               "unit": "G VALU instructions/s (wave64)", "frac": round(gips / VALU_PEAK_GIPS, 4),
+               "valu_insts_per_launch": int(insts), "issue_busy_frac": busy, "valu_source": vsrc,
+               "note": "integer modular arithmetic bound by VALU issue: executed VALU instructions per launch "
+                       "(PMC SQ_INSTS_VALU) over the launch time, against 1024 SIMDs x one wave64 instruction "
+                       "per 4 cycles at 2.4 GHz; VOP2 v_add/v_sub (about a quarter of eval_check's) can issue "
+                       "faster, so frac is an upper bound. issue_busy_frac is the same count over the SIMD "
+                       "cycles at the measured clock (SQ_ACTIVE_INST_VALU)"}
+    else:
+        out = {"kernel": name, "bound": "hbm", **hbm}
+    out.update({"traffic": traffic, "alg_bytes_per_launch": int(per_launch), "avg_launch_ms": round(avg_s * 1000, 4)})
+    if out["bound"] != "hbm":
+        out["hbm"] = hbm
+    if tsrc:
+        out["traffic_source"] = tsrc
     return out
 
 
-def pmc_valu_busy(family, args):
-    """Time-weighted share of cycles the SIMDs issue VALU instructions in `family`'s kernels,
-    from the newest committed SQ_ACTIVE_INST_VALU summary (profiles/r*_pmc_valu.txt, made by
-    tools/pmc_summary.py from a rocprofv3 --pmc pass of this bench)."""
+def pmc_valu(family, args):
+    """VALU instructions per launch of `family` and the time-weighted share of SIMD cycles
+    issuing VALU, from the newest committed rocprofv3 --pmc summary of this bench
+    (profiles/r*_pmc_valu.json, tools/pmc_summary.py). PMC counters cannot be read inside
+    the timed process, so these are the committed measurement, labelled by file."""
     import glob
     if args.circuit != "rv32im" or args.po2 != 20 or args.hashfn != "poseidon2":
-        return None, None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_valu.txt")))
+        return None, None, None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_valu.json")))
     if not files:
-        return None, None
+        return None, None, None
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from rocprof_families import family as fam_of
-    tot = busy = 0.0
-    for line in open(files[-1]).read().splitlines()[1:]:
-        f = line.split()
-        try:
-            ms, pct = float(f[-6]), float(f[-3])
-        except (ValueError, IndexError):
+    with open(files[-1]) as f:
+        ks = json.load(f)["kernels"]
+    insts = tot = busy = 0.0
+    for k, d in ks.items():
+        if fam_of(k) != family or not d["dispatches"]:
             continue
-        name = " ".join(f[:-6])
-        if fam_of(name) == family.split("_poseidon2")[0]:
-            tot += ms
-            busy += ms * min(pct, 100.0) / 100.0
+        # per launcher call: every kernel of the family runs once per call (eval_check: the
+        # 30 generated kernels), so average each kernel over its own dispatches
+        insts += d["insts_valu"] / d["dispatches"] if family == "eval_check" else d["insts_valu"]
+        util = d["active_inst_valu"] * 4 / (256 * 4 * d["gui_active_cycles"]) if d["gui_active_cycles"] else 0
+        tot += d["ms"]
+        busy += d["ms"] * min(util, 1.0)
+    if family != "eval_check":
+        insts = None  # launches per proof differ per kernel: only eval_check is quoted per launch
     if tot == 0:
-        return None, None
-    return round(busy / tot, 3), os.path.relpath(files[-1], ROOT)
+        return None, None, None
+    return insts, round(busy / tot, 3), os.path.relpath(files[-1], ROOT)
 
 
 def end_to_end(r, hal, args, witness, k, version):
@@ -304,25 +321,55 @@ def pmc_traffic(family, calls, args):
     return int((d["read_bytes"] + d["write_bytes"]) / calls), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(args, circ):
-    """The CPU oracle (C++ restatement of CpuHal + Prover) on a bounded sample."""
+def host_cores():
+    """CPUs this process may use on the box: the affinity mask, capped by the cgroup CPU
+    quota (cgroup v2 cpu.max or v1 cfs_quota/period) when one is set."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
     try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota:
+        n = min(n, max(1, int(quota)))
+    return n
+
+
+def cpu_baseline(args, circ):
+    """The CPU oracle (C++ restatement of CpuHal + Prover, eval_check through the
+    reference's compiled poly_fp) proving one segment of the bench's own config, with the
+    per-Hal-op breakdown, on every host core the process may use."""
+    try:
+        cores = host_cores()
+        os.environ["ORACLE_THREADS"] = str(cores)  # read once, at the oracle's first parallel op
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
         if oracle.ref_lib() is None:
             return None
-        po2 = args.cpu_po2
+        po2 = args.cpu_po2 if args.cpu_po2 is not None else min(args.po2, 20)  # po2=24 would take ~30 min
         rng = np.random.default_rng(0x5249534330)
         code, data, accum, glob = synthetic_witness(rng, circ, po2)
         suite = {"poseidon2": oracle.POSEIDON2, "sha-256": oracle.SHA256, "poseidon_254": oracle.POSEIDON254}[args.hashfn]
+        oracle.op_times(reset=True)
         t0 = time.perf_counter()
         oracle.prove_segment(args.circuit, suite, po2, code, data, accum, glob,
                              version=2 if args.circuit == "rv32im" else None)
         t = time.perf_counter() - t0
+        ops = {k: round(v[0], 3) for k, v in sorted(oracle.op_times().items(), key=lambda kv: -kv[1][0])}
+        ops["other (transcript, openings, host polys)"] = round(t - sum(ops.values()), 3)
         return {"value": round((1 << po2) / t, 1), "unit": "cycles/s", "cores": int(oracle.num_threads()),
                 "kind": "port",
-                "sample": f"one {args.circuit} segment at po2={po2} ({args.hashfn}), {t:.1f} s; "
-                          "eval_check uses the reference's compiled C++ poly_fp"}
+                "sample": f"one {args.circuit} segment at po2={po2} ({args.hashfn}), {t:.1f} s wall; "
+                          "eval_check uses the reference's compiled C++ poly_fp",
+                "seconds_by_hal_op": ops}
     except Exception as e:  # the baseline is reported, never required
         print(f"cpu baseline failed: {e}", file=sys.stderr)
         return None

@@ -183,6 +183,14 @@ const char* r0hip_kernel_times(char* buf, size_t cap);
 /* per-phase device timings (ms) of the last r0hip_prove_segment, as "name=ms;..." */
 const char* r0hip_last_profile(char* buf, size_t cap);
 
+/* Device-memory accounting, replacing the reference HAL's MemoryTracker
+ * (risc0/zkp/src/hal/mod.rs:292-317, reported as the datasheet's `ram`,
+ * risc0/zkvm/examples/datasheet.rs:251). out[5] = {live bytes (buffers handed out),
+ * peak live bytes, reserved bytes (held from hipMalloc incl. the free pool), peak
+ * reserved bytes, number of hipMalloc calls}. Peaks are since the last reset. Host-only. */
+const char* r0hip_mem_stats(uint64_t* out);
+const char* r0hip_mem_reset_peak(void);
+
 #ifdef __cplusplus
 }
 #endif

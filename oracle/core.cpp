@@ -25,9 +25,10 @@ size_t num_threads() {
   static size_t n = [] {
     const char* s = getenv("ORACLE_THREADS");
     if (s && atoi(s) > 0) return (size_t)atoi(s);
+    // every hardware thread unless the caller says otherwise (bench.py passes the CPUs the
+    // process may use: its affinity mask, capped by the cgroup CPU quota)
     size_t hc = std::thread::hardware_concurrency();
-    if (hc == 0) hc = 1;
-    return std::min<size_t>(hc, 16);  // the GPU box grants 16 host cores
+    return hc ? hc : size_t(1);
   }();
   return n;
 }

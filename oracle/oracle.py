@@ -337,3 +337,20 @@ def prove_segment(name, suite, po2, code, data, accum, glob, version=None):
 
 def num_threads():
     return lib().oracle_num_threads()
+
+
+def op_times(reset=True):
+    """{hal_op: (seconds, calls)} of the oracle proofs since the last reset (the CPU
+    baseline's per-op breakdown)."""
+    f = lib().oracle_op_times
+    f.restype = C.c_size_t
+    f.argtypes = [C.c_char_p, C.c_size_t, C.c_int]
+    buf = C.create_string_buffer(f(None, 0, 0) + 1)
+    f(buf, len(buf), int(reset))
+    out = {}
+    for item in buf.value.decode().split(";"):
+        if item:
+            k, v = item.split("=")
+            t, n = v.split(":")
+            out[k] = (float(t), int(n))
+    return out

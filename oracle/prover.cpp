@@ -9,7 +9,10 @@
 //   risc0/zkp/src/core/poly.rs:23-89
 //   risc0/circuit/rv32im/src/prove/hal/mod.rs:143-224 (segment header / group order)
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -39,6 +42,26 @@ long oracle_combos_divide(uint32_t*, size_t, const uint32_t*, const uint32_t*, s
 }
 
 namespace {
+
+// Wall time per Hal op of the proofs run so far (the CPU baseline's per-op breakdown,
+// BASELINE.md §2). Keys follow the reference Hal method names.
+std::mutex g_op_mu;
+std::map<std::string, std::pair<double, long>> g_op_time;
+struct OpTime {
+  const char* name;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  explicit OpTime(const char* n) : name(n) {}
+  ~OpTime() {
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    std::lock_guard<std::mutex> lk(g_op_mu);
+    auto& e = g_op_time[name];
+    e.first += s;
+    e.second += 1;
+  }
+};
+#define OP_CAT2(a, b) a##b
+#define OP_CAT(a, b) OP_CAT2(a, b)
+#define OP_TIME(n) OpTime OP_CAT(op_time_, __LINE__)(n)
 
 constexpr size_t INV_RATE = 4, QUERIES = 50, FRI_FOLD = 16, FRI_MIN_DEGREE = 256, EXT = 4,
                  CHECK_SIZE = INV_RATE * EXT;
@@ -101,7 +124,11 @@ struct MerkleTreeProver {
   Digest root;
   MerkleTreeProver(int suite, const Buf& m, size_t rows, size_t cols, size_t queries)
       : params(rows, cols, queries), matrix(&m), nodes(rows * 2 * 8, 0) {
-    oracle_hash_rows(suite, nodes.data() + rows * 8, rows, m.data(), rows * cols);
+    {
+      OP_TIME("hash_rows");
+      oracle_hash_rows(suite, nodes.data() + rows * 8, rows, m.data(), rows * cols);
+    }
+    OP_TIME("hash_fold");
     for (size_t i = params.layers; i-- > 0;) {
       size_t layer = size_t(1) << i;
       oracle_hash_fold(suite, nodes.data(), layer * 2, layer);
@@ -134,9 +161,15 @@ struct PolyGroup {
   PolyGroup(int suite, Buf c, size_t cnt, size_t size) : coeffs(std::move(c)), count(cnt) {
     size_t domain = size * INV_RATE;
     evaluated.assign(count * domain, 0);
-    oracle_batch_expand_into_evaluate_ntt(evaluated.data(), evaluated.size(), coeffs.data(),
-                                          coeffs.size(), count, log2_ceil(INV_RATE));
-    oracle_batch_bit_reverse(coeffs.data(), coeffs.size(), count);
+    {
+      OP_TIME("batch_expand_into_evaluate_ntt");
+      oracle_batch_expand_into_evaluate_ntt(evaluated.data(), evaluated.size(), coeffs.data(),
+                                            coeffs.size(), count, log2_ceil(INV_RATE));
+    }
+    {
+      OP_TIME("batch_bit_reverse");
+      oracle_batch_bit_reverse(coeffs.data(), coeffs.size(), count);
+    }
     merkle.reset(new MerkleTreeProver(suite, evaluated, domain, count, QUERIES));
   }
 };
@@ -306,8 +339,14 @@ struct Prover {
   void commit_group(size_t g, const uint32_t* witness) {
     size_t gs = taps.group_size(g);
     Buf coeffs(witness, witness + gs * cycles);
-    oracle_batch_interpolate_ntt(coeffs.data(), coeffs.size(), gs);
-    oracle_zk_shift(coeffs.data(), coeffs.size(), gs);
+    {
+      OP_TIME("batch_interpolate_ntt");
+      oracle_batch_interpolate_ntt(coeffs.data(), coeffs.size(), gs);
+    }
+    {
+      OP_TIME("zk_shift");
+      oracle_zk_shift(coeffs.data(), coeffs.size(), gs);
+    }
     groups[g].reset(new PolyGroup(suite, std::move(coeffs), gs, cycles));
     groups[g]->merkle->commit(iop);
   }
@@ -319,8 +358,14 @@ struct Prover {
     Buf check(EXT * domain, 0);
     std::vector<const uint32_t*> gptrs;
     for (auto& g : groups) gptrs.push_back(g->evaluated.data());
-    eval_check(c, check.data(), gptrs.data(), mix, global, poly_mix, (uint32_t)po2);
-    oracle_batch_interpolate_ntt(check.data(), check.size(), EXT);
+    {
+      OP_TIME("eval_check");
+      eval_check(c, check.data(), gptrs.data(), mix, global, poly_mix, (uint32_t)po2);
+    }
+    {
+      OP_TIME("batch_interpolate_ntt");
+      oracle_batch_interpolate_ntt(check.data(), check.size(), EXT);
+    }
     PolyGroup check_group(suite, std::move(check), CHECK_SIZE, cycles);
     check_group.merkle->commit(iop);
 
@@ -337,6 +382,7 @@ struct Prover {
         all_xs.push_back(x);
       }
       std::vector<ExtElem> out(which.size());
+      OP_TIME("batch_evaluate_any");
       oracle_batch_evaluate_any(groups[id]->coeffs.data(), groups[id]->coeffs.size(),
                                 groups[id]->count, which.data(), &xs[0].e[0].v, &out[0].e[0].v,
                                 which.size());
@@ -356,6 +402,7 @@ struct Prover {
       std::vector<uint32_t> which(CHECK_SIZE);
       for (size_t i = 0; i < CHECK_SIZE; i++) which[i] = (uint32_t)i;
       std::vector<ExtElem> xs(CHECK_SIZE, z_pow), out(CHECK_SIZE);
+      OP_TIME("batch_evaluate_any");
       oracle_batch_evaluate_any(check_group.coeffs.data(), check_group.coeffs.size(), CHECK_SIZE,
                                 which.data(), &xs[0].e[0].v, &out[0].e[0].v, CHECK_SIZE);
       coeff_u.insert(coeff_u.end(), out.begin(), out.end());
@@ -366,6 +413,7 @@ struct Prover {
     size_t combo_count = c->combos_count;
     Buf combos(cycles * (combo_count + 1) * 4, 0);
     {
+      OP_TIME("mix_poly_coeffs");
       ExtElem cur_mix = ExtElem::one();
       for (size_t id = 0; id < groups.size(); id++) {
         size_t gs = taps.group_size(id);
@@ -394,6 +442,7 @@ struct Prover {
       });
       uint32_t mm[4];
       mix_fri.store(mm);
+      OP_TIME("combos_prepare+combos_divide");
       oracle_combos_prepare(combos.data(), &coeff_u[0].e[0].v, combo_count, cycles, reg_sizes.data(),
                             reg_combo_ids.data(), reg_sizes.size(), mm);
       std::vector<ExtElem> pows;
@@ -409,8 +458,14 @@ struct Prover {
       if (bad >= 0) throw std::runtime_error("combos_divide: nonzero remainder in chunk " + std::to_string(bad));
     }
     Buf final_poly(cycles * EXT, 0);
-    oracle_eltwise_sum_extelem(final_poly.data(), final_poly.size(), combos.data(), combos.size() / 4);
-    oracle_batch_bit_reverse(final_poly.data(), final_poly.size(), EXT);
+    {
+      OP_TIME("eltwise_sum_extelem");
+      oracle_eltwise_sum_extelem(final_poly.data(), final_poly.size(), combos.data(), combos.size() / 4);
+    }
+    {
+      OP_TIME("batch_bit_reverse");
+      oracle_batch_bit_reverse(final_poly.data(), final_poly.size(), EXT);
+    }
     fri_prove(final_poly, check_group);
   }
 
@@ -431,14 +486,18 @@ struct Prover {
       size_t size = coeffs->size() / EXT;
       r->domain = size * INV_RATE;
       r->evaluated.assign(r->domain * EXT, 0);
-      oracle_batch_expand_into_evaluate_ntt(r->evaluated.data(), r->evaluated.size(), coeffs->data(),
-                                            coeffs->size(), EXT, log2_ceil(INV_RATE));
+      {
+        OP_TIME("batch_expand_into_evaluate_ntt");
+        oracle_batch_expand_into_evaluate_ntt(r->evaluated.data(), r->evaluated.size(), coeffs->data(),
+                                              coeffs->size(), EXT, log2_ceil(INV_RATE));
+      }
       r->merkle.reset(new MerkleTreeProver(suite, r->evaluated, r->domain / FRI_FOLD, FRI_FOLD * EXT, QUERIES));
       r->merkle->commit(iop);
       ExtElem fold_mix = iop.rng->random_ext_elem();
       r->coeffs.assign(size / FRI_FOLD * EXT, 0);
       uint32_t fm[4];
       fold_mix.store(fm);
+      OP_TIME("fri_fold");
       oracle_fri_fold(r->coeffs.data(), r->coeffs.size(), coeffs->data(), fm);
       rounds.push_back(std::move(r));
       coeffs = &rounds.back()->coeffs;
@@ -461,6 +520,21 @@ struct Prover {
 };
 
 }  // namespace
+
+// "name=seconds:calls;..." for every Hal op timed since the last reset (reset = nonzero)
+extern "C" size_t oracle_op_times(char* buf, size_t cap, int reset) {
+  std::lock_guard<std::mutex> lk(g_op_mu);
+  std::string s;
+  for (auto& kv : g_op_time)
+    s += kv.first + "=" + std::to_string(kv.second.first) + ":" + std::to_string(kv.second.second) + ";";
+  if (reset) g_op_time.clear();
+  if (buf && cap) {
+    const size_t n = std::min(cap - 1, s.size());
+    memcpy(buf, s.data(), n);
+    buf[n] = 0;
+  }
+  return s.size();
+}
 
 extern "C" const char* oracle_eval_check(const oracle_circuit_t* c, uint32_t* check,
                                          const uint32_t** groups, const uint32_t* mix,

@@ -42,6 +42,16 @@ const char* wrap(F f) {
   }
   return nullptr;
 }
+// host-only entry points: no stream, no device
+template <typename F>
+const char* wrap_nosync(F f) {
+  try {
+    f();
+  } catch (const std::exception& e) {
+    return strdup(e.what());
+  }
+  return nullptr;
+}
 uint32_t lg(size_t n, const char* what) {
   uint32_t r = 0;
   while ((size_t(1) << r) < n) r++;
@@ -314,6 +324,24 @@ const char* r0hip_last_profile(char* buf, size_t cap) {
       buf[cap - 1] = 0;
     }
   });
+}
+
+// MemoryTracker (zkp/src/hal/mod.rs:292-317): out[0..5) = live bytes, peak live bytes,
+// reserved bytes, peak reserved bytes, hipMalloc calls so far. Host-only, never fails.
+const char* r0hip_mem_stats(uint64_t* out) {
+  return wrap_nosync([&] {
+    R0_REQUIRE(out != nullptr, "r0hip_mem_stats: null output");
+    const MemStats m = mem_stats();
+    out[0] = m.live;
+    out[1] = m.peak_live;
+    out[2] = m.reserved;
+    out[3] = m.peak_reserved;
+    out[4] = m.mallocs;
+  });
+}
+
+const char* r0hip_mem_reset_peak(void) {
+  return wrap_nosync([&] { mem_reset_peak(); });
 }
 
 }  // extern "C"

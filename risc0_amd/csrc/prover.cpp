@@ -100,7 +100,10 @@ struct MerkleTree {
     }
     top_size = size_t(1) << top_layer;
     nodes = DevBuf(rows * 2 * 8);
-    merkle_tree(stream(), suite, nodes.p, m, rows, cols);
+    {
+      Span sp("commit");  // prove/merkle.rs:85
+      merkle_tree(stream(), suite, nodes.p, m, rows, cols);
+    }
     // root (node 1) .. end of the top layer in one copy
     std::vector<uint32_t> h((2 * top_size - 1) * 8);
     d2h(h.data(), nodes.p + 8, h.size() * 4);
@@ -243,6 +246,7 @@ void run_eval_check(const CircuitDef& c, uint32_t* check, const uint32_t* const*
   }
   double bytes = 16.0 * domain;
   for (int g = 0; g < 3; g++) bytes += 4.0 * domain * c.group_sizes[g];
+  Span span("eval_check");
   KScope ks("eval_check", bytes, double(domain) * info.modmuls_per_point);
   c.eval_check(s, e);
 }
@@ -261,15 +265,20 @@ struct Prover {
 
   // prover.rs:38-48 + 81-108; zk_shift fused into the interpolation's last pass
   void commit_group(size_t g, const uint32_t* witness) {
+    Span span("commit_group");
     size_t gs = c.group_size(g);
     DevBuf coeffs(gs * cycles);
-    ntt_interpolate_from(stream(), coeffs.p, witness, gs, uint32_t(po2), true);
+    {
+      Span sp("make_coeffs");
+      ntt_interpolate_from(stream(), coeffs.p, witness, gs, uint32_t(po2), true);
+    }
     groups[g].reset(new PolyGroup(suite, std::move(coeffs), gs, po2));
     groups[g]->tree.commit(iop);
   }
 
   // prover.rs:111-393
   void finalize(const uint32_t* mix, const uint32_t* global) {
+    Span span("finalize");
     hipStream_t s = stream();
     FpExt poly_mix = iop.rng->random_ext_elem();
     size_t domain = cycles * INV_RATE;
@@ -285,6 +294,7 @@ struct Prover {
     FpExt z = iop.rng->random_ext_elem();
     FpExt back_one = fe_from_fp(fp_encode(kRouRev[po2]));
     std::vector<FpExt> all_xs, eval_u;
+    Span span_u("eval_u");
     {
       // one batched launch per group; a single host sync for all of them
       std::vector<std::vector<uint32_t>> whichs(3);
@@ -335,6 +345,7 @@ struct Prover {
     }
     if (prof) prof->mark("eval_u");
     FpExt mix_fri = iop.rng->random_ext_elem();
+    Span span_mix("mix_poly_coeffs");
 
     size_t combo_count = c.combos_count;
     DevBuf combos(cycles * (combo_count + 1) * 4);
@@ -355,6 +366,7 @@ struct Prover {
     }
     if (prof) prof->mark("mix");
     {
+      Span sp("divide");
       // combos_prepare (hal/mod.rs:202-234) as per-row deltas on the low coefficients
       size_t width = 1;
       c.regs(0, c.n_taps, [&](size_t cur) { width = std::max<size_t>(width, c.tap(cur).skip); });
@@ -392,6 +404,7 @@ struct Prover {
     }
     if (prof) prof->mark("divide");
     DevBuf final_poly(cycles * EXT);
+    Span span_sum("sum");
     eltwise_sum_extelem(s, final_poly.p, combos.p, cycles, combo_count + 1);
     bit_reverse(s, final_poly.p, EXT, uint32_t(po2));
     combos = DevBuf();
@@ -406,6 +419,7 @@ struct Prover {
 
   // fri.rs:86-126 with all query openings gathered in one device pass
   void fri_prove(DevBuf coeffs, const PolyGroup& check_group) {
+    Span span("fri_prove");
     hipStream_t s = stream();
     size_t size = coeffs.words / EXT;
     size_t orig_domain = size * INV_RATE;
@@ -501,6 +515,7 @@ std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2
                                     bool write_version, uint32_t version, std::vector<uint32_t>* mix_out) {
   R0_REQUIRE(suite >= 0 && suite <= 2, "unknown hash suite");
   R0_REQUIRE(po2 >= 2 && po2 <= 24, "po2 out of range");
+  Span span("prove_core");
   hipStream_t s = stream();
   stage_reset();
   Profile prof;

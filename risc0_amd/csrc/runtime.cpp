@@ -14,6 +14,10 @@
 #include <thread>
 #include <unordered_map>
 
+#include <atomic>
+
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "devmem.h"
 
 namespace r0 {
@@ -37,6 +41,8 @@ std::multimap<size_t, void*> g_orphans;
 std::thread::id g_main_thread;
 std::vector<hipStream_t> g_free_streams;  // streams of exited threads (drained)
 std::vector<Stage> g_free_stages;         // their pinned upload arenas
+// MemStats counters (see mem_stats)
+std::atomic<uint64_t> g_mem_live{0}, g_peak_live{0}, g_reserved{0}, g_peak_reserved{0}, g_mallocs{0};
 
 struct ThreadCtx {
   hipStream_t stream = nullptr;
@@ -53,7 +59,10 @@ struct ThreadCtx {
     std::lock_guard<std::mutex> lk(g_mu);
     for (auto& kv : pool) g_orphans.emplace(kv.first, kv.second);
     for (auto& kv : scratch)
-      if (kv.second.p) g_orphans.emplace(kv.second.bytes, kv.second.p);
+      if (kv.second.p) {
+        g_orphans.emplace(kv.second.bytes, kv.second.p);
+        g_mem_live.fetch_sub(kv.second.bytes, std::memory_order_relaxed);
+      }
     g_free_streams.push_back(stream);
     if (stage.base) g_free_stages.push_back(Stage{stage.base, stage.cap, 0});
     // superseded arenas in stage_old are left allocated (rare: only after growth)
@@ -62,7 +71,39 @@ struct ThreadCtx {
   }
 };
 thread_local ThreadCtx t_ctx;
+
+// ---- accounting (MemStats) ----
+void raise_peak(std::atomic<uint64_t>& peak, uint64_t v) {
+  uint64_t cur = peak.load(std::memory_order_relaxed);
+  while (v > cur && !peak.compare_exchange_weak(cur, v, std::memory_order_relaxed)) {
+  }
+}
+void live_add(uint64_t b) { raise_peak(g_peak_live, g_mem_live.fetch_add(b, std::memory_order_relaxed) + b); }
+void live_sub(uint64_t b) { g_mem_live.fetch_sub(b, std::memory_order_relaxed); }
+// every device allocation of the library goes through these two
+hipError_t counted_malloc(void** p, size_t bytes) {
+  const hipError_t e = hipMalloc(p, bytes);
+  if (e == hipSuccess) {
+    g_mallocs.fetch_add(1, std::memory_order_relaxed);
+    raise_peak(g_peak_reserved, g_reserved.fetch_add(bytes, std::memory_order_relaxed) + bytes);
+  }
+  return e;
+}
+void counted_free(void* p, size_t bytes) {
+  if (hipFree(p) == hipSuccess) g_reserved.fetch_sub(bytes, std::memory_order_relaxed);
+}
 }  // namespace
+
+MemStats mem_stats() {
+  return MemStats{g_mem_live.load(), g_peak_live.load(), g_reserved.load(), g_peak_reserved.load(), g_mallocs.load()};
+}
+void mem_reset_peak() {
+  g_peak_live.store(g_mem_live.load());
+  g_peak_reserved.store(g_reserved.load());
+}
+
+Span::Span(const char* name) { roctxRangePushA(name); }
+Span::~Span() { roctxRangePop(); }
 
 void ensure_init() {
   if (t_ctx.stream) return;
@@ -119,12 +160,12 @@ const uint32_t* dev_table(const std::string& key, const std::function<std::vecto
   }
   std::vector<uint32_t> host = gen();
   uint32_t* d = nullptr;
-  HIP_OK(hipMalloc(&d, host.size() * 4));
+  HIP_OK(counted_malloc(reinterpret_cast<void**>(&d), host.size() * 4));
   HIP_OK(hipMemcpy(d, host.data(), host.size() * 4, hipMemcpyHostToDevice));
   std::lock_guard<std::mutex> lk(g_mu);
   auto it = g_tables.find(key);
   if (it != g_tables.end()) {
-    (void)hipFree(d);
+    counted_free(d, host.size() * 4);
     return it->second;
   }
   g_tables[key] = d;
@@ -137,7 +178,8 @@ void* scratch(size_t bytes, int slot) {
   if (s.bytes < bytes) {
     if (s.p) {
       HIP_OK(hipStreamSynchronize(t_ctx.stream));  // last user of the old block must be done
-      HIP_OK(hipFree(s.p));
+      counted_free(s.p, s.bytes);
+      live_sub(s.bytes);
     }
     size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
     s.p = nullptr;
@@ -152,11 +194,12 @@ void* scratch(size_t bytes, int slot) {
         g_orphans.erase(ot);
       }
     }
-    if (!s.p && hipMalloc(&s.p, want) != hipSuccess) {
+    if (!s.p && counted_malloc(&s.p, want) != hipSuccess) {
       dev_trim();
-      HIP_OK(hipMalloc(&s.p, want));
+      HIP_OK(counted_malloc(&s.p, want));
     }
     s.bytes = want;
+    live_add(want);
   }
   return s.p;
 }
@@ -263,6 +306,7 @@ void* dev_alloc(size_t bytes) {
     if (it != t_ctx.pool.end()) {
       void* p = it->second;
       t_ctx.pool.erase(it);
+      live_add(bytes);
       std::lock_guard<std::mutex> lk(g_mu);
       g_live[p] = bytes;
       return p;
@@ -272,17 +316,19 @@ void* dev_alloc(size_t bytes) {
     if (ot != g_orphans.end() && ot->first <= bytes + bytes / 4) {
       void* p = ot->second;
       g_live[p] = ot->first;
+      live_add(ot->first);
       g_orphans.erase(ot);
       return p;
     }
   }
   void* p = nullptr;
-  hipError_t e = hipMalloc(&p, bytes);
+  hipError_t e = counted_malloc(&p, bytes);
   if (e != hipSuccess) {
     // release pooled blocks and retry once
     dev_trim();
-    HIP_OK(hipMalloc(&p, bytes));
+    HIP_OK(counted_malloc(&p, bytes));
   }
+  live_add(bytes);
   std::lock_guard<std::mutex> lk(g_mu);
   g_live[p] = bytes;
   return p;
@@ -298,15 +344,16 @@ void dev_free(void* p) {
     bytes = it->second;
     g_live.erase(it);
   }
+  live_sub(bytes);
   t_ctx.pool.emplace(bytes, p);  // reused only by this thread, i.e. on this stream
 }
 
 void dev_trim() {
   if (t_ctx.stream) HIP_OK(hipStreamSynchronize(t_ctx.stream));
-  for (auto& kv : t_ctx.pool) (void)hipFree(kv.second);
+  for (auto& kv : t_ctx.pool) counted_free(kv.second, kv.first);
   t_ctx.pool.clear();
   std::lock_guard<std::mutex> lk(g_mu);
-  for (auto& kv : g_orphans) (void)hipFree(kv.second);
+  for (auto& kv : g_orphans) counted_free(kv.second, kv.first);
   g_orphans.clear();
 }
 

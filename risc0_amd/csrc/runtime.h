@@ -60,6 +60,27 @@ struct KScope {
 void ktimer_enable(bool on);
 std::string ktimer_report();  // "name=total_ms:calls:alg_bytes:alg_modmuls;..." (synchronises)
 
+// Device-memory accounting, the reference HAL's MemoryTracker (zkp/src/hal/mod.rs:292-317):
+// `live` = bytes of the buffers handed out (pooled DevBufs and per-thread scratch), `reserved`
+// = bytes held from hipMalloc (live + free pool blocks + constant tables), their peaks since
+// the last reset, and the number of hipMalloc calls the library has made.
+struct MemStats {
+  uint64_t live, peak_live, reserved, peak_reserved, mallocs;
+};
+MemStats mem_stats();
+void mem_reset_peak();
+
+// A named host range for rocprofv3 --marker-trace (roctx), the reference's scope! spans
+// (core/src/perf.rs:40-72; prover.rs, fri.rs, merkle.rs use the same names). Like the
+// reference's, a range covers the host work of a phase: the device work it queues runs
+// asynchronously on the thread's stream and shows up in the kernel trace.
+struct Span {
+  explicit Span(const char* name);
+  ~Span();
+  Span(const Span&) = delete;
+  Span& operator=(const Span&) = delete;
+};
+
 // Workgroups for a 1-D launch of a lanes at b per workgroup. An AQL dispatch counts
 // work-items in 32 bits, so a grid of 2^32 or more lanes cannot launch; such sizes go
 // through grid_stride() instead.

@@ -86,6 +86,8 @@ def _declare(L):
         "r0hip_last_profile": [C.c_char_p, sz],
         "r0hip_set_kernel_timing": [C.c_int],
         "r0hip_kernel_times": [C.c_char_p, sz],
+        "r0hip_mem_stats": [C.POINTER(C.c_uint64)],
+        "r0hip_mem_reset_peak": [],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -431,3 +433,15 @@ def kernel_times():
             ms, calls, b, mm = v.split(":")
             out[k] = (float(ms), int(calls), float(b), float(mm))
     return out
+
+
+def mem_stats():
+    """The library's MemoryTracker (zkp/src/hal/mod.rs:292-317): live and reserved device
+    bytes, their peaks since mem_reset_peak(), and how many hipMalloc calls it has made."""
+    out = (C.c_uint64 * 5)()
+    check(lib().r0hip_mem_stats(out))
+    return dict(zip(("live", "peak_live", "reserved", "peak_reserved", "mallocs"), (int(x) for x in out)))
+
+
+def mem_reset_peak():
+    check(lib().r0hip_mem_reset_peak())

@@ -596,3 +596,40 @@ def test_abi_errors_are_reported_not_fatal(hal, oracle):
     ref = np.zeros(8 * 8, np.uint32)
     oracle.hash_rows(oracle.POSEIDON2, ref, h_ok.to_numpy())
     assert np.array_equal(out.to_numpy(), ref)
+
+
+def test_steady_state_proving_makes_no_hipmalloc(oracle):
+    """Locks in ae46b24: once a segment size has been proved, proofs on NEW host threads
+    (the bench and the pipeline start fresh ones) reuse the pooled blocks and scratch that
+    exited threads left: zero hipMalloc calls (r0hip_mem_stats, the MemoryTracker
+    equivalent), identical seals, and the peak live bytes reported."""
+    import threading
+
+    import risc0_amd as r
+    case = G.INDEX["seals"][0]
+    h = H(case["suite"])
+    code, data, accum, glob = G.seal_inputs(oracle, case["circuit"], case["po2"])
+    bufs = [dev(h, x) for x in (code, data, accum)]
+    globs = [dev(h, glob) for _ in range(2)]
+    version = 2 if case["circuit"] == "rv32im" else None
+    seals = {}
+
+    def batch(tag):
+        def run(i):
+            seals[(tag, i)] = r.prove_segment(h, case["circuit"], case["po2"], *bufs, globs[i], version=version)[0]
+        ts = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+
+    batch("warm")
+    r.mem_reset_peak()
+    before = r.mem_stats()
+    batch("steady")
+    after = r.mem_stats()
+    assert after["mallocs"] == before["mallocs"], (before, after)
+    assert after["peak_live"] > after["live"] >= 0
+    assert after["reserved"] >= after["peak_live"]
+    for i in range(2):
+        assert G.digest(seals[("steady", i)]) == case["seal_sha256"]

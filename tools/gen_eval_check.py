@@ -247,6 +247,10 @@ WAVES = int(os.environ.get("EC_WAVES", "2"))
 #                                                but more live registers -> spills in 6 kernels
 #   EC_SADDR=1 saddr tap loads                   28.9-30.0 ms: -1.1k VALU per big kernel, no gain
 #   EC_SPLIT=2 / 3 split accumulation chains     30.6 / 32.7 ms (register pressure)
+#   poly_mix powers staged in LDS per kernel (instead of scalar loads, which the compiler
+#   hoists and spills to VGPR lanes: ~640 v_writelane/v_readlane in k13)   not adopted:
+#   plain, volatile and sched_barrier-fenced LDS reads all compiled k13 to 256 VGPRs +
+#   256 AGPRs (1 wave/SIMD, AGPR spills) against 227 VGPRs at 2 waves with SGPR operands
 # The kernels are bound by register pressure and issue stalls (SQ_WAIT_INST_ANY 30-55% of
 # wave cycles), not by the count of VALU instructions.
 # EC_CANON=1: every Fp/FpExt result canonical; EC_CANON=0: the lazy range analysis below
@@ -382,6 +386,9 @@ def emit(circuit, outdir, budget, host=False):
         "  uint32_t base, count;  // this launch covers points [base, base + count)",
         "};",
         f"constexpr int NPM = {npm};",
+        "// one more than the largest tapped column index of any argument: 32-bit tap indices",
+        "// are exact while kTapCols * domain <= 2^32",
+        f"constexpr uint32_t kTapCols = {max(c for _, c in colslot) + 1 if colslot else 1}u;",
         "// lazy Fp/FpExt words: congruent mod p, below a generator-tracked bound (see",
         "// tools/gen_eval_check.py); lred/xred take one p off values >= p",
         "EC_FN uint32_t lmul(uint32_t a, uint32_t b) {",
@@ -392,6 +399,12 @@ def emit(circuit, outdir, budget, host=False):
         "// tap load: scalar column base + 32-bit byte offset (saddr-form global load)",
         "EC_FN uint32_t ldc(const uint32_t* p, uint32_t off) {",
         "  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(p) + off);",
+        "}",
+        "// trace tap: W = false indexes in 32 bits (col * domain + row < 2^32 words), W = true",
+        "// forms the column base in 64 bits (needed once columns x domain reach 2^32)",
+        "template <bool W> EC_FN uint32_t tap(const uint32_t* a, uint32_t col, uint32_t domain, uint32_t row) {",
+        "  if constexpr (W) return ldc(a + uint64_t(col) * domain, row * 4u);",
+        "  else return a[col * domain + row];",
         "}",
         "EC_FN uint32_t lred(uint32_t x) { return umin(x, x - kP); }",
         "EC_FN uint32_t lsub(uint32_t a, uint32_t b, uint32_t kp) { return a + (kp - b); }",
@@ -772,14 +785,11 @@ def emit(circuit, outdir, budget, host=False):
                 Mv[i] = PM
                 continue
             if op == "l" and not SADDR:
-                # column base in 64-bit scalar arithmetic (211 columns x 2^26 points exceed
-                # 2^32 words at po2=24) + one 32-bit byte offset per `back`, so each load is
-                # a saddr-form global_load with no per-load VALU address arithmetic
-                back = ins[4]
-                if back not in offs:
-                    offs.add(back)
-                    w(f"  const uint32_t o{back} = ((cycle - {4 * back}u) & mask) * 4u;")
-                w(f"  const uint32_t v{i} = ldc(A.a[{ins[2]}] + uint64_t({ins[3]}u) * A.domain, o{back});")
+                # tap<W>: 32-bit column index while columns x domain < 2^32 words (every
+                # po2 <= 22), 64-bit column base above (211 columns x 2^26 points at po2=24);
+                # each kernel is instantiated for both, the launcher picks by domain
+                g, col, back = ins[2], ins[3], ins[4]
+                w(f"  const uint32_t v{i} = tap<W>(A.a[{g}], {col}u, A.domain, (cycle - {4 * back}u) & mask);")
                 Mv[i] = PM
                 continue
             if op == "l":
@@ -880,6 +890,7 @@ def emit(circuit, outdir, budget, host=False):
              head]
         for ki, (L, _) in enumerate(bodies):
             T.append(f"static void k{ki}(const Args& A, uint32_t cycle) {{")
+            T.append("  constexpr bool W = true;")
             T.append("  const uint32_t mask = A.domain - 1;")
             T += L
             T.append("}")
@@ -911,14 +922,17 @@ def emit(circuit, outdir, budget, host=False):
     for ki, (L, kwaves) in enumerate(bodies):
         K = [head]
         lb = "256" if kwaves <= 1 else f"256, {kwaves}"
-        K.append(f"__global__ __launch_bounds__({lb}) void k{ki}(Args A) {{")
+        K.append(f"template <bool W> __global__ __launch_bounds__({lb}) void k{ki}(Args A) {{")
         K.append("  const uint32_t cycle = A.base + blockIdx.x * 256u + threadIdx.x;")
         K.append("  if (cycle >= A.base + A.count) return;")
         K.append("  const uint32_t mask = A.domain - 1;")
         K += L
         K.append("}")
         K.append(f"void launch_k{ki}(hipStream_t s, const Args& A) {{")
-        K.append(f"  hipLaunchKernelGGL(k{ki}, dim3(div_up(A.count, 256)), dim3(256), 0, s, A);")
+        K.append(f"  if (uint64_t(kTapCols) * A.domain > (uint64_t(1) << 32))")
+        K.append(f"    hipLaunchKernelGGL(k{ki}<true>, dim3(div_up(A.count, 256)), dim3(256), 0, s, A);")
+        K.append("  else")
+        K.append(f"    hipLaunchKernelGGL(k{ki}<false>, dim3(div_up(A.count, 256)), dim3(256), 0, s, A);")
         K.append("  HIP_OK(hipGetLastError());")
         K.append("}")
         K.append(f"}}  // namespace ec_{circuit}")

@@ -10,4 +10,4 @@ tail -1 $O/ec.log
 timeout -k 10 300 python -u bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python3 bench.py --no-cpu-baseline --e2e-steps 0 --inflight 1 > $O/bench_stats.json 2> $O/bench_stats.err || { tail -20 $O/bench_stats.err; exit 1; }
-python3 tools/rocprof_families.py $(find $O/stats -name '*kernel_stats.csv' | head -1) > $O/families.txt && cat $O/families.txt
+python3 tools/rocprof_families.py $(find $O/stats -name "*kernel_stats.csv") 9 > $O/families.txt && cat $O/families.txt

@@ -17,7 +17,7 @@ def short(n):
     return n.replace("r0::", "")[:60]
 
 
-def main(path):
+def main(path, json_out=None):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
     dur = collections.defaultdict(float)
@@ -38,10 +38,22 @@ def main(path):
         park = d.get("SQ_WAIT_ANY", 0) / wc if wc else 0
         rows.append((ms, k, len(disp[k]), clk, util, park, d.get("SQ_INSTS_VALU", 0) / max(d.get("SQ_WAVES", 1), 1)))
     rows.sort(reverse=True)
+    if json_out:
+        # per-kernel totals over the run, for bench.py's instruction roof (SQ_INSTS_VALU per
+        # launch) and issue-busy share
+        import json
+        out = {}
+        for k, d in agg.items():
+            gui = d.get("GRBM_GUI_ACTIVE", 0) / XCDS
+            out[k] = {"ms": dur[k], "dispatches": len(disp[k]), "insts_valu": d.get("SQ_INSTS_VALU", 0),
+                      "active_inst_valu": d.get("SQ_ACTIVE_INST_VALU", 0), "waves": d.get("SQ_WAVES", 0),
+                      "gui_active_cycles": gui}
+        with open(json_out, "w") as f:
+            json.dump({"source": path, "kernels": out}, f, indent=1, sort_keys=True)
     print(f"{'kernel':60s} {'ms':>8s} {'n':>4s} {'GHz':>5s} {'valu%':>6s} {'park%':>6s} {'valu/wave':>10s}")
     for ms, k, n, clk, util, park, ipw in rows:
         print(f"{k:60s} {ms:8.3f} {n:4d} {clk:5.2f} {100 * util:6.1f} {100 * park:6.1f} {ipw:10.0f}")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
