@@ -1,0 +1,291 @@
+// The circuit side of the HIP backend: one file per circuit crate, behind `feature = "hip"`.
+//   risc0/circuit/rv32im/src/prove/hal/hip.rs     (counterpart of prove/hal/cuda.rs)
+//   risc0/circuit/recursion/src/prove/hal/hip.rs  (counterpart of prove/hal/cuda.rs)
+// Both are shown here; split them at the marked line.
+//
+// eval_check runs on the device (r0hip_eval_check: the constraint program generated for
+// gfx950 from the circuit, tools/gen_eval_check.py). Witness generation and the per-cycle
+// accumulation step stay on the host CPU code of the circuit crates (the same C++ the CPU
+// HAL calls), and their results are uploaded once: a GPU stepExec/stepAccum is SURVEY.md
+// §8(f) rank 1 and is not part of libr0hip.
+//
+// Selection (one arm each):
+//   circuit/rv32im/src/prove/mod.rs:45-55       if #[cfg(feature = "hip")] { self::hal::hip::segment_prover() }
+//   circuit/recursion/src/prove/mod.rs:82-93    if #[cfg(feature = "hip")] { self::hal::hip::recursion_prover(hashfn) }
+//
+// NOT COMPILED IN THIS REPOSITORY (no Rust toolchain in the image).
+
+// ======================= risc0/circuit/rv32im/src/prove/hal/hip.rs =======================
+use std::{ffi::CString, rc::Rc};
+
+use anyhow::Result;
+use risc0_circuit_rv32im_sys::{
+    RawAccumBuffers, RawBuffer, RawExecBuffers, RawPreflightTrace, risc0_circuit_rv32im_cpu_accum,
+    risc0_circuit_rv32im_cpu_witgen,
+};
+use risc0_core::{field::ExtElem as _, scope};
+use risc0_sys::{ffi_wrap, hip::r0hip_eval_check};
+use risc0_zkp::hal::{
+    AccumPreflight, Buffer, CircuitHal,
+    hip::{BufferImpl as HipBuffer, HipHal, HipHash, HipHashPoseidon2},
+};
+
+use super::{
+    CircuitAccumulator, CircuitWitnessGenerator, MetaBuffer, PreflightTrace, SegmentProverImpl, StepMode,
+};
+use crate::{
+    prove::{GLOBAL_MIX, GLOBAL_OUT, SegmentProver},
+    zirgen::circuit::{ExtVal, REGISTER_GROUP_ACCUM, REGISTER_GROUP_CODE, REGISTER_GROUP_DATA, Val},
+};
+
+pub struct HipCircuitHal<HS: HipHash> {
+    _hal: Rc<HipHal<HS>>, // keeps the device bound while the circuit HAL lives
+}
+
+impl<HS: HipHash> HipCircuitHal<HS> {
+    pub fn new(_hal: Rc<HipHal<HS>>) -> Self {
+        Self { _hal }
+    }
+}
+
+/// Host image of a MetaBuffer: the C++ step code works on host memory, then the result goes
+/// back to the device buffer in one copy.
+struct HostRows {
+    vals: Vec<Val>,
+    rows: usize,
+    cols: usize,
+    checked: bool,
+}
+
+impl HostRows {
+    fn of<HS: HipHash>(m: &MetaBuffer<HipHal<HS>>) -> Self {
+        Self { vals: m.buf.to_vec(), rows: m.rows, cols: m.cols, checked: m.checked }
+    }
+
+    fn raw(&self) -> RawBuffer {
+        RawBuffer { buf: self.vals.as_ptr(), rows: self.rows, cols: self.cols, checked: self.checked }
+    }
+
+    fn store<HS: HipHash>(&self, m: &MetaBuffer<HipHal<HS>>) {
+        m.buf.view_mut(|dst| dst.copy_from_slice(&self.vals));
+    }
+}
+
+fn raw_preflight(p: &PreflightTrace) -> RawPreflightTrace {
+    RawPreflightTrace {
+        cycles: p.cycles.as_ptr(),
+        txns: p.txns.as_ptr(),
+        bigint_bytes: p.bigint_bytes.as_ptr(),
+        txns_len: p.txns.len() as u32,
+        bigint_bytes_len: p.bigint_bytes.len() as u32,
+        table_split_cycle: p.table_split_cycle,
+    }
+}
+
+impl<HS: HipHash> CircuitWitnessGenerator<HipHal<HS>> for HipCircuitHal<HS> {
+    fn generate_witness(
+        &self,
+        mode: StepMode,
+        preflight: &PreflightTrace,
+        global: &MetaBuffer<HipHal<HS>>,
+        data: &MetaBuffer<HipHal<HS>>,
+    ) -> Result<()> {
+        scope!("witgen");
+        let cycles = preflight.cycles.len();
+        assert_eq!(cycles, data.rows);
+        let (g, d) = (HostRows::of(global), HostRows::of(data));
+        let buffers = RawExecBuffers { global: g.raw(), data: d.raw() };
+        let pf = raw_preflight(preflight);
+        ffi_wrap(|| unsafe { risc0_circuit_rv32im_cpu_witgen(mode as u32, &buffers, &pf, cycles as u32) })?;
+        g.store(global);
+        d.store(data);
+        Ok(())
+    }
+}
+
+impl<HS: HipHash> CircuitAccumulator<HipHal<HS>> for HipCircuitHal<HS> {
+    fn step_accum(
+        &self,
+        preflight: &PreflightTrace,
+        data: &MetaBuffer<HipHal<HS>>,
+        accum: &MetaBuffer<HipHal<HS>>,
+        global: &MetaBuffer<HipHal<HS>>,
+        mix: &MetaBuffer<HipHal<HS>>,
+    ) -> Result<()> {
+        scope!("accumulate");
+        let cycles = preflight.cycles.len();
+        let (d, a, g, m) = (HostRows::of(data), HostRows::of(accum), HostRows::of(global), HostRows::of(mix));
+        let buffers = RawAccumBuffers { data: d.raw(), accum: a.raw(), global: g.raw(), mix: m.raw() };
+        let pf = raw_preflight(preflight);
+        // all three phases of ffi.cpp:262-368 on the host (phases 2-3 alone also exist on
+        // the device: r0hip_rv32im_accum_finalize)
+        ffi_wrap(|| unsafe { risc0_circuit_rv32im_cpu_accum(&buffers, &pf, cycles as u32) })?;
+        a.store(accum);
+        Ok(())
+    }
+}
+
+impl<HS: HipHash> CircuitHal<HipHal<HS>> for HipCircuitHal<HS> {
+    fn accumulate(
+        &self,
+        _preflight: &AccumPreflight,
+        _ctrl: &HipBuffer<Val>,
+        _io: &HipBuffer<Val>,
+        _data: &HipBuffer<Val>,
+        _mix: &HipBuffer<Val>,
+        _accum: &HipBuffer<Val>,
+        _steps: usize,
+    ) {
+        // rv32im accumulates through CircuitAccumulator::step_accum (as the CUDA HAL does)
+    }
+
+    fn eval_check(
+        &self,
+        check: &HipBuffer<Val>,
+        groups: &[&HipBuffer<Val>],
+        globals: &[&HipBuffer<Val>],
+        poly_mix: ExtVal,
+        po2: usize,
+        steps: usize,
+    ) {
+        scope!("eval_check");
+        assert_eq!(steps, 1 << po2);
+        // r0hip takes the groups in tap-group order (accum 0, code 1, data 2) and expands the
+        // poly_mix powers itself (zirgen/info.rs POLY_MIX_POWERS are compiled in)
+        let g = [
+            groups[REGISTER_GROUP_ACCUM].dev() as *const u32,
+            groups[REGISTER_GROUP_CODE].dev() as *const u32,
+            groups[REGISTER_GROUP_DATA].dev() as *const u32,
+        ];
+        let pm = poly_mix.to_u32_words();
+        let name = CString::new("rv32im").unwrap();
+        ffi_wrap(|| unsafe {
+            r0hip_eval_check(
+                name.as_ptr(),
+                check.dev(),
+                g.as_ptr(),
+                globals[GLOBAL_MIX].dev(),
+                globals[GLOBAL_OUT].dev(),
+                pm.as_ptr(),
+                po2 as u32,
+            )
+        })
+        .unwrap();
+    }
+}
+
+pub type HipCircuitHalPoseidon2 = HipCircuitHal<HipHashPoseidon2>;
+
+pub fn segment_prover() -> Result<Box<dyn SegmentProver>> {
+    let hal_factory = || {
+        let hal = Rc::new(HipHal::<HipHashPoseidon2>::new());
+        let circuit_hal = Rc::new(HipCircuitHalPoseidon2::new(hal.clone()));
+        (hal, circuit_hal)
+    };
+    Ok(Box::new(SegmentProverImpl::new(hal_factory)))
+}
+
+#[cfg(test)]
+mod tests {
+    // eval_check on the device against the CPU circuit HAL on the same random buffers, as
+    // prove/hal/cuda.rs tests do with EvalCheckParams (po2 = 4 .. 10, every cycle).
+    use std::rc::Rc;
+
+    use risc0_core::field::baby_bear::BabyBear;
+    use risc0_zkp::{
+        core::hash::sha::Sha256HashSuite,
+        hal::{Hal, cpu::CpuHal, hip::HipHalSha256},
+    };
+
+    use super::*;
+    use crate::prove::hal::{cpu::CpuCircuitHal, cuda::tests::EvalCheckParams};
+
+    #[test]
+    fn eval_check_matches_cpu() {
+        for po2 in [4, 8, 10] {
+            let p = EvalCheckParams::new(po2);
+            let cpu_hal: CpuHal<BabyBear> = CpuHal::new(Sha256HashSuite::new_suite());
+            let gpu_hal = Rc::new(HipHalSha256::new());
+            let check_cpu = {
+                let check = cpu_hal.alloc_elem("check", 4 * p.domain);
+                let bufs = [&p.accum, &p.code, &p.data].map(|v| cpu_hal.copy_from_elem("g", v));
+                let (mix, out) = (cpu_hal.copy_from_elem("mix", &p.mix), cpu_hal.copy_from_elem("out", &p.out));
+                CpuCircuitHal.eval_check(&check, &[&bufs[0], &bufs[1], &bufs[2]], &[&mix, &out], p.poly_mix, po2, p.steps);
+                check.to_vec()
+            };
+            let check_gpu = {
+                let check = gpu_hal.alloc_elem("check", 4 * p.domain);
+                let bufs = [&p.accum, &p.code, &p.data].map(|v| gpu_hal.copy_from_elem("g", v));
+                let (mix, out) = (gpu_hal.copy_from_elem("mix", &p.mix), gpu_hal.copy_from_elem("out", &p.out));
+                HipCircuitHal::new(gpu_hal.clone())
+                    .eval_check(&check, &[&bufs[0], &bufs[1], &bufs[2]], &[&mix, &out], p.poly_mix, po2, p.steps);
+                check.to_vec()
+            };
+            assert_eq!(check_cpu, check_gpu, "po2 = {po2}");
+        }
+    }
+}
+
+// ===================== risc0/circuit/recursion/src/prove/hal/hip.rs ======================
+// (separate file; its own imports)
+//
+// use risc0_circuit_recursion_sys::{RawAccumBuffers, RawExecBuffers, RawPreflightTrace,
+//     risc0_circuit_recursion_cpu_accum, risc0_circuit_recursion_cpu_witgen};
+// use risc0_zkp::hal::hip::{HipHal, HipHashPoseidon2, HipHashPoseidon254, HipHashSha256};
+// use super::{CircuitAccumulator, CircuitWitnessGenerator, RecursionProver, RecursionProverImpl};
+// use crate::{REGISTER_GROUP_ACCUM, REGISTER_GROUP_CTRL, REGISTER_GROUP_DATA, GLOBAL_MIX, GLOBAL_OUT};
+//
+// pub struct HipRecursionCircuitHal<HS: HipHash> { _hal: Rc<HipHal<HS>> }
+//
+// impl<HS: HipHash> CircuitWitnessGenerator<HipHal<HS>> for HipRecursionCircuitHal<HS> {
+//     fn generate_witness(&self, mode: StepMode, total_cycles: u32, preflight: &RawPreflightTrace,
+//                         ctrl: &BufferImpl<BabyBearElem>, data: &BufferImpl<BabyBearElem>,
+//                         global: &BufferImpl<BabyBearElem>) -> Result<()> {
+//         // host images of ctrl/data/global, the CPU witgen (recursion-sys ffi.cpp), then upload
+//         let (mut c, mut d, mut g) = (ctrl.to_vec(), data.to_vec(), global.to_vec());
+//         let buffers = RawExecBuffers { ctrl: c.as_ptr(), data: d.as_mut_ptr(), global: g.as_mut_ptr() };
+//         ffi_wrap(|| unsafe { risc0_circuit_recursion_cpu_witgen(mode, &buffers, preflight, total_cycles) })?;
+//         data.view_mut(|v| v.copy_from_slice(&d));
+//         global.view_mut(|v| v.copy_from_slice(&g));
+//         Ok(())
+//     }
+// }
+//
+// impl<HS: HipHash> CircuitAccumulator<HipHal<HS>> for HipRecursionCircuitHal<HS> {
+//     fn accumulate(&self, work_cycles: u32, total_cycles: u32, ctrl: &BufferImpl<BabyBearElem>,
+//                   global: &BufferImpl<BabyBearElem>, data: &BufferImpl<BabyBearElem>,
+//                   mix: &BufferImpl<BabyBearElem>, accum: &BufferImpl<BabyBearElem>) -> Result<()> {
+//         let (c, g, d, m, mut a) = (ctrl.to_vec(), global.to_vec(), data.to_vec(), mix.to_vec(), accum.to_vec());
+//         let buffers = RawAccumBuffers { ctrl: c.as_ptr(), global: g.as_ptr(), data: d.as_ptr(),
+//                                         mix: m.as_ptr(), accum: a.as_mut_ptr() };
+//         ffi_wrap(|| unsafe { risc0_circuit_recursion_cpu_accum(&buffers, work_cycles, total_cycles) })?;
+//         accum.view_mut(|v| v.copy_from_slice(&a));
+//         Ok(())
+//     }
+// }
+//
+// impl<HS: HipHash> CircuitHal<HipHal<HS>> for HipRecursionCircuitHal<HS> {
+//     fn eval_check(&self, check: &BufferImpl<BabyBearElem>, groups: &[&BufferImpl<BabyBearElem>],
+//                   globals: &[&BufferImpl<BabyBearElem>], poly_mix: BabyBearExtElem, po2: usize, _steps: usize) {
+//         let g = [groups[REGISTER_GROUP_ACCUM].dev() as *const u32, groups[REGISTER_GROUP_CTRL].dev() as *const u32,
+//                  groups[REGISTER_GROUP_DATA].dev() as *const u32];
+//         let pm = poly_mix.to_u32_words();
+//         ffi_wrap(|| unsafe { r0hip_eval_check(c"recursion".as_ptr(), check.dev(), g.as_ptr(),
+//             globals[GLOBAL_MIX].dev(), globals[GLOBAL_OUT].dev(), pm.as_ptr(), po2 as u32) }).unwrap();
+//     }
+//     fn accumulate(&self, /* AccumPreflight variant, unused by recursion like cuda.rs:174-185 */) { unimplemented!() }
+// }
+//
+// pub(crate) fn recursion_prover(hashfn: &str) -> Result<Box<dyn RecursionProver>> {
+//     macro_rules! with { ($hs:ty) => {{
+//         let hal = Rc::new(HipHal::<$hs>::new());
+//         let circuit_hal = Rc::new(HipRecursionCircuitHal { _hal: hal.clone() });
+//         Ok(Box::new(RecursionProverImpl::new(hal, circuit_hal)) as Box<dyn RecursionProver>)
+//     }}}
+//     match hashfn {
+//         "poseidon2" => with!(HipHashPoseidon2),
+//         "poseidon_254" => with!(HipHashPoseidon254),
+//         "sha-256" => with!(HipHashSha256),
+//         _ => anyhow::bail!("Unsupported hashfn: {hashfn}"),
+//     }
+// }

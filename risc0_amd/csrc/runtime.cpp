@@ -36,8 +36,11 @@ struct Stage {
   uint8_t* base = nullptr;
   size_t cap = 0, used = 0;
 };
-// blocks left by exited threads (their stream was drained), reusable by anyone
+// blocks left by exited threads (their stream was drained), reusable by anyone: pool
+// blocks by size, scratch blocks by (slot, size) — kept apart so a new thread's scratch
+// never takes the block its own dev_alloc of the same phase is about to need
 std::multimap<size_t, void*> g_orphans;
+std::map<int, std::multimap<size_t, void*>> g_scratch_orphans;
 std::thread::id g_main_thread;
 std::vector<hipStream_t> g_free_streams;  // streams of exited threads (drained)
 std::vector<Stage> g_free_stages;         // their pinned upload arenas
@@ -60,7 +63,7 @@ struct ThreadCtx {
     for (auto& kv : pool) g_orphans.emplace(kv.first, kv.second);
     for (auto& kv : scratch)
       if (kv.second.p) {
-        g_orphans.emplace(kv.second.bytes, kv.second.p);
+        g_scratch_orphans[kv.first].emplace(kv.second.bytes, kv.second.p);
         g_mem_live.fetch_sub(kv.second.bytes, std::memory_order_relaxed);
       }
     g_free_streams.push_back(stream);
@@ -187,11 +190,12 @@ void* scratch(size_t bytes, int slot) {
       // a block left by an exited thread (bench and pipeline threads come and go; each
       // new one would otherwise hipMalloc its eval_check scratch again, GBs at po2 >= 20)
       std::lock_guard<std::mutex> lk(g_mu);
-      auto ot = g_orphans.lower_bound(bytes);
-      if (ot != g_orphans.end() && ot->first <= 2 * want) {
+      auto& orph = g_scratch_orphans[slot];
+      auto ot = orph.lower_bound(bytes);
+      if (ot != orph.end()) {
         s.p = ot->second;
         want = ot->first;
-        g_orphans.erase(ot);
+        orph.erase(ot);
       }
     }
     if (!s.p && counted_malloc(&s.p, want) != hipSuccess) {
@@ -355,6 +359,9 @@ void dev_trim() {
   std::lock_guard<std::mutex> lk(g_mu);
   for (auto& kv : g_orphans) counted_free(kv.second, kv.first);
   g_orphans.clear();
+  for (auto& sl : g_scratch_orphans)
+    for (auto& kv : sl.second) counted_free(kv.second, kv.first);
+  g_scratch_orphans.clear();
 }
 
 }  // namespace r0

@@ -633,3 +633,22 @@ def test_steady_state_proving_makes_no_hipmalloc(oracle):
     assert after["reserved"] >= after["peak_live"]
     for i in range(2):
         assert G.digest(seals[("steady", i)]) == case["seal_sha256"]
+
+
+@pytest.mark.parametrize("idx", range(len(G.INDEX["seals"])))
+def test_per_op_abi_prover_matches_golden_seal(idx, oracle):
+    """The drop-in path at seal level: the reference Prover call sequence (prover.rs,
+    poly_group.rs, merkle.rs, fri.rs, restated in tests/hal_prover.py) drives ONLY the
+    per-op Hal symbols of include/r0hip.h (alloc/memcpy, NTTs, zk_shift, bit_reverse,
+    hash_rows/hash_fold, eval_check, batch_evaluate_any, mix_poly_coeffs,
+    combos_prepare/combos_divide, eltwise ops, fri_fold, gather_sample openings as with
+    has_unified_memory() = false) — what a Rust HipHal would call — and the seal equals
+    the golden digest for every (circuit, suite, po2) case, as r0hip_prove_segment's does."""
+    import hal_prover
+    case = G.INDEX["seals"][idx]
+    h = H(case["suite"])
+    code, data, accum, glob = G.seal_inputs(oracle, case["circuit"], case["po2"])
+    bufs = [dev(h, x) for x in (code, data, accum, glob)]
+    seal, mix = hal_prover.prove_segment(oracle, h, case["circuit"], case["po2"], *bufs)
+    assert [int(x) for x in mix] == case["mix"]
+    assert G.digest(seal) == case["seal_sha256"], case
