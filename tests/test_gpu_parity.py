@@ -45,7 +45,7 @@ def dev(hal, a):
     return hal.copy_from_elem("x", a)
 
 
-@pytest.mark.parametrize("count,log_n", [(224, 12), (3, 1), (5, 2), (7, 5), (1, 10), (2, 11), (4, 14), (1, 20)])
+@pytest.mark.parametrize("count,log_n", [(224, 14), (224, 12), (3, 1), (5, 2), (7, 5), (1, 10), (2, 11), (4, 14), (1, 20)])
 def test_batch_bit_reverse(hal, oracle, count, log_n):
     # hal/mod.rs:354-366 (224 x 2^14)
     a = rnd(oracle, 1, count << log_n)
@@ -55,7 +55,7 @@ def test_batch_bit_reverse(hal, oracle, count, log_n):
     assert np.array_equal(d.to_numpy(), a)
 
 
-@pytest.mark.parametrize("count,log_in", [(224, 12), (1, 1), (3, 2), (5, 8), (2, 10), (9, 11), (4, 16), (1, 20)])
+@pytest.mark.parametrize("count,log_in", [(224, 16), (224, 12), (1, 1), (3, 2), (5, 8), (2, 10), (9, 11), (4, 16), (1, 20)])
 def test_batch_expand_into_evaluate_ntt(hal, oracle, count, log_in):
     # hal/mod.rs:389-404 (224 x 2^16 -> 2^18)
     a = rnd(oracle, 2, count << log_in)
@@ -66,7 +66,7 @@ def test_batch_expand_into_evaluate_ntt(hal, oracle, count, log_in):
     assert np.array_equal(out.to_numpy(), ref)
 
 
-@pytest.mark.parametrize("count,log_n", [(224, 14), (1, 1), (3, 3), (2, 12), (3, 13), (1, 17), (2, 22)])
+@pytest.mark.parametrize("count,log_n", [(224, 18), (224, 14), (1, 1), (3, 3), (2, 12), (3, 13), (1, 17), (2, 22)])
 def test_batch_interpolate_ntt(hal, oracle, count, log_n):
     # hal/mod.rs:406-418 (224 x 2^18)
     a = rnd(oracle, 3, count << log_n)
@@ -100,13 +100,28 @@ def test_zk_shift(hal, oracle, poly_count, log_n):
     assert np.array_equal(d.to_numpy(), a)
 
 
-def test_batch_evaluate_any(hal, oracle):
-    # hal/mod.rs:368-387 (223 polys x 2^16, 865 evals); mixed `which` and xs here
+@pytest.mark.parametrize("poly_count,log_n,evals,kind", [
+    (223, 16, 865, "reference"),  # hal/mod.rs:368-387 exactly: which = 0, every x = z^4
+    (223, 16, 865, "mixed"),      # every polynomial, distinct points
+    (16, 20, 16, "check"),        # the prover's check evaluation (prover.rs:253-262): 16 x 2^20 at z^4
+    (223, 12, 865, "mixed"),
+    (3, 1, 5, "mixed"),           # shorter than one 64-coefficient lane chunk
+])
+def test_batch_evaluate_any(hal, oracle, poly_count, log_n, evals, kind):
+    # polynomials longer than one 16384-coefficient chunk (log_n >= 15) go through the
+    # multi-chunk Horner combine (eltwise.hip)
     rng = np.random.default_rng(6)
-    poly_count, log_n, evals = 223, 12, 865
     coeffs = oracle.rand_elems(rng, poly_count << log_n)
-    which = rng.integers(0, poly_count, evals).astype(np.uint32)
-    xs = oracle.rand_elems(rng, 4 * evals)
+    if kind == "mixed":
+        which = rng.integers(0, poly_count, evals).astype(np.uint32)
+        xs = oracle.rand_elems(rng, 4 * evals)
+    else:
+        which = (np.zeros(evals) if kind == "reference" else np.arange(evals)).astype(np.uint32)
+        z = oracle.rand_elems(rng, 4)
+        zp = z
+        for _ in range(3):
+            zp = oracle.ext_mul(zp, z)
+        xs = np.tile(zp, evals).astype(np.uint32)
     out = hal.alloc_extelem("out", evals)
     hal.batch_evaluate_any(dev(hal, coeffs), poly_count, dev(hal, which), hal.copy_from_extelem("xs", xs), out)
     ref = np.zeros(4 * evals, np.uint32)

@@ -265,6 +265,16 @@ SADDR = os.environ.get("EC_SADDR", "0") == "1"
 # sums, joined where the value is used, so consecutive products do not wait on each
 # other's v_mad_u64_u32 results
 SPLIT = int(os.environ.get("EC_SPLIT", "1"))
+# EC_PIN=1: each poly_mix read goes through pin(), an empty asm that makes the table
+# pointer depend on the running sum it is added to, so the scalar load of pm[k] cannot be
+# hoisted ahead of that sum (hoisted loads were spilled from SGPRs to VGPR lanes)
+# Measured (rv32im po2=20, sum of kernel means): pinned to the running sum itself 50.5 ms,
+# 4 accumulations back 40.7 ms (volatile asm) / 45.3 ms (plain asm), against 26.9 ms for the
+# hoisted-and-spilled default — the spills go away (k13: 302 -> 0) but the pinned scalar
+# loads cannot be scheduled around; not adopted.
+PIN = os.environ.get("EC_PIN", "0") == "1"
+# ... pinned to the running sum EC_PIND accumulations back, so the load has that long to land
+PIND = int(os.environ.get("EC_PIND", "4"))
 
 
 def kernel_config(circuit, budget):
@@ -457,6 +467,16 @@ def emit(circuit, outdir, budget, host=False):
         "  for (int i = 0; i < 4; i++) a.c[i] += b.c[i];",
         "  return a;",
         "}",
+        "// the table pointer, made to depend on `a` (no instruction): pm[k] is loaded after `a`",
+        "#ifdef R0_EC_HOST",
+        "EC_FN const uint32_t* pin(const uint32_t* p, const Acc&) { return p; }",
+        "#else",
+        "EC_FN const uint32_t* pin(const uint32_t* p, const Acc& a) {",
+        "  const uint32_t d = uint32_t(a.c[0]);",
+        "  asm(\"\" : \"+s\"(p) : \"v\"(d));",
+        "  return p;",
+        "}",
+        "#endif",
         "// a += t * pm[k]  (t in Fp)",
         "EC_FN Acc acc_fp(Acc a, uint32_t t, const uint32_t* pm, int k) {",
         "#pragma unroll",
@@ -517,6 +537,7 @@ def emit(circuit, outdir, budget, host=False):
         cval = {}    # Fp constants: Montgomery word
         red_memo = {}
         offs = set()
+        acc_hist = []  # Acc variables in emission order (anchors of pin())
         tmp = {"n": 0}
         L = []
         w = L.append
@@ -673,9 +694,14 @@ def emit(circuit, outdir, budget, host=False):
                     t = reduce1(t)
                 add = 4 * t[1] * PM
                 expr, bd = room(expr, bd, add)
+                if PIN and len(acc_hist) >= PIND:
+                    a_ = acc_hist[-PIND]
+                    return f"acc_ext({expr}, {t[0]}, pin(A.pm, {a_}), pin(A.pmn, {a_}), {k})", bd + add
                 return f"acc_ext({expr}, {t[0]}, A.pm, A.pmn, {k})", bd + add
             add = t[1] * PM
             expr, bd = room(expr, bd, add)
+            if PIN and len(acc_hist) >= PIND:
+                return f"acc_fp({expr}, {t[0]}, pin(A.pm, {acc_hist[-PIND]}), {k})", bd + add
             return f"acc_fp({expr}, {t[0]}, A.pm, {k})", bd + add
 
         def acc_to_ext(expr, bd, name):
@@ -767,6 +793,7 @@ def emit(circuit, outdir, budget, host=False):
                 k = f"NPM + {combo_index[pms]}"
             e2, sb = add_prod(f"s{sn}", sb, cur, k)
             w(f"  const Acc s{sn + 1} = {e2};")
+            acc_hist.append(f"s{sn + 1}")
             acc_state["n"], acc_state["b"] = sn + 1, sb
 
         if mine or last:
@@ -822,6 +849,7 @@ def emit(circuit, outdir, budget, host=False):
                     ps.append(("Acc{{0, 0, 0, 0}}", 0))
                 expr, bd = add_prod(ps[idx][0], ps[idx][1], t, k)
                 w(f"  const Acc a{i} = {expr};")
+                acc_hist.append(f"a{i}")
                 ps[idx] = (f"a{i}", bd)
                 parts[i], chainpos[i] = ps, pos
                 if i in canon:
