@@ -127,6 +127,18 @@ const char* r0hip_prove_segment(const char* circuit, int suite, uint32_t po2, co
  * group, column-major with `rows` rows (the per-cycle stepAccum phase stays the caller's). */
 const char* r0hip_rv32im_accum_finalize(uint32_t* d_accum, size_t rows, size_t cols, size_t last_cycle);
 
+/* ---- recursion witness side: the accumulation step (risc0_circuit_recursion_cuda_accum,
+ * recursion-sys/kernels/cuda/ffi.cu; CPU driver recursion-sys/kernels/cxx/ffi.cpp:160-217,
+ * called from circuit/recursion/src/prove/witgen.rs:162-170): for cycles [0, work_cycles) the
+ * per-cycle accumulator factors (step_compute_accum), their inclusive prefix product, and the
+ * accum-group registers (step_verify_accum) written into d_accum. Groups are column-major with
+ * total_cycles rows (a power of two); d_mix holds the mix values, d_global the globals. Cells
+ * no step writes are left as they were (the reference leaves them INVALID for the caller to
+ * zeroize, witgen.rs:172-175). */
+const char* r0hip_recursion_accum(const uint32_t* d_ctrl, const uint32_t* d_global, const uint32_t* d_data,
+                                  const uint32_t* d_mix, uint32_t* d_accum, size_t work_cycles,
+                                  size_t total_cycles);
+
 /* ---- segment pipeline (r0vm's per-GPU worker queue, r0vm/src/actors/worker.rs:75-76, over the
  * zkvm's per-segment prove loop, zkvm/src/host/server/prove/prover_impl.rs:84-94) ----
  * Proves njobs segments of one (circuit, suite, po2) from HOST witness buffers: an uploader

@@ -253,6 +253,14 @@ const char* r0hip_rv32im_accum_finalize(uint32_t* d_accum, size_t rows, size_t c
   // layout.cpp.inc:6993-6999): the first machine accumulator column
   return wrap([&] { rv32im_accum_finalize(stream(), d_accum, rows, cols, 23, last_cycle); });
 }
+const char* r0hip_recursion_accum(const uint32_t* d_ctrl, const uint32_t* d_global, const uint32_t* d_data,
+                                  const uint32_t* d_mix, uint32_t* d_accum, size_t work_cycles,
+                                  size_t total_cycles) {
+  return wrap([&] {
+    R0_REQUIRE(d_ctrl && d_global && d_data && d_mix && d_accum, "r0hip_recursion_accum: null argument");
+    recursion_accum(stream(), d_ctrl, d_global, d_data, d_mix, d_accum, work_cycles, total_cycles);
+  });
+}
 const char* r0hip_fill_uniform(uint32_t* d_out, size_t count, uint64_t seed) {
   return wrap([&] { fill_uniform(stream(), d_out, count, seed); });
 }

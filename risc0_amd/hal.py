@@ -55,6 +55,7 @@ def _declare(L):
         "r0hip_host_free": [vp],
         "r0hip_fill_uniform": [vp, sz, C.c_uint64],
         "r0hip_rv32im_accum_finalize": [vp, sz, sz, sz],
+        "r0hip_recursion_accum": [vp, vp, vp, vp, vp, sz, sz],
         "r0hip_prove_segments": [C.c_char_p, C.c_int, C.c_uint32, C.c_int, C.c_uint32, C.c_void_p, sz, C.c_uint32],
         "r0hip_verify_seal": [C.c_char_p, C.c_int, u32p, sz, u32p, sz, u32p, C.POINTER(C.c_uint32)],
         "r0hip_testing_verify_seal_structure": [C.c_char_p, C.c_int, u32p, sz, C.POINTER(C.c_uint32)],
@@ -292,6 +293,12 @@ class HipHal:
     def rv32im_accum_finalize(self, accum, rows, cols, last_cycle):
         """accumulation phases 2-3 of risc0_circuit_rv32im_cuda_accum (ffi.cu:480-509)"""
         check(lib().r0hip_rv32im_accum_finalize(accum.ptr, rows, cols, last_cycle))
+
+    def recursion_accum(self, ctrl, glob, data, mix, accum, work_cycles, total_cycles):
+        """CircuitAccumulator::accumulate of the recursion circuit (witgen.rs:162-170 ->
+        risc0_circuit_recursion_cuda_accum): compute, prefix product, verify"""
+        check(lib().r0hip_recursion_accum(ctrl.ptr, glob.ptr, data.ptr, mix.ptr, accum.ptr, work_cycles,
+                                          total_cycles))
 
     def prefix_products(self, io):
         check(lib().r0hip_prefix_products(io.ptr, io.size))

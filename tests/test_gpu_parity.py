@@ -667,3 +667,27 @@ def test_per_op_abi_prover_matches_golden_seal(idx, oracle):
     seal, mix = hal_prover.prove_segment(oracle, h, case["circuit"], case["po2"], *bufs)
     assert [int(x) for x in mix] == case["mix"]
     assert G.digest(seal) == case["seal_sha256"], case
+
+
+@pytest.mark.parametrize("po2,short", [(10, 0), (12, 7), (16, 0), (18, 0), (4, 3)])
+def test_recursion_accum_matches_reference(hal, oracle, po2, short):
+    """Recursion accumulation on the GPU (r0hip_recursion_accum: compute, prefix product,
+    verify; kernels generated from risc0_amd/circuits/recursion.accum.ir) against the
+    reference's own compiled risc0_circuit_recursion_cpu_accum (recursion-sys
+    kernels/cxx/ffi.cpp:208-217, oracle/_ref/libref_recursion.so) on the same synthetic rows:
+    every accum word identical, including the cells neither writes (INVALID); work cycles
+    below the total leave the ZK tail rows alone."""
+    import accum_ir as A
+    d = A.circuit()
+    gs = d["group_sizes"]
+    n = 1 << po2
+    rng = np.random.default_rng(100 + po2)
+    ctrl, glob, data, mix = A.synthetic(rng, oracle, po2, gs, d["output_size"], d["mix_size"])
+    acc0 = np.full(gs[0] * n, A.INVALID, np.uint32)
+    steps = n - short
+    ref = acc0.copy()
+    A.ref_accum(ctrl, glob, data, mix, ref, steps, n)
+    dacc = dev(hal, acc0)
+    hal.recursion_accum(dev(hal, ctrl), dev(hal, glob), dev(hal, data), dev(hal, mix), dacc, steps, n)
+    got = dacc.to_numpy()
+    assert np.array_equal(got, ref), int((got != ref).sum())

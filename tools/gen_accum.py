@@ -1,0 +1,240 @@
+#!/usr/bin/env python3
+"""Emit the gfx950 kernels of the recursion circuit's accumulation step from its block IR
+(risc0_amd/circuits/recursion.accum.ir, tools/gen_accum_ir.py):
+
+  compute : per cycle, the accumulator factor (recursion-sys step_compute_accum.cpp)
+  verify  : per cycle, the accum-group registers from the prefix product
+            (recursion-sys step_verify_accum.cpp)
+
+One lane per cycle, values are canonical Montgomery words in VGPRs, `if (x != 0)` blocks
+stay branches (the control columns are one-hot per cycle, so a wave takes a few arms).
+Each function is cut into kernels of at most LIMIT operations along its block structure:
+a piece re-evaluates the pure definitions it uses from enclosing blocks (loads, constants,
+arithmetic) and runs under the conjunction of its enclosing guards. Pieces run in program
+order, so every register write of a cycle lands in the order the reference makes it.
+
+  gen_accum.py OUTDIR [LIMIT]
+Writes OUTDIR/accum_k<i>.hip and OUTDIR/accum.hip (launchers of both functions).
+"""
+import os
+import sys
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+P = 15 * 2**27 + 1
+
+
+def load():
+    fns, cur = {}, None
+    for line in open(os.path.join(ROOT, "risc0_amd", "circuits", "recursion.accum.ir")):
+        if line.startswith("#") or not line.strip():
+            continue
+        t = line.split()
+        if t[0] == "fn":
+            cur = fns.setdefault(t[1], [])
+            continue
+        cur.append((t[0],) + tuple(int(x) for x in t[1:]))
+    return fns
+
+
+def tree(prog):
+    """statements -> nested [('s', ins) | ('if', cond, children)]"""
+    root, stack = [], []
+    cur = root
+    for ins in prog:
+        if ins[0] == "if":
+            node = ("if", ins[1], [])
+            cur.append(node)
+            stack.append(cur)
+            cur = node[2]
+        elif ins[0] == "end":
+            cur = stack.pop()
+        else:
+            cur.append(("s", ins))
+    assert not stack
+    return root
+
+
+def size(node):
+    return 1 if node[0] == "s" else 1 + sum(size(c) for c in node[2])
+
+
+def chunks(children, guards, limit, out):
+    cur, n = [], 0
+    for c in children:
+        s = size(c)
+        if c[0] == "if" and s > limit:
+            if cur:
+                out.append((guards, cur))
+                cur, n = [], 0
+            chunks(c[2], guards + [c[1]], limit, out)
+            continue
+        if cur and n + s > limit:
+            out.append((guards, cur))
+            cur, n = [], 0
+        cur.append(c)
+        n += s
+    if cur:
+        out.append((guards, cur))
+
+
+DEFS = {"c", "l", "g", "+", "-", "*", "n", "i", "ra"}
+
+
+def defined(ins):
+    if ins[0] == "ra":
+        return list(ins[1:5])
+    return [ins[1]] if ins[0] in DEFS else []
+
+
+def used(ins):
+    op = ins[0]
+    if op in "+-*":
+        return [ins[2], ins[3]]
+    if op in ("n", "i"):
+        return [ins[2]]
+    if op == "w":
+        return [ins[3]]
+    if op == "wa":
+        return list(ins[1:5])
+    return []
+
+
+def flat(nodes):
+    for n in nodes:
+        if n[0] == "s":
+            yield n[1]
+        else:
+            yield ("if", n[1])
+            yield from flat(n[2])
+            yield ("end",)
+
+
+def emit_fn(name, prog, limit, kbase):
+    defs = {}
+    order = {}
+    for pos, ins in enumerate(prog):
+        for d in defined(ins):
+            defs[d] = ins
+            order[id(ins)] = pos
+    out = []
+    chunks(tree(prog), [], limit, out)
+    kernels = []
+    for guards, nodes in out:
+        body = list(flat(nodes))
+        if not any(ins[0] in ("w", "wa") for ins in body):
+            continue  # nothing observable (definitions only; their users re-evaluate them)
+        have = set(d for ins in body if ins[0] in DEFS for d in defined(ins))
+        need = set(guards)
+        for ins in body:
+            if ins[0] == "if":
+                need.add(ins[1])
+            need.update(used(ins))
+        pre = {}
+        stack = [v for v in need if v not in have]
+        while stack:
+            v = stack.pop()
+            ins = defs[v]
+            if id(ins) in pre:
+                continue
+            pre[id(ins)] = ins
+            stack += [u for u in used(ins) if u not in have]
+        pre = sorted(pre.values(), key=lambda i: order[id(i)])
+        L = []
+        w = L.append
+        ind = "  "
+
+        def stmt(ins, ind):
+            op = ins[0]
+            if op == "c":
+                w(f"{ind}const uint32_t v{ins[1]} = {(ins[2] % P) * 2**32 % P}u;")
+            elif op == "l":
+                _, i, a, col, back = ins
+                w(f"{ind}const uint32_t v{i} = A.a[{a}][uint64_t({col}u) * A.cycles + ((cycle - {back}u) & mask)];")
+            elif op == "g":
+                w(f"{ind}const uint32_t v{ins[1]} = A.a[{ins[2]}][{ins[3]}];")
+            elif op in "+-*":
+                f = {"+": "fp_add", "-": "fp_sub", "*": "fp_mul"}[op]
+                w(f"{ind}const uint32_t v{ins[1]} = {f}(v{ins[2]}, v{ins[3]});")
+            elif op == "n":
+                w(f"{ind}const uint32_t v{ins[1]} = fp_neg(v{ins[2]});")
+            elif op == "i":
+                w(f"{ind}const uint32_t v{ins[1]} = fp_inv(v{ins[2]});")
+            elif op == "ra":
+                w(f"{ind}const uint4 r{ins[1]} = A.vals[cycle];")
+                for k, c in enumerate("xyzw"):
+                    w(f"{ind}const uint32_t v{ins[1 + k]} = r{ins[1]}.{c};")
+            elif op == "wa":
+                w(f"{ind}A.vals[cycle] = make_uint4(v{ins[1]}, v{ins[2]}, v{ins[3]}, v{ins[4]});")
+            elif op == "w":
+                _, a, col, i = ins
+                w(f"{ind}A.a[{a}][uint64_t({col}u) * A.cycles + cycle] = v{i};")
+            else:
+                raise ValueError(op)
+
+        for ins in pre:
+            stmt(ins, ind)
+        if guards:
+            w(f"  if ({' && '.join(f'v{g} != 0u' for g in guards)}) {{")
+            ind = "    "
+        depth = ind
+        for ins in body:
+            if ins[0] == "if":
+                w(f"{depth}if (v{ins[1]} != 0u) {{")
+                depth += "  "
+            elif ins[0] == "end":
+                depth = depth[:-2]
+                w(f"{depth}}}")
+            else:
+                stmt(ins, depth)
+        if guards:
+            w("  }")
+        kernels.append(L)
+    return kernels
+
+
+HEAD = """// GENERATED by tools/gen_accum.py from risc0_amd/circuits/recursion.accum.ir — do not edit.
+#include "accum_gen.h"
+namespace r0 {
+namespace rec_accum {
+"""
+
+
+def main():
+    outdir = sys.argv[1]
+    limit = int(sys.argv[2]) if len(sys.argv) > 2 else 1200
+    fns = load()
+    os.makedirs(outdir, exist_ok=True)
+    launch = {}
+    k = 0
+    for name in ("compute", "verify"):
+        launch[name] = []
+        for L in emit_fn(name, fns[name], limit, k):
+            src = [HEAD, f"__global__ __launch_bounds__(256) void k{k}(AccArgs A) {{",
+                   "  const uint32_t cycle = blockIdx.x * 256u + threadIdx.x;",
+                   "  if (cycle >= A.steps) return;",
+                   "  const uint32_t mask = A.cycles - 1;"]
+            src += L
+            src += ["}", f"void launch_k{k}(hipStream_t s, const AccArgs& A) {{",
+                    f"  hipLaunchKernelGGL(k{k}, dim3(div_up(A.steps, 256)), dim3(256), 0, s, A);",
+                    "  HIP_OK(hipGetLastError());", "}", "}  // namespace rec_accum", "}  // namespace r0"]
+            with open(os.path.join(outdir, f"accum_k{k}.hip"), "w") as f:
+                f.write("\n".join(src) + "\n")
+            launch[name].append(k)
+            k += 1
+    L = [HEAD]
+    for i in range(k):
+        L.append(f"void launch_k{i}(hipStream_t s, const AccArgs& A);")
+    L.append("}  // namespace rec_accum")
+    for name in ("compute", "verify"):
+        L.append(f"void recursion_accum_{name}(hipStream_t s, const rec_accum::AccArgs& A) {{")
+        for i in launch[name]:
+            L.append(f"  rec_accum::launch_k{i}(s, A);")
+        L.append("}")
+    L.append("}  // namespace r0")
+    with open(os.path.join(outdir, "accum.hip"), "w") as f:
+        f.write("\n".join(L) + "\n")
+    print(f"recursion accum: {len(launch['compute'])} compute + {len(launch['verify'])} verify kernels")
+
+
+if __name__ == "__main__":
+    main()
