@@ -4,10 +4,11 @@
 // Both are shown here; split them at the marked line.
 //
 // eval_check runs on the device (r0hip_eval_check: the constraint program generated for
-// gfx950 from the circuit, tools/gen_eval_check.py). Witness generation and the per-cycle
-// accumulation step stay on the host CPU code of the circuit crates (the same C++ the CPU
-// HAL calls), and their results are uploaded once: a GPU stepExec/stepAccum is SURVEY.md
-// §8(f) rank 1 and is not part of libr0hip.
+// gfx950 from the circuit, tools/gen_eval_check.py), and so does the recursion circuit's
+// accumulation (r0hip_recursion_accum). Witness generation of both circuits and the rv32im
+// per-cycle accumulation step stay on the host CPU code of the circuit crates (the same C++
+// the CPU HAL calls), and their results are uploaded once: a GPU stepExec/stepAccum for
+// rv32im is SURVEY.md §8(f) rank 1 and is not part of libr0hip.
 //
 // Selection (one arm each):
 //   circuit/rv32im/src/prove/mod.rs:45-55       if #[cfg(feature = "hip")] { self::hal::hip::segment_prover() }
@@ -252,15 +253,15 @@ mod tests {
 // }
 //
 // impl<HS: HipHash> CircuitAccumulator<HipHal<HS>> for HipRecursionCircuitHal<HS> {
+//     // on the device: compute, prefix product and verify of recursion-sys ffi.cpp:160-217
+//     // (r0hip_recursion_accum, generated from the reference step code)
 //     fn accumulate(&self, work_cycles: u32, total_cycles: u32, ctrl: &BufferImpl<BabyBearElem>,
 //                   global: &BufferImpl<BabyBearElem>, data: &BufferImpl<BabyBearElem>,
 //                   mix: &BufferImpl<BabyBearElem>, accum: &BufferImpl<BabyBearElem>) -> Result<()> {
-//         let (c, g, d, m, mut a) = (ctrl.to_vec(), global.to_vec(), data.to_vec(), mix.to_vec(), accum.to_vec());
-//         let buffers = RawAccumBuffers { ctrl: c.as_ptr(), global: g.as_ptr(), data: d.as_ptr(),
-//                                         mix: m.as_ptr(), accum: a.as_mut_ptr() };
-//         ffi_wrap(|| unsafe { risc0_circuit_recursion_cpu_accum(&buffers, work_cycles, total_cycles) })?;
-//         accum.view_mut(|v| v.copy_from_slice(&a));
-//         Ok(())
+//         ffi_wrap(|| unsafe {
+//             r0hip_recursion_accum(ctrl.dev(), global.dev(), data.dev(), mix.dev(), accum.dev(),
+//                                   work_cycles as usize, total_cycles as usize)
+//         })
 //     }
 // }
 //

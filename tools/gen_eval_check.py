@@ -271,7 +271,8 @@ SPLIT = int(os.environ.get("EC_SPLIT", "1"))
 # Measured (rv32im po2=20, sum of kernel means): pinned to the running sum itself 50.5 ms,
 # 4 accumulations back 40.7 ms (volatile asm) / 45.3 ms (plain asm), against 26.9 ms for the
 # hoisted-and-spilled default — the spills go away (k13: 302 -> 0) but the pinned scalar
-# loads cannot be scheduled around; not adopted.
+# loads cannot be scheduled around; not adopted. Never-taken branches every 100/300
+# statements (basic-block boundaries) made it worse: k13 630-666 SGPR spills, 1 wave/SIMD.
 PIN = os.environ.get("EC_PIN", "0") == "1"
 # ... pinned to the running sum EC_PIND accumulations back, so the load has that long to land
 PIND = int(os.environ.get("EC_PIND", "4"))
