@@ -129,14 +129,18 @@ __global__ __launch_bounds__(kThreads) void mix_kernel(uint32_t* out, const uint
 // ---- batch_evaluate_any (cpu.rs:362-393) -----------------------------------------
 // out[k] = sum_i coeffs[which[k]][i] * xs[k]^i. Evaluations of the same polynomial
 // are grouped (a trace column has one tap per `back`), so each coefficient is read
-// once per group. A workgroup takes a 16384-coefficient chunk of one polynomial; a
-// lane owns 64 consecutive coefficients and, per evaluation x, forms
-// sum_j c_j x^j as four unreduced u64 dot products against the x^j table in LDS
-// (4 v_mad_u64_u32 per coefficient, folded every 4), scales it by x^(64 lane) and
-// the block adds lanes. A last kernel combines chunks by Horner in x^16384.
+// once per group. A workgroup reads a 16384-coefficient chunk of one polynomial; each of
+// its waves owns 4096 of them and works alone (no workgroup barrier per evaluation).
+// The wave reads its piece with fully coalesced 1 KB uint4 loads, so lane l holds the
+// coefficients at 256 q + 4 l + r (q < 16, r < 4); per evaluation x it forms
+// sum c x^(256 q + r) as four unreduced u64 dot products against the wave's copy of that
+// 64-entry table in LDS (4 v_mad_u64_u32 per coefficient, folded every 4), scales by
+// x^(4 l), and the wave adds its lanes with xor shuffles. A last kernel combines the
+// 4096-coefficient pieces by Horner in x^4096.
 constexpr int kEvLane = 64;                     // coefficients per lane
+constexpr int kEvWave = 64 * kEvLane;           // 4096 per wave
 constexpr int kEvChunk = kThreads * kEvLane;    // 16384 per workgroup
-constexpr int kEvTab = kEvLane + kThreads + 1;  // x^0..63, x^(64 t) t < 256, x^16384
+constexpr int kEvTab = kEvLane + 64 + 1;        // x^(256 q + r), x^(4 l) l < 64, x^4096
 
 __global__ __launch_bounds__(kThreads) void eval_tables_kernel(const uint32_t* __restrict__ xs, uint32_t evals,
                                                              uint32_t* tab) {
@@ -144,8 +148,15 @@ __global__ __launch_bounds__(kThreads) void eval_tables_kernel(const uint32_t* _
   if (id >= uint64_t(evals) * kEvTab) return;
   const uint32_t k = uint32_t(id / kEvTab), e = uint32_t(id % kEvTab);
   const FpExt x = ld_fe(xs + 4 * k);
-  const uint64_t pw = e < kEvLane ? e : (e < kEvLane + kThreads ? uint64_t(kEvLane) * (e - kEvLane) : kEvChunk);
+  const uint64_t pw = e < kEvLane ? 256 * (e >> 2) + (e & 3) : (e < kEvLane + 64 ? 4 * (e - kEvLane) : kEvWave);
   st_fe(tab + (uint64_t(k) * kEvTab + e) * 4, fe_pow(x, pw));
+}
+
+__device__ __forceinline__ FpExt shfl_xor4(const FpExt& a, int m) {
+  FpExt r;
+#pragma unroll
+  for (int i = 0; i < 4; i++) r.c[i] = __shfl_xor(a.c[i], m, 64);
+  return r;
 }
 
 __global__ __launch_bounds__(kThreads) void eval_chunk_kernel(const uint32_t* __restrict__ coeffs, uint64_t n,
@@ -153,18 +164,18 @@ __global__ __launch_bounds__(kThreads) void eval_chunk_kernel(const uint32_t* __
                                                             const uint32_t* __restrict__ gbegin,
                                                             const uint32_t* __restrict__ geval,
                                                             const uint32_t* __restrict__ tab, uint32_t* partial,
-                                                            uint32_t nchunks) {
-  __shared__ FpExt xp[kEvLane];
-  __shared__ FpExt red[kThreads];
-  const uint32_t g = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
+                                                            uint32_t npieces) {
+  __shared__ FpExt xp[kThreads / 64][kEvLane];  // one x^0..63 table per wave
+  const uint32_t g = blockIdx.y, chunk = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t piece = chunk * (kThreads / 64) + wave;
   const uint32_t* poly = coeffs + uint64_t(gpoly[g]) * n;
-  const uint64_t start = uint64_t(chunk) * kEvChunk + uint64_t(tid) * kEvLane;
-  uint32_t c[kEvLane];
-  if (start + kEvLane <= n) {
+  const uint64_t start = uint64_t(piece) * kEvWave;
+  uint32_t c[kEvLane];  // c[4 q + r] = coefficient start + 256 q + 4 lane + r
+  if (start + kEvWave <= n) {
     const uint4* src = reinterpret_cast<const uint4*>(poly + start);
 #pragma unroll
     for (int q = 0; q < kEvLane / 4; q++) {
-      const uint4 v = src[q];
+      const uint4 v = src[q * 64 + lane];
       c[4 * q] = v.x;
       c[4 * q + 1] = v.y;
       c[4 * q + 2] = v.z;
@@ -172,44 +183,67 @@ __global__ __launch_bounds__(kThreads) void eval_chunk_kernel(const uint32_t* __
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < kEvLane; j++) c[j] = start + j < n ? poly[start + j] : 0u;
+    for (int j = 0; j < kEvLane; j++) {
+      const uint64_t i = start + 256 * (j >> 2) + 4 * lane + (j & 3);
+      c[j] = i < n ? poly[i] : 0u;
+    }
   }
+  FpExt* t = xp[wave];
   for (uint32_t q = gbegin[g]; q < gbegin[g + 1]; q++) {
     const uint32_t k = geval[q];
     const uint32_t* tk = tab + uint64_t(k) * kEvTab * 4;
-    __syncthreads();  // previous evaluation's readers of xp / red are done
-    if (tid < kEvLane) xp[tid] = ld_fe(tk + 4 * tid);
-    __syncthreads();
+    // the wave's previous readers of t are done (one wave, LDS ops in order): rewrite it
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    t[lane] = ld_fe(tk + 4 * lane);
+    const FpExt scale = ld_fe(tk + 4 * (kEvLane + lane));
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     uint64_t acc[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int j = 0; j < kEvLane; j++) {
-      const FpExt w = xp[j];
+      const FpExt w = t[j];
 #pragma unroll
       for (int i = 0; i < 4; i++) acc[i] += uint64_t(c[j]) * w.c[i];
       if (j % 4 == 3) {
 #pragma unroll
         for (int i = 0; i < 4; i++) acc[i] = fold64(acc[i]);
+        // keep the table reads next to their products: hoisted, the 64 ds_read_b128
+        // results took 256 VGPRs and spilled to scratch
+        asm volatile("" ::: "memory");
       }
     }
     FpExt a{{mont_reduce(acc[0]), mont_reduce(acc[1]), mont_reduce(acc[2]), mont_reduce(acc[3])}};
-    red[tid] = fe_mul(a, ld_fe(tk + 4 * (kEvLane + tid)));
-    __syncthreads();
-    for (uint32_t w2 = kThreads / 2; w2 >= 1; w2 >>= 1) {
-      if (tid < w2) red[tid] = fe_add(red[tid], red[tid + w2]);
-      __syncthreads();
-    }
-    if (tid == 0) st_fe(partial + (uint64_t(k) * nchunks + chunk) * 4, red[0]);
+    a = fe_mul(a, scale);
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) a = fe_add(a, shfl_xor4(a, m));
+    if (lane == 0) st_fe(partial + (uint64_t(k) * npieces + piece) * 4, a);
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
-__global__ void eval_any_reduce(const uint32_t* partial, uint32_t nchunks, const uint32_t* tab, uint32_t* out,
-                                uint32_t evals) {
-  uint32_t k = blockIdx.x * kThreads + threadIdx.x;
-  if (k >= evals) return;
-  const FpExt y = ld_fe(tab + (uint64_t(k) * kEvTab + kEvTab - 1) * 4);  // x^16384
+// one wave per evaluation: lane l runs Horner over pieces l, l + 64, ... in y^64 (y = x^4096),
+// then the wave adds S_l * y^l
+__global__ __launch_bounds__(kThreads) void eval_any_reduce(const uint32_t* partial, uint32_t npieces,
+                                                          const uint32_t* tab, uint32_t* out, uint32_t evals) {
+  const uint32_t k = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (k >= evals) return;  // whole waves leave together
+  const FpExt y = ld_fe(tab + (uint64_t(k) * kEvTab + kEvTab - 1) * 4);  // x^4096
+  FpExt y64 = y;
+#pragma unroll
+  for (int i = 0; i < 6; i++) y64 = fe_mul(y64, y64);
+  const uint32_t* pk = partial + uint64_t(k) * npieces * 4;
   FpExt s = fe_zero();
-  for (uint32_t c = nchunks; c-- > 0;) s = fe_add(fe_mul(s, y), ld_fe(partial + (uint64_t(k) * nchunks + c) * 4));
-  st_fe(out + uint64_t(k) * 4, s);
+  if (lane < npieces) {
+    uint32_t c = lane + ((npieces - 1 - lane) / 64) * 64;  // the lane's last piece
+    for (;; c -= 64) {
+      s = fe_add(fe_mul(s, y64), ld_fe(pk + uint64_t(c) * 4));
+      if (c < 64) break;
+    }
+  }
+  s = fe_mul(s, fe_pow(y, lane));
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) s = fe_add(s, shfl_xor4(s, m));
+  if (lane == 0) st_fe(out + uint64_t(k) * 4, s);
 }
 
 // ---- prefix products (cpu.rs:637-642), serial by definition --------------------------
@@ -475,6 +509,7 @@ void batch_evaluate_any_host(hipStream_t s, const uint32_t* coeffs, size_t poly_
   if (!eval_count) return;
   const uint64_t n = uint64_t(1) << log_n;
   const uint32_t nchunks = uint32_t((n + kEvChunk - 1) / kEvChunk);
+  const uint32_t npieces = nchunks * (kThreads / 64);  // 4096-coefficient pieces, one per wave
   // group evaluations by polynomial
   std::map<uint32_t, std::vector<uint32_t>> groups;
   for (size_t k = 0; k < eval_count; k++) {
@@ -497,14 +532,14 @@ void batch_evaluate_any_host(hipStream_t s, const uint32_t* coeffs, size_t poly_
   upload_async(d_gbegin, gbegin.data(), gbegin.size() * 4);
   upload_async(d_geval, geval.data(), geval.size() * 4);
   uint32_t* tab = static_cast<uint32_t*>(scratch(eval_count * kEvTab * 16, 12));
-  uint32_t* partial = static_cast<uint32_t*>(scratch(eval_count * nchunks * 16, 2));
+  uint32_t* partial = static_cast<uint32_t*>(scratch(eval_count * npieces * 16, 2));
   hipLaunchKernelGGL(eval_tables_kernel, dim3(div_up(eval_count * kEvTab, kThreads)), dim3(kThreads), 0, s, xs,
                      uint32_t(eval_count), tab);
   HIP_OK(hipGetLastError());
   hipLaunchKernelGGL(eval_chunk_kernel, dim3(nchunks, unsigned(groups.size())), dim3(kThreads), 0, s, coeffs, n,
-                     d_gpoly, d_gbegin, d_geval, tab, partial, nchunks);
+                     d_gpoly, d_gbegin, d_geval, tab, partial, npieces);
   HIP_OK(hipGetLastError());
-  hipLaunchKernelGGL(eval_any_reduce, dim3(div_up(eval_count, kThreads)), dim3(kThreads), 0, s, partial, nchunks,
+  hipLaunchKernelGGL(eval_any_reduce, dim3(div_up(eval_count, kThreads / 64)), dim3(kThreads), 0, s, partial, npieces,
                      tab, out, uint32_t(eval_count));
   HIP_OK(hipGetLastError());
 }
