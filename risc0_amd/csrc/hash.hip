@@ -72,6 +72,26 @@ __global__ __launch_bounds__(kThreads) void p2_fold_kernel(uint32_t* io, uint64_
   store_digest(io + (out_off + i) * 8, c);
 }
 
+// Small layers: four lanes per node (poseidon2_mix_quad), so a layer of n nodes keeps 4n
+// lanes busy. Lane q loads cells 4j + q (j < 4) of the two child digests and stores
+// digest words q and 4 + q.
+__global__ __launch_bounds__(kThreads) void p2_fold_quad_kernel(uint32_t* io, uint64_t in_off, uint64_t out_off,
+                                                              uint64_t n) {
+  const uint64_t t = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  const uint64_t i = t >> 2;
+  if (i >= n) return;  // whole quads: n * 4 lanes
+  const uint32_t q = threadIdx.x & 3;
+  const uint32_t* src = io + (in_off + 2 * i) * 8;
+  uint32_t c[6];
+#pragma unroll
+  for (int j = 0; j < 4; j++) c[j] = src[4 * j + q];
+  c[4] = c[5] = 0;
+  poseidon2_mix_quad(c);
+  uint32_t* dst = io + (out_off + i) * 8;
+  dst[q] = c[0];
+  dst[4 + q] = c[1];
+}
+
 // ---- Poseidon254 (BN254 Fr, poseidon_254/mod.rs) ---------------------------------
 // One lane per row as above; the 3-cell state is 27 VGPRs of 29-bit limbs. Row values are
 // decoded from Montgomery to canonical (Elem::as_u32) and packed 8 per cell.
@@ -205,8 +225,42 @@ __global__ __launch_bounds__(kThreads) void sha_fold_kernel(uint32_t* io, uint64
   store_digest(io + (out_off + i) * 8, d);
 }
 
-// Top of a tree inside one workgroup: layers with <= 512 nodes, all hashed by
-// 256 lanes with a workgroup barrier between layers (same-CU visibility).
+// Poseidon2 tree top in one workgroup of 512 lanes: layers of >= 256 nodes one lane per
+// node, smaller layers one quad per node (measured per layer size).
+constexpr uint32_t kTopThreads = 512;
+__global__ __launch_bounds__(kTopThreads) void p2_fold_top_kernel(uint32_t* io, uint32_t top_layer_size,
+                                                                 uint32_t quad_max) {
+  for (uint32_t out = top_layer_size; out >= 1; out >>= 1) {
+    if (out > quad_max) {
+      for (uint32_t i = threadIdx.x; i < out; i += kTopThreads) {
+        const uint32_t* src = io + (uint64_t(2 * out) + 2 * i) * 8;
+        uint32_t c[24];
+#pragma unroll
+        for (int k = 0; k < 16; k++) c[k] = src[k];
+#pragma unroll
+        for (int k = 16; k < 24; k++) c[k] = 0;
+        poseidon2_mix(c);
+        store_digest(io + (uint64_t(out) + i) * 8, c);
+      }
+    } else if (threadIdx.x < 4 * out) {
+      const uint32_t i = threadIdx.x >> 2, q = threadIdx.x & 3;
+      const uint32_t* src = io + (uint64_t(2 * out) + 2 * i) * 8;
+      uint32_t c[6];
+#pragma unroll
+      for (int j = 0; j < 4; j++) c[j] = src[4 * j + q];
+      c[4] = c[5] = 0;
+      poseidon2_mix_quad(c);
+      uint32_t* dst = io + (uint64_t(out) + i) * 8;
+      dst[q] = c[0];
+      dst[4 + q] = c[1];
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
+}
+
+// SHA-256 / Poseidon254 tree top inside one workgroup: layers with <= 512 nodes, all
+// hashed by 256 lanes with a workgroup barrier between layers (same-CU visibility).
 template <int SUITE>
 __global__ __launch_bounds__(kThreads) void fold_top_kernel(uint32_t* io, uint32_t top_layer_size) {
   for (uint32_t out = top_layer_size; out >= 1; out >>= 1) {
@@ -215,15 +269,6 @@ __global__ __launch_bounds__(kThreads) void fold_top_kernel(uint32_t* io, uint32
       uint32_t d[8];
       if (SUITE == 2) {
         p254_node(src, d);
-      } else if (SUITE == 0) {
-        uint32_t c[24];
-#pragma unroll
-        for (int k = 0; k < 16; k++) c[k] = src[k];
-#pragma unroll
-        for (int k = 16; k < 24; k++) c[k] = 0;
-        poseidon2_mix(c);
-#pragma unroll
-        for (int k = 0; k < 8; k++) d[k] = c[k];
       } else {
         uint32_t s[8], w[16];
         sha_init(s);
@@ -261,13 +306,32 @@ void hash_rows(hipStream_t s, int suite, uint32_t* out, const uint32_t* matrix, 
   HIP_OK(hipGetLastError());
 }
 
+// Poseidon2 layers up to this many nodes hash one quad per node: below it one lane per
+// node leaves SIMDs idle (<= 1 wave each), so the quad's 3x shorter latency wins.
+// R0_P2_QUAD_MAX overrides it (tools/micro/fold_latency.py measures the crossover).
+static size_t env_size(const char* name, size_t dflt) {
+  const char* e = getenv(name);
+  return e ? size_t(strtoull(e, nullptr, 10)) : dflt;
+}
+static size_t quad_fold_max() {
+  static const size_t v = env_size("R0_P2_QUAD_MAX", 32768);
+  return v;
+}
+// tree tops (one workgroup): quads for layers up to this size (R0_P2_TOP_QUAD_MAX)
+static uint32_t quad_top_max() {
+  static const uint32_t v = uint32_t(env_size("R0_P2_TOP_QUAD_MAX", 128));
+  return v;
+}
+
 void hash_fold(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t output_size) {
   if (output_size == 0) return;
   R0_REQUIRE(input_size == 2 * output_size, "hash_fold: input_size != 2*output_size");
   R0_REQUIRE(suite >= 0 && suite <= 2, "hash_fold: unknown hash suite");
   const dim3 grid(div_up(output_size, kThreads)), block(kThreads);
   const uint64_t in = input_size, out = output_size;
-  if (suite == 0)
+  if (suite == 0 && output_size <= quad_fold_max())
+    hipLaunchKernelGGL(p2_fold_quad_kernel, dim3(div_up(4 * output_size, kThreads)), block, 0, s, io, in, out, out);
+  else if (suite == 0)
     hipLaunchKernelGGL(p2_fold_kernel, grid, block, 0, s, io, in, out, out);
   else if (suite == 1)
     hipLaunchKernelGGL(sha_fold_kernel, grid, block, 0, s, io, in, out, out);
@@ -285,7 +349,8 @@ void merkle_tree(hipStream_t s, int suite, uint32_t* nodes, const uint32_t* matr
   for (; layer > 512; layer /= 2) hash_fold(s, suite, nodes, 2 * layer, layer);
   if (layer >= 1) {
     const dim3 grid(1), block(kThreads);
-    if (suite == 0) hipLaunchKernelGGL(fold_top_kernel<0>, grid, block, 0, s, nodes, uint32_t(layer));
+    if (suite == 0) hipLaunchKernelGGL(p2_fold_top_kernel, grid, dim3(kTopThreads), 0, s, nodes, uint32_t(layer),
+                                    quad_top_max());
     else if (suite == 1) hipLaunchKernelGGL(fold_top_kernel<1>, grid, block, 0, s, nodes, uint32_t(layer));
     else hipLaunchKernelGGL(fold_top_kernel<2>, grid, block, 0, s, nodes, uint32_t(layer));
     HIP_OK(hipGetLastError());

@@ -247,12 +247,13 @@ def test_hash_rows(hal, hal_sha, oracle, suite):
     assert np.array_equal(nodes.to_numpy()[rows * 8:], ref)
 
 
-@pytest.mark.parametrize("suite", ["poseidon2", "sha-256", "poseidon_254"])
-def test_hash_fold(hal, hal_sha, oracle, suite):
-    # hal/mod.rs:551-573 (1024 inputs; digests of reduced words for Poseidon2)
+@pytest.mark.parametrize("suite,inputs", [("poseidon2", 1024), ("sha-256", 1024), ("poseidon_254", 1024),
+                                          ("poseidon2", 1 << 17)])
+def test_hash_fold(hal, hal_sha, oracle, suite, inputs):
+    # hal/mod.rs:551-573 (1024 inputs; digests of reduced words for Poseidon2); 2^17
+    # inputs cross the Poseidon2 one-quad-per-node threshold (layers <= 32768 nodes)
     h, s = H(suite), S(oracle, suite)
     rng = np.random.default_rng(12)
-    inputs = 1024
     io = np.zeros(inputs * 2 * 8, np.uint32)
     io[inputs * 8:] = (rng.integers(0, 2**32, inputs * 8, dtype=np.uint64) // 3).astype(np.uint32)
     if suite == "poseidon_254":  # digests are canonical BN254 Fr values (< r < 2^254, mod.rs:94-98)

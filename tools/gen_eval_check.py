@@ -251,6 +251,11 @@ WAVES = int(os.environ.get("EC_WAVES", "2"))
 #   hoists and spills to VGPR lanes: ~640 v_writelane/v_readlane in k13)   not adopted:
 #   plain, volatile and sched_barrier-fenced LDS reads all compiled k13 to 256 VGPRs +
 #   256 AGPRs (1 wave/SIMD, AGPR spills) against 227 VGPRs at 2 waves with SGPR operands
+#   xmul as a polynomial product (c_0..c_6, then NBETA * REDC(c_4..c_6) added back: 38
+#   VALU against 43, no NBETA * b Montgomery products)   not adopted: 26.46 -> 27.29 ms;
+#   k16 -0.1 ms but k27 +0.68 ms (256 VGPRs + AGPRs, one wave per SIMD) because LLVM no
+#   longer shares NBETA * b between products with a common operand; a hybrid keeping the
+#   shared form for operands of several products still took k23/k27 to 256 VGPRs
 # The kernels are bound by register pressure and issue stalls (SQ_WAIT_INST_ANY 30-55% of
 # wave cycles), not by the count of VALU instructions.
 # EC_CANON=1: every Fp/FpExt result canonical; EC_CANON=0: the lazy range analysis below
