@@ -114,15 +114,17 @@ R0_HD uint32_t p2_sbox_lazy(uint32_t x) {  // x canonical -> x^7 in [0, 2p)
   uint32_t x6 = mont_lazy(uint64_t(x4) * x2);
   return mont_lazy(uint64_t(x6) * x);
 }
-// y = M_EXT * x over the integers (x < 2p)
+// y = M_EXT * x over the integers (x < 2p). The 32-bit cells enter the 64-bit sums
+// through v_mad_u64_u32 (x * 1 + acc, x * 2 + acc): a plain zero-extended add costs a
+// v_mov of the high word per cell first (49 per round in p2_fold_kernel).
 R0_HD void p2_m_ext64(const uint32_t* x, uint64_t* y) {
 #pragma unroll
   for (int b = 0; b < 6; b++) {
     const uint32_t* v = x + 4 * b;
-    uint64_t t0 = uint64_t(v[0]) + v[1];
-    uint64_t t1 = uint64_t(v[2]) + v[3];
-    uint64_t t2 = (uint64_t(v[1]) << 1) + t1;
-    uint64_t t3 = (uint64_t(v[3]) << 1) + t0;
+    uint64_t t0 = mad64(v[0], 1u, mad64(v[1], 1u, 0));
+    uint64_t t1 = mad64(v[2], 1u, mad64(v[3], 1u, 0));
+    uint64_t t2 = mad64(v[1], 2u, t1);
+    uint64_t t3 = mad64(v[3], 2u, t0);
     uint64_t t4 = (t1 << 2) + t3;
     uint64_t t5 = (t0 << 2) + t2;
     y[4 * b] = t3 + t5;
@@ -210,9 +212,10 @@ R0_HD void poseidon2_mix(uint32_t* c) {
     c[0] = p2_sbox_lazy(fp_add(umin(c[0], c[0] - kP), kP2Partial[r]));
     uint64_t s0 = 0, s1 = 0;
 #pragma unroll
-    for (int i = 0; i < 12; i++) s0 = mad64(c[i], kFoldC, s0);
-#pragma unroll
-    for (int i = 12; i < 24; i++) s1 = mad64(c[i], kFoldC, s1);
+    for (int i = 0; i < 12; i++) {  // two interleaved chains: no dependent back-to-back mads
+      s0 = mad64(c[i], kFoldC, s0);
+      s1 = mad64(c[12 + i], kFoldC, s1);
+    }
     const uint64_t sf = fold64(fold64(s0) + fold64(s1));
 #pragma unroll
     for (int i = 0; i < 24; i++) c[i] = mont_lazy(uint64_t(c[i]) * kP2Diag[i] + sf);
