@@ -416,10 +416,12 @@ def emit(circuit, outdir, budget, host=False):
         "EC_FN uint32_t ldc(const uint32_t* p, uint32_t off) {",
         "  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(p) + off);",
         "}",
-        "// trace tap: W = false indexes in 32 bits (col * domain + row < 2^32 words), W = true",
-        "// forms the column base in 64 bits (needed once columns x domain reach 2^32)",
-        "template <bool W> EC_FN uint32_t tap(const uint32_t* a, uint32_t col, uint32_t domain, uint32_t row) {",
-        "  if constexpr (W) return ldc(a + uint64_t(col) * domain, row * 4u);",
+        "// trace tap: W = false indexes in 32 bits (col * domain + row < 2^32 words); W = true",
+        "// (columns x domain >= 2^32) takes the column's base from the host table A.cp (one",
+        "// scalar load) plus a 32-bit byte offset, instead of a 64-bit col * domain per tap",
+        "template <bool W> EC_FN uint32_t tap(const uint32_t* a, const uint32_t* const* cp, uint32_t slot, uint32_t col,",
+        "                                     uint32_t domain, uint32_t row) {",
+        "  if constexpr (W) return ldc(cp[slot], row * 4u);",
         "  else return a[col * domain + row];",
         "}",
         "EC_FN uint32_t lred(uint32_t x) { return umin(x, x - kP); }",
@@ -819,10 +821,10 @@ def emit(circuit, outdir, budget, host=False):
                 continue
             if op == "l" and not SADDR:
                 # tap<W>: 32-bit column index while columns x domain < 2^32 words (every
-                # po2 <= 22), 64-bit column base above (211 columns x 2^26 points at po2=24);
-                # each kernel is instantiated for both, the launcher picks by domain
+                # po2 <= 22), the column-pointer table above (211 columns x 2^26 points at
+                # po2=24); each kernel is instantiated for both, the launcher picks by domain
                 g, col, back = ins[2], ins[3], ins[4]
-                w(f"  const uint32_t v{i} = tap<W>(A.a[{g}], {col}u, A.domain, (cycle - {4 * back}u) & mask);")
+                w(f"  const uint32_t v{i} = tap<W>(A.a[{g}], A.cp, {colslot[(g, col)]}u, {col}u, A.domain, (cycle - {4 * back}u) & mask);")
                 Mv[i] = PM
                 continue
             if op == "l":
