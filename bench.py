@@ -300,7 +300,8 @@ def end_to_end(r, hal, args, witness, k, version):
             "ms_per_step": round(1000.0 * t / args.e2e_steps, 3), "steps": args.e2e_steps,
             "h2d_bytes_per_segment": int(h2d_bytes), "ms_one_segment_unpipelined": round(1000.0 * t_one, 1),
             "note": f"witness in pinned host memory; native pipeline (r0hip_prove_segments): an uploader fills "
-                    f"{k + 1} device buffer sets ahead of {k} prover threads, so H2D overlaps proving"}
+                    f"{k + 1} device buffer sets ahead of {k} prover threads, so H2D overlaps proving; a prover "
+                    f"starts a segment while its later witness groups still upload (per-group gate)"}
 
 
 def pmc_traffic(family, calls, args):

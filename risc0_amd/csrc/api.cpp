@@ -21,7 +21,8 @@ void run_eval_check(const CircuitDef& c, uint32_t* check, const uint32_t* const*
                     const uint32_t* global, FpExt poly_mix, size_t po2);
 std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2, const uint32_t* code,
                                     const uint32_t* data, const uint32_t* accum, uint32_t* global,
-                                    bool write_version, uint32_t version, std::vector<uint32_t>* mix_out);
+                                    bool write_version, uint32_t version, std::vector<uint32_t>* mix_out,
+                                    const UploadGate* uploads = nullptr);
 std::string last_profile();
 }  // namespace r0
 

@@ -4,8 +4,10 @@
 // the zkvm prover (risc0/zkvm/src/host/server/prove/prover_impl.rs:84-94), native here.
 //
 // One uploader thread copies a job's witness groups from host memory (page-locked for
-// full PCIe rate) into a free device buffer set on its own stream; `in_flight` prover
-// threads each take a filled set, run the whole-segment prover on their own stream
+// full PCIe rate) into a free device buffer set on its own stream, recording an event per
+// group; `in_flight` prover threads each take a set as soon as its copies are queued, run
+// the whole-segment prover on their own stream (which waits on each group's event just
+// before that group's first use)
 // (runtime.cpp gives every host thread its own stream, pool and staging), write the
 // seal, and hand the set back. in_flight + 1 sets circulate, so an upload is always
 // running ahead while the GPU proves. Each job reports its own error.
@@ -27,13 +29,36 @@
 namespace r0 {
 std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2, const uint32_t* code,
                                     const uint32_t* data, const uint32_t* accum, uint32_t* global,
-                                    bool write_version, uint32_t version, std::vector<uint32_t>* mix_out);
+                                    bool write_version, uint32_t version, std::vector<uint32_t>* mix_out,
+                                    const UploadGate* uploads);
 
 namespace {
 
-struct BufSet {
-  DevBuf g[4];  // code, data, accum, global
+// A device buffer set and its upload state. hipMemcpyAsync from page-locked memory returns
+// only when a large copy is done, so the set is handed to a prover before its copies are
+// queued: the prover blocks in wait(g) until the uploader has queued group g and recorded
+// its event, then its stream waits on that event.
+struct BufSet final : UploadGate {
+  DevBuf g[4];         // code, data, accum, global
+  hipEvent_t ev[4]{};  // recorded on the uploader stream after each group's copy
   size_t job = 0;
+  mutable std::mutex mu;
+  mutable std::condition_variable cv;
+  int queued = 0;      // bit g: group g's copy is queued and ev[g] recorded (or the upload failed)
+  void mark(int bits) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      queued |= bits;
+    }
+    cv.notify_all();
+  }
+  void wait(int grp, hipStream_t s) const override {
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return (queued >> grp) & 1; });
+    }
+    HIP_OK(hipStreamWaitEvent(s, ev[grp], 0));
+  }
 };
 
 // a bounded queue of set indices
@@ -85,8 +110,19 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
     // group_sizes: accum 0, code 1, data 2 (the reference's register-group order)
     const size_t words[4] = {c->group_sizes[1] * n, c->group_sizes[2] * n, c->group_sizes[0] * n, c->output_size};
     std::vector<BufSet> sets(k + 1);
+    struct Events {  // destroyed on every exit path
+      std::vector<BufSet>& sets;
+      ~Events() {
+        for (auto& s : sets)
+          for (auto& e : s.ev)
+            if (e) (void)hipEventDestroy(e);
+      }
+    } events{sets};
     for (auto& s : sets)
-      for (int g = 0; g < 4; g++) s.g[g] = DevBuf(words[g]);
+      for (int g = 0; g < 4; g++) {
+        s.g[g] = DevBuf(words[g]);
+        HIP_OK(hipEventCreateWithFlags(&s.ev[g], hipEventDisableTiming));
+      }
     HIP_OK(hipDeviceSynchronize());  // allocations complete before other streams use them
     for (size_t i = 0; i < njobs; i++) {
       jobs[i].error = nullptr;
@@ -101,18 +137,35 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
         long s = free_q.get();
         BufSet& b = sets[s];
         b.job = i;
+        {
+          std::lock_guard<std::mutex> lk(b.mu);
+          b.queued = 0;  // the set is free: no prover waits on it
+        }
+        const uint32_t* src[4] = {jobs[i].h_code, jobs[i].h_data, jobs[i].h_accum, jobs[i].h_global};
+        bool null_group = false;
+        for (int g = 0; g < 4; g++) null_group |= !src[g];
+        if (null_group) jobs[i].error = dup_msg("witness group pointer is NULL");  // before the hand-over
+        ready_q.put(s);  // a prover may start now; it waits per group (BufSet::wait)
+        if (null_group) {
+          b.mark(15);
+          continue;
+        }
         try {
           ensure_init();
-          const uint32_t* src[4] = {jobs[i].h_code, jobs[i].h_data, jobs[i].h_accum, jobs[i].h_global};
-          for (int g = 0; g < 4; g++) {
-            R0_REQUIRE(src[g], "witness group pointer is NULL");
+          // in the order the prover first touches them (globals, code, data, accum), so a
+          // segment's code commit overlaps its data upload and its data commit the accum upload
+          for (int g : {3, 0, 1, 2}) {
             HIP_OK(hipMemcpyAsync(b.g[g].p, src[g], words[g] * 4, hipMemcpyHostToDevice, stream()));
+            HIP_OK(hipEventRecord(b.ev[g], stream()));
+            b.mark(1 << g);
           }
-          HIP_OK(hipStreamSynchronize(stream()));
         } catch (const std::exception& e) {
-          jobs[i].error = dup_msg(e.what());
+          {
+            std::lock_guard<std::mutex> lk(b.mu);
+            if (!jobs[i].error) jobs[i].error = dup_msg(e.what());
+          }
+          b.mark(15);  // release a waiting prover; the job reports the error
         }
-        ready_q.put(s);
       }
       for (size_t t = 0; t < k; t++) ready_q.put(-1);  // one stop token per prover
     });
@@ -125,19 +178,29 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
           if (s < 0) return;
           BufSet& b = sets[s];
           r0hip_segment_job& j = jobs[b.job];
-          if (!j.error) {
+          // j.error is written by the uploader under b.mu while this job's copies are queued
+          auto failed = [&] {
+            std::lock_guard<std::mutex> lk(b.mu);
+            return j.error != nullptr;
+          };
+          if (!failed()) {
             try {
               ensure_init();
               std::vector<uint32_t> mix;
               std::vector<uint32_t> seal = prove_segment(*c, suite, po2, b.g[0].p, b.g[1].p, b.g[2].p, b.g[3].p,
-                                                         write_version != 0, version, &mix);
+                                                         write_version != 0, version, &mix, &b);
               HIP_OK(hipStreamSynchronize(stream()));
-              j.seal_len = seal.size();
-              if (j.h_mix_out) memcpy(j.h_mix_out, mix.data(), mix.size() * 4);
-              R0_REQUIRE(!j.h_seal || seal.size() <= j.seal_cap, "seal buffer too small");
-              if (j.h_seal) memcpy(j.h_seal, seal.data(), seal.size() * 4);
+              if (!failed()) {  // an upload error leaves the proof meaningless: drop it
+                j.seal_len = seal.size();
+                if (j.h_mix_out) memcpy(j.h_mix_out, mix.data(), mix.size() * 4);
+                R0_REQUIRE(!j.h_seal || seal.size() <= j.seal_cap, "seal buffer too small");
+                if (j.h_seal) memcpy(j.h_seal, seal.data(), seal.size() * 4);
+              }
             } catch (const std::exception& e) {
-              j.error = dup_msg(e.what());
+              {
+                std::lock_guard<std::mutex> lk(b.mu);
+                if (!j.error) j.error = dup_msg(e.what());
+              }
               // kernels queued before the throw may still read this buffer set: drain
               // them before the uploader refills it
               drain_after_error();

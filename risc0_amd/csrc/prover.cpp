@@ -510,13 +510,19 @@ thread_local std::string g_last_profile;  // per host thread (segments in flight
 std::string last_profile() { return g_last_profile; }
 
 // circuit/rv32im/src/prove/hal/mod.rs:181-224 (recursion: prove/mod.rs:176-226, no version word)
+// `uploads` (optional): the groups may still be uploading; each is waited for just before
+// its first use, so a segment's early phases overlap the upload of its later groups
 std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2, const uint32_t* code,
                                     const uint32_t* data, const uint32_t* accum, uint32_t* global,
-                                    bool write_version, uint32_t version, std::vector<uint32_t>* mix_out) {
+                                    bool write_version, uint32_t version, std::vector<uint32_t>* mix_out,
+                                    const UploadGate* uploads) {
   R0_REQUIRE(suite >= 0 && suite <= 2, "unknown hash suite");
   R0_REQUIRE(po2 >= 2 && po2 <= 24, "po2 out of range");
   Span span("prove_core");
   hipStream_t s = stream();
+  auto gate = [&](int g) {
+    if (uploads) uploads->wait(g, s);
+  };
   stage_reset();
   Profile prof;
   prof.mark("start");
@@ -530,6 +536,7 @@ std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2
   p.iop.commit(hash_elems(suite, psi, 16));
   p.iop.commit(hash_elems(suite, ci, 16));
   // header = globals (INVALID -> 0, in place) || po2 as a raw word
+  gate(3);
   eltwise_zeroize(s, global, c.output_size);
   std::vector<uint32_t> header(c.output_size + 1);
   d2h(header.data(), global, c.output_size * 4);
@@ -538,8 +545,10 @@ std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2
   p.iop.write(header.data(), header.size());
   p.po2 = po2;
   p.cycles = size_t(1) << po2;
+  gate(0);
   p.commit_group(1, code);
   prof.mark("commit_code");
+  gate(1);
   p.commit_group(2, data);
   prof.mark("commit_data");
   std::vector<uint32_t> mix(c.mix_size);
@@ -547,6 +556,7 @@ std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2
   if (mix_out) *mix_out = mix;
   DevBuf dmix(mix.size() ? mix.size() : 1);
   upload_async(dmix.p, mix.data(), mix.size() * 4);
+  gate(2);
   p.commit_group(0, accum);
   prof.mark("commit_accum");
   p.finalize(dmix.p, global);

@@ -81,6 +81,15 @@ struct Span {
   Span& operator=(const Span&) = delete;
 };
 
+// Witness groups that may still be uploading when a proof starts (the segment pipeline):
+// wait(g, s) returns once group g (0 code, 1 data, 2 accum, 3 global) has its copy queued,
+// with stream s made to wait for the copy on the device.
+struct UploadGate {
+  virtual void wait(int group, hipStream_t s) const = 0;
+ protected:
+  ~UploadGate() = default;
+};
+
 // Workgroups for a 1-D launch of a lanes at b per workgroup. An AQL dispatch counts
 // work-items in 32 bits, so a grid of 2^32 or more lanes cannot launch; such sizes go
 // through grid_stride() instead.
