@@ -26,13 +26,26 @@ __device__ __forceinline__ void store_digest(uint32_t* out, const uint32_t* d) {
   o[1] = make_uint4(d[4], d[5], d[6], d[7]);
 }
 
-__global__ __launch_bounds__(kThreads) void p2_rows_kernel(uint32_t* out, const uint32_t* __restrict__ m,
-                                                         uint64_t rows, uint32_t cols) {
+// FIRST/LAST: a column range of a longer row (hash_rows_range) starts from the capacity
+// cells 16..23 saved in `state` and ends by saving them there (overwrite-mode sponge: the
+// rate cells are replaced by the next block, so the capacity is the whole carried state)
+template <bool FIRST, bool LAST>
+__global__ __launch_bounds__(kThreads) void p2_rows_kernel(uint32_t* out, uint32_t* state,
+                                                         const uint32_t* __restrict__ m, uint64_t rows,
+                                                         uint32_t cols) {
   uint64_t row = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (row >= rows) return;
   uint32_t c[24];
 #pragma unroll
-  for (int i = 0; i < 24; i++) c[i] = 0;
+  for (int i = 0; i < 16; i++) c[i] = 0;
+  if (FIRST) {
+#pragma unroll
+    for (int i = 16; i < 24; i++) c[i] = 0;
+  } else {
+    const uint4* st = reinterpret_cast<const uint4*>(state + row * 8);
+    const uint4 a = st[0], b = st[1];
+    c[16] = a.x; c[17] = a.y; c[18] = a.z; c[19] = a.w; c[20] = b.x; c[21] = b.y; c[22] = b.z; c[23] = b.w;
+  }
   // blocks of 16 columns (the last one zero-padded; cols == 0 is one all-zero block),
   // software-pipelined: the next block's loads are in flight while the current block is
   // permuted. One permutation call site keeps the kernel small for the instruction cache.
@@ -54,7 +67,8 @@ __global__ __launch_bounds__(kThreads) void p2_rows_kernel(uint32_t* out, const 
     if (b + 1 < nblk) load((b + 1) * 16);
     poseidon2_mix(c);
   }
-  store_digest(out + row * 8, c);
+  if (LAST) store_digest(out + row * 8, c);
+  else store_digest(state + row * 8, c + 16);
 }
 
 __global__ __launch_bounds__(kThreads) void p2_fold_kernel(uint32_t* io, uint64_t in_off, uint64_t out_off,
@@ -185,12 +199,19 @@ __device__ __forceinline__ void sha_init(uint32_t* s) {
 }
 
 // Digest words are the big-endian digest bytes in memory order: bswap each state word.
-__global__ __launch_bounds__(kThreads) void sha_rows_kernel(uint32_t* out, const uint32_t* __restrict__ m,
-                                                          uint64_t rows, uint32_t cols) {
+template <bool FIRST, bool LAST>
+__global__ __launch_bounds__(kThreads) void sha_rows_kernel(uint32_t* out, uint32_t* state,
+                                                          const uint32_t* __restrict__ m, uint64_t rows,
+                                                          uint32_t cols) {
   uint64_t row = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (row >= rows) return;
   uint32_t s[8], w[16], nxt[16];
-  sha_init(s);
+  if (FIRST) {
+    sha_init(s);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; i++) s[i] = state[row * 8 + i];
+  }
   // the next block's loads are in flight during the current compression
   auto load = [&](uint32_t col) {
 #pragma unroll
@@ -202,6 +223,10 @@ __global__ __launch_bounds__(kThreads) void sha_rows_kernel(uint32_t* out, const
     for (int i = 0; i < 16; i++) w[i] = __builtin_bswap32(nxt[i]);
     if (col + 16 < cols) load(col + 16);
     sha_compress(s, w);
+  }
+  if (!LAST) {
+    store_digest(state + row * 8, s);
+    return;
   }
   uint32_t d[8];
 #pragma unroll
@@ -298,12 +323,43 @@ void hash_rows(hipStream_t s, int suite, uint32_t* out, const uint32_t* matrix, 
             suite == 0 ? perms * kP2Modmuls : 0);
   const dim3 grid(div_up(rows, kThreads)), block(kThreads);
   if (suite == 0)
-    hipLaunchKernelGGL(p2_rows_kernel, grid, block, 0, s, out, matrix, uint64_t(rows), uint32_t(cols));
+    hipLaunchKernelGGL((p2_rows_kernel<true, true>), grid, block, 0, s, out, nullptr, matrix, uint64_t(rows),
+                       uint32_t(cols));
   else if (suite == 1)
-    hipLaunchKernelGGL(sha_rows_kernel, grid, block, 0, s, out, matrix, uint64_t(rows), uint32_t(cols));
+    hipLaunchKernelGGL((sha_rows_kernel<true, true>), grid, block, 0, s, out, nullptr, matrix, uint64_t(rows),
+                       uint32_t(cols));
   else
     hipLaunchKernelGGL(p254_rows_kernel, grid, block, 0, s, out, matrix, uint64_t(rows), uint32_t(cols));
   HIP_OK(hipGetLastError());
+}
+
+template <bool FIRST, bool LAST>
+static void launch_rows_range(hipStream_t s, int suite, uint32_t* out, uint32_t* state, const uint32_t* chunk,
+                              size_t rows, size_t cols) {
+  const dim3 grid(div_up(rows, kThreads)), block(kThreads);
+  if (suite == 0)
+    hipLaunchKernelGGL((p2_rows_kernel<FIRST, LAST>), grid, block, 0, s, out, state, chunk, uint64_t(rows),
+                       uint32_t(cols));
+  else
+    hipLaunchKernelGGL((sha_rows_kernel<FIRST, LAST>), grid, block, 0, s, out, state, chunk, uint64_t(rows),
+                       uint32_t(cols));
+  HIP_OK(hipGetLastError());
+}
+
+void hash_rows_range(hipStream_t s, int suite, uint32_t* out, uint32_t* state, const uint32_t* chunk, size_t rows,
+                     size_t cols, bool first, bool last) {
+  if (rows == 0) return;
+  R0_REQUIRE(suite == 0 || suite == 1, "hash_rows_range: Poseidon2 and SHA-256 only");
+  R0_REQUIRE(last || (cols > 0 && cols % 16 == 0), "hash_rows_range: a range before the last needs 16k columns");
+  R0_REQUIRE(cols > 0 || (first && last), "hash_rows_range: empty range");
+  R0_REQUIRE((first && last) || state, "hash_rows_range: state buffer is NULL");
+  static const char* names[2] = {"hash_rows_poseidon2", "hash_rows_sha256"};
+  const double perms = double(rows) * ((cols + 15) / 16);
+  KScope ks(names[suite], double(rows) * (cols * 4 + 32), suite == 0 ? perms * kP2Modmuls : 0);
+  if (first && last) launch_rows_range<true, true>(s, suite, out, state, chunk, rows, cols);
+  else if (first) launch_rows_range<true, false>(s, suite, out, state, chunk, rows, cols);
+  else if (last) launch_rows_range<false, true>(s, suite, out, state, chunk, rows, cols);
+  else launch_rows_range<false, false>(s, suite, out, state, chunk, rows, cols);
 }
 
 // Poseidon2 layers up to this many nodes hash one quad per node: below it one lane per
@@ -343,6 +399,10 @@ void hash_fold(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t
 // MerkleTreeProver::new (risc0/zkp/src/prove/merkle.rs:54-81): leaves, then every layer.
 void merkle_tree(hipStream_t s, int suite, uint32_t* nodes, const uint32_t* matrix, size_t rows, size_t cols) {
   hash_rows(s, suite, nodes + rows * 8, matrix, rows, cols);
+  merkle_layers(s, suite, nodes, rows);
+}
+
+void merkle_layers(hipStream_t s, int suite, uint32_t* nodes, size_t rows) {
   static const char* names[3] = {"merkle_fold_poseidon2", "merkle_fold_sha256", "merkle_fold_poseidon254"};
   KScope ks(names[suite], double(rows) * 32 * 1.5, suite == 0 ? double(rows - 1) * kP2Modmuls : 0);
   size_t layer = rows / 2;

@@ -14,6 +14,7 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <deque>
 #include <mutex>
 #include <stdexcept>
@@ -34,30 +35,48 @@ std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2
 
 namespace {
 
+// Columns per upload chunk: a multiple of 16, so the prover can hash a group's rows range by
+// range as the chunks land (hash_rows_range); ~200 MB per chunk at po2=20.
+constexpr size_t kChunkCols = 48;
+
 // A device buffer set and its upload state. hipMemcpyAsync from page-locked memory returns
 // only when a large copy is done, so the set is handed to a prover before its copies are
-// queued: the prover blocks in wait(g) until the uploader has queued group g and recorded
-// its event, then its stream waits on that event.
+// queued: the prover blocks in wait() until the uploader has queued the chunks it needs and
+// recorded the last one's event, then its stream waits on that event.
 struct BufSet final : UploadGate {
-  DevBuf g[4];         // code, data, accum, global
-  hipEvent_t ev[4]{};  // recorded on the uploader stream after each group's copy
+  DevBuf g[4];                     // code, data, accum, global
+  size_t cols[4] = {1, 1, 1, 1};   // columns per group (global: one)
+  size_t col_words[4] = {0, 0, 0, 0};
+  std::vector<hipEvent_t> ev[4];   // per chunk, recorded on the uploader stream
   size_t job = 0;
   mutable std::mutex mu;
   mutable std::condition_variable cv;
-  int queued = 0;      // bit g: group g's copy is queued and ev[g] recorded (or the upload failed)
-  void mark(int bits) {
+  size_t queued[4] = {0, 0, 0, 0};  // chunks queued per group (all of them after an upload error)
+  size_t chunks(int grp) const { return (cols[grp] + kChunkCols - 1) / kChunkCols; }
+  size_t chunk_cols(int) const override { return kChunkCols; }
+  void mark(int grp, size_t n) {
     {
       std::lock_guard<std::mutex> lk(mu);
-      queued |= bits;
+      queued[grp] = n;
     }
     cv.notify_all();
   }
-  void wait(int grp, hipStream_t s) const override {
+  void mark_all() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      for (int i = 0; i < 4; i++) queued[i] = chunks(i);
+    }
+    cv.notify_all();
+  }
+  void wait(int grp, size_t col_end, hipStream_t s) const override {
+    const size_t need = (std::min(col_end, cols[grp]) + kChunkCols - 1) / kChunkCols;
+    if (need == 0) return;
     {
       std::unique_lock<std::mutex> lk(mu);
-      cv.wait(lk, [&] { return (queued >> grp) & 1; });
+      cv.wait(lk, [&] { return queued[grp] >= need; });
     }
-    HIP_OK(hipStreamWaitEvent(s, ev[grp], 0));
+    // one stream carries every copy in order: the last needed chunk's event covers the rest
+    HIP_OK(hipStreamWaitEvent(s, ev[grp][need - 1], 0));
   }
 };
 
@@ -114,14 +133,19 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
       std::vector<BufSet>& sets;
       ~Events() {
         for (auto& s : sets)
-          for (auto& e : s.ev)
-            if (e) (void)hipEventDestroy(e);
+          for (auto& v : s.ev)
+            for (auto e : v)
+              if (e) (void)hipEventDestroy(e);
       }
     } events{sets};
+    const size_t gcols[4] = {c->group_sizes[1], c->group_sizes[2], c->group_sizes[0], 1};
     for (auto& s : sets)
       for (int g = 0; g < 4; g++) {
         s.g[g] = DevBuf(words[g]);
-        HIP_OK(hipEventCreateWithFlags(&s.ev[g], hipEventDisableTiming));
+        s.cols[g] = std::max<size_t>(1, gcols[g]);
+        s.col_words[g] = g == 3 ? words[3] : n;
+        s.ev[g].assign(s.chunks(g), nullptr);
+        for (auto& e : s.ev[g]) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       }
     HIP_OK(hipDeviceSynchronize());  // allocations complete before other streams use them
     for (size_t i = 0; i < njobs; i++) {
@@ -139,7 +163,7 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
         b.job = i;
         {
           std::lock_guard<std::mutex> lk(b.mu);
-          b.queued = 0;  // the set is free: no prover waits on it
+          for (auto& q : b.queued) q = 0;  // the set is free: no prover waits on it
         }
         const uint32_t* src[4] = {jobs[i].h_code, jobs[i].h_data, jobs[i].h_accum, jobs[i].h_global};
         bool null_group = false;
@@ -147,24 +171,28 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
         if (null_group) jobs[i].error = dup_msg("witness group pointer is NULL");  // before the hand-over
         ready_q.put(s);  // a prover may start now; it waits per group (BufSet::wait)
         if (null_group) {
-          b.mark(15);
+          b.mark_all();
           continue;
         }
         try {
           ensure_init();
-          // in the order the prover first touches them (globals, code, data, accum), so a
-          // segment's code commit overlaps its data upload and its data commit the accum upload
+          // in the order the prover first touches them (globals, code, data, accum), each in
+          // column chunks, so a segment's commits run while its later columns still upload
           for (int g : {3, 0, 1, 2}) {
-            HIP_OK(hipMemcpyAsync(b.g[g].p, src[g], words[g] * 4, hipMemcpyHostToDevice, stream()));
-            HIP_OK(hipEventRecord(b.ev[g], stream()));
-            b.mark(1 << g);
+            for (size_t k = 0; k < b.chunks(g); k++) {
+              const size_t c0 = k * kChunkCols, cc = std::min(kChunkCols, b.cols[g] - c0);
+              HIP_OK(hipMemcpyAsync(b.g[g].p + c0 * b.col_words[g], src[g] + c0 * b.col_words[g],
+                                    cc * b.col_words[g] * 4, hipMemcpyHostToDevice, stream()));
+              HIP_OK(hipEventRecord(b.ev[g][k], stream()));
+              b.mark(g, k + 1);
+            }
           }
         } catch (const std::exception& e) {
           {
             std::lock_guard<std::mutex> lk(b.mu);
             if (!jobs[i].error) jobs[i].error = dup_msg(e.what());
           }
-          b.mark(15);  // release a waiting prover; the job reports the error
+          b.mark_all();  // release a waiting prover; the job reports the error
         }
       }
       for (size_t t = 0; t < k; t++) ready_q.put(-1);  // one stop token per prover

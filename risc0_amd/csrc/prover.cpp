@@ -89,9 +89,26 @@ struct MerkleTree {
   std::vector<uint32_t> top;  // nodes[top_size .. 2*top_size)
 
   void build(int suite, const uint32_t* m, size_t r, size_t c) {
+    DevBuf n(r * 2 * 8);
+    {
+      Span sp("commit");  // prove/merkle.rs:85
+      merkle_tree(stream(), suite, n.p, m, r, c);
+    }
+    finish(std::move(n), m, r, c);
+  }
+  // the leaves are already in leaf_nodes[r .. 2r) (hash_rows_range as the matrix arrived)
+  void build_from_leaves(int suite, DevBuf leaf_nodes, const uint32_t* m, size_t r, size_t c) {
+    {
+      Span sp("commit");
+      merkle_layers(stream(), suite, leaf_nodes.p, r);
+    }
+    finish(std::move(leaf_nodes), m, r, c);
+  }
+  void finish(DevBuf n, const uint32_t* m, size_t r, size_t c) {
     rows = r;
     cols = c;
     matrix = m;
+    nodes = std::move(n);
     layers = log2_exact(rows);
     size_t top_layer = 0;
     for (size_t i = 1; i < layers; i++) {
@@ -99,11 +116,6 @@ struct MerkleTree {
       top_layer = i;
     }
     top_size = size_t(1) << top_layer;
-    nodes = DevBuf(rows * 2 * 8);
-    {
-      Span sp("commit");  // prove/merkle.rs:85
-      merkle_tree(stream(), suite, nodes.p, m, rows, cols);
-    }
     // root (node 1) .. end of the top layer in one copy
     std::vector<uint32_t> h((2 * top_size - 1) * 8);
     d2h(h.data(), nodes.p + 8, h.size() * 4);
@@ -128,6 +140,11 @@ struct PolyGroup {
     ntt_evaluate(stream(), evaluated.p, coeffs.p, count, uint32_t(po2 + 2), 2);
     bit_reverse(stream(), coeffs.p, count, uint32_t(po2));
     tree.build(suite, evaluated.p, domain, count);
+  }
+  // coefficients (natural order), evaluations and leaf digests already made chunk by chunk
+  PolyGroup(int suite, DevBuf c, DevBuf ev, DevBuf leaf_nodes, size_t cnt, size_t po2)
+      : coeffs(std::move(c)), count(cnt), evaluated(std::move(ev)) {
+    tree.build_from_leaves(suite, std::move(leaf_nodes), evaluated.p, (size_t(1) << po2) * INV_RATE, count);
   }
 };
 
@@ -264,6 +281,30 @@ struct Prover {
   Prover(const CircuitDef& circ, int s, Profile* p) : c(circ), suite(s), iop(s), prof(p) {}
 
   // prover.rs:38-48 + 81-108; zk_shift fused into the interpolation's last pass
+  // A group still uploading in column chunks (the segment pipeline): each chunk's
+  // interpolate, evaluate, bit-reverse and leaf-hash range run as soon as it lands, so the
+  // group's NTTs and row hashes overlap its own upload. Same words as commit_group.
+  void commit_group_streamed(size_t g, int up_group, const uint32_t* witness, const UploadGate& up) {
+    Span span("commit_group");
+    hipStream_t s = stream();
+    const size_t gs = c.group_size(g), n = cycles, domain = n * INV_RATE, ch = up.chunk_cols(up_group);
+    DevBuf coeffs(gs * n), evaluated(gs * domain), nodes(domain * 2 * 8), state(domain * 8);
+    for (size_t c0 = 0; c0 < gs; c0 += ch) {
+      const size_t cc = std::min(ch, gs - c0);
+      up.wait(up_group, c0 + cc, s);
+      {
+        Span sp("make_coeffs");
+        ntt_interpolate_from(s, coeffs.p + c0 * n, witness + c0 * n, cc, uint32_t(po2), true);
+      }
+      ntt_evaluate(s, evaluated.p + c0 * domain, coeffs.p + c0 * n, cc, uint32_t(po2 + 2), 2);
+      bit_reverse(s, coeffs.p + c0 * n, cc, uint32_t(po2));
+      hash_rows_range(s, suite, nodes.p + domain * 8, state.p, evaluated.p + c0 * domain, domain, cc, c0 == 0,
+                      c0 + cc == gs);
+    }
+    groups[g].reset(new PolyGroup(suite, std::move(coeffs), std::move(evaluated), std::move(nodes), gs, po2));
+    groups[g]->tree.commit(iop);
+  }
+
   void commit_group(size_t g, const uint32_t* witness) {
     Span span("commit_group");
     size_t gs = c.group_size(g);
@@ -521,7 +562,7 @@ std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2
   Span span("prove_core");
   hipStream_t s = stream();
   auto gate = [&](int g) {
-    if (uploads) uploads->wait(g, s);
+    if (uploads) uploads->wait(g, SIZE_MAX, s);
   };
   stage_reset();
   Profile prof;
@@ -545,19 +586,26 @@ std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2
   p.iop.write(header.data(), header.size());
   p.po2 = po2;
   p.cycles = size_t(1) << po2;
-  gate(0);
-  p.commit_group(1, code);
+  // reference group index, pipeline buffer index (0 code, 1 data, 2 accum)
+  auto commit = [&](size_t g, int up_group, const uint32_t* w) {
+    const size_t gs = c.group_size(g);
+    if (uploads && suite != 2 && gs > uploads->chunk_cols(up_group) && uploads->chunk_cols(up_group) % 16 == 0) {
+      p.commit_group_streamed(g, up_group, w, *uploads);
+    } else {
+      gate(up_group);
+      p.commit_group(g, w);
+    }
+  };
+  commit(1, 0, code);
   prof.mark("commit_code");
-  gate(1);
-  p.commit_group(2, data);
+  commit(2, 1, data);
   prof.mark("commit_data");
   std::vector<uint32_t> mix(c.mix_size);
   for (auto& m : mix) m = p.iop.rng->random_elem();
   if (mix_out) *mix_out = mix;
   DevBuf dmix(mix.size() ? mix.size() : 1);
   upload_async(dmix.p, mix.data(), mix.size() * 4);
-  gate(2);
-  p.commit_group(0, accum);
+  commit(0, 2, accum);
   prof.mark("commit_accum");
   p.finalize(dmix.p, global);
   HIP_OK(hipStreamSynchronize(s));

@@ -81,11 +81,13 @@ struct Span {
   Span& operator=(const Span&) = delete;
 };
 
-// Witness groups that may still be uploading when a proof starts (the segment pipeline):
-// wait(g, s) returns once group g (0 code, 1 data, 2 accum, 3 global) has its copy queued,
-// with stream s made to wait for the copy on the device.
+// Witness groups that may still be uploading when a proof starts (the segment pipeline),
+// copied in column chunks of chunk_cols(g): wait(g, col_end, s) returns once columns
+// [0, col_end) of group g (0 code, 1 data, 2 accum, 3 global) have their copies queued,
+// with stream s made to wait for those copies on the device.
 struct UploadGate {
-  virtual void wait(int group, hipStream_t s) const = 0;
+  virtual void wait(int group, size_t col_end, hipStream_t s) const = 0;
+  virtual size_t chunk_cols(int group) const = 0;
  protected:
   ~UploadGate() = default;
 };
@@ -115,11 +117,19 @@ void ntt_interpolate_from(hipStream_t s, uint32_t* io, const uint32_t* src, size
 void bit_reverse(hipStream_t s, uint32_t* io, size_t count, uint32_t log_n);
 void zk_shift(hipStream_t s, uint32_t* io, size_t count, uint32_t log_n);
 
-// Hashes (poseidon2.hip / sha256.hip). suite: 0 = poseidon2, 1 = sha-256.
+// Hashes (hash.hip). suite: 0 = poseidon2, 1 = sha-256, 2 = poseidon254.
 void hash_rows(hipStream_t s, int suite, uint32_t* out, const uint32_t* matrix, size_t rows, size_t cols);
+// Row hashes over a matrix that arrives in column ranges: `cols` columns starting at
+// `chunk` (column-major, `rows` per column), continuing the per-row sponge held in `state`
+// (8 words per row) unless `first`; the `last` range writes the digests to `out`. Every
+// range but the last must hold a multiple of 16 columns. Poseidon2 and SHA-256 only.
+void hash_rows_range(hipStream_t s, int suite, uint32_t* out, uint32_t* state, const uint32_t* chunk, size_t rows,
+                     size_t cols, bool first, bool last);
 void hash_fold(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t output_size);
 // Full merkle tree: nodes[rows..2rows) = leaves, hashes every layer up to the root.
 void merkle_tree(hipStream_t s, int suite, uint32_t* nodes, const uint32_t* matrix, size_t rows, size_t cols);
+// The layers above leaves already in nodes[rows..2rows).
+void merkle_layers(hipStream_t s, int suite, uint32_t* nodes, size_t rows);
 
 // Element-wise and polynomial kernels (eltwise.hip).
 void eltwise_add(hipStream_t s, uint32_t* out, const uint32_t* a, const uint32_t* b, size_t n);

@@ -454,11 +454,12 @@ def test_prove_segment_from_pinned_host(oracle):
     assert [int(x) for x in mix] == case["mix"]
 
 
-def test_prove_segments_pipeline_golden(oracle):
+@pytest.mark.parametrize("case", G.INDEX["seals"], ids=lambda c: f"{c['circuit']}-{c['suite']}-po2{c['po2']}")
+def test_prove_segments_pipeline_golden(hal, hal_sha, oracle, case):
     """The native segment pipeline (r0hip_prove_segments): uploader + 2 provers over 5
-    jobs from host witnesses; every seal matches its golden fixture."""
+    jobs from host witnesses, groups of more than 48 columns committed chunk by chunk as
+    they upload (Poseidon2 / SHA-256); every seal matches its golden fixture."""
     import risc0_amd as r
-    case = G.INDEX["seals"][0]
     h = H(case["suite"])
     w = G.seal_inputs(oracle, case["circuit"], case["po2"])
     out = r.prove_segments(h, case["circuit"], case["po2"], [w] * 5,
@@ -467,6 +468,23 @@ def test_prove_segments_pipeline_golden(oracle):
     for seal, mix in out:
         assert G.digest(seal) == case["seal_sha256"]
         assert [int(x) for x in mix] == case["mix"]
+
+
+@pytest.mark.parametrize("circuit,suite,po2", [("rv32im", "poseidon2", 16), ("rv32im", "sha-256", 14),
+                                               ("recursion", "poseidon2", 14), ("rv32im", "poseidon2", 20)])
+def test_prove_segments_streamed_matches_resident(hal, hal_sha, oracle, circuit, suite, po2):
+    """A segment proved through the pipeline (chunked upload, streamed commits: interpolate,
+    evaluate, bit-reverse and row-hash ranges per 48-column chunk) gives the same seal as
+    the resident-witness prover on the same witness."""
+    import risc0_amd as r
+    h = H(suite)
+    w = G.seal_inputs(oracle, circuit, po2)
+    version = 2 if circuit == "rv32im" else None
+    seal, mix = r.prove_segment(h, circuit, po2, *(dev(h, a) for a in w), version=version)
+    out = r.prove_segments(h, circuit, po2, [w] * 2, version=version, in_flight=1)
+    for s2, m2 in out:
+        assert np.array_equal(m2, mix)
+        assert np.array_equal(s2, seal)
 
 
 def device_witness(h, n, seed):
