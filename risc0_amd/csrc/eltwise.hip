@@ -96,33 +96,46 @@ __global__ void copy_slice_kernel(uint32_t* into, const uint32_t* from, uint64_t
 
 // ---- mix_poly_coeffs (cpu.rs:410-455) ---------------------------------------------
 // out[combo*count + idx] += sum_{i: combos[i]==combo} mix_start*mix^i * in[i*count + idx]
-// One lane per idx streams all input rows (coalesced) and keeps one FpExt
-// accumulator per combo in VGPRs; combo ids are wave-uniform.
-constexpr int kMaxCombos = 8;
-template <int NC>
+// The host sorts the input rows by combo (rows[], with their mix powers in the same
+// order, and one segment per combo). One lane per idx streams its segment's rows with
+// coalesced loads, four in flight, into four unreduced u64 sums (one v_mad_u64_u32 per
+// product limb, folded every 3 products below 2^64), then one REDC per limb and one add
+// into the combo's FpExt: per product 4 multiply-adds instead of a canonical FpExt*Fp
+// multiply and add (32 instructions).
 __global__ __launch_bounds__(kThreads) void mix_kernel(uint32_t* out, const uint32_t* __restrict__ in,
-                                                      const uint32_t* __restrict__ combos,
-                                                      const uint32_t* __restrict__ pows,  // input_size FpExt
-                                                      uint32_t input_size, uint64_t count, uint32_t used_mask) {
-  uint64_t idx = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+                                                      const uint32_t* __restrict__ rows,
+                                                      const uint32_t* __restrict__ pows,  // FpExt per sorted row
+                                                      const uint32_t* __restrict__ seg,   // nseg + 1 bounds
+                                                      const uint32_t* __restrict__ seg_combo, uint32_t nseg,
+                                                      uint64_t count) {
+  const uint64_t idx = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (idx >= count) return;
-  FpExt acc[NC];
+  for (uint32_t sg = 0; sg < nseg; sg++) {
+    const uint32_t b = seg[sg], e = seg[sg + 1];
+    uint64_t a[4] = {0, 0, 0, 0};
+    uint32_t since_fold = 0;  // products added since the sums were last folded (< 2^58)
+    for (uint32_t j = b; j < e; j += 4) {
+      uint32_t v[4];
 #pragma unroll
-  for (int k = 0; k < NC; k++) acc[k] = fe_zero();
-  for (uint32_t i = 0; i < input_size; i++) {
-    uint32_t cid = combos[i];
-    FpExt mp = ld_fe(pows + 4 * i);
-    FpExt t = fe_mul_fp(mp, in[uint64_t(i) * count + idx]);
+      for (int u = 0; u < 4; u++) v[u] = j + u < e ? in[uint64_t(rows[j + u]) * count + idx] : 0u;
 #pragma unroll
-    for (int k = 0; k < NC; k++)
-      if (cid == uint32_t(k)) acc[k] = fe_add(acc[k], t);
-  }
+      for (int u = 0; u < 4; u++) {
+        if (since_fold == 3) {  // 2^58 + 3 p^2 < 2^64; one more product could pass it
 #pragma unroll
-  for (int k = 0; k < NC; k++) {
-    if (used_mask & (1u << k)) {
-      uint32_t* o = out + (uint64_t(k) * count + idx) * 4;
-      st_fe(o, fe_add(ld_fe(o), acc[k]));
+          for (int k = 0; k < 4; k++) a[k] = fold64(a[k]);
+          since_fold = 0;
+        }
+        const uint32_t* pw = pows + 4 * uint64_t(j + u < e ? j + u : b);
+#pragma unroll
+        for (int k = 0; k < 4; k++) a[k] += uint64_t(v[u]) * pw[k];
+        since_fold++;
+      }
     }
+    uint32_t* o = out + (uint64_t(seg_combo[sg]) * count + idx) * 4;
+    FpExt r;
+#pragma unroll
+    for (int k = 0; k < 4; k++) r.c[k] = mont_reduce(fold64(a[k]));
+    st_fe(o, fe_add(ld_fe(o), r));
   }
 }
 
@@ -487,19 +500,35 @@ void mix_poly_coeffs(hipStream_t s, uint32_t* out, const uint32_t* in, const uin
     used |= 1u << c;
     maxc = std::max(maxc, c);
   }
-  std::vector<uint32_t> pows(input_size * 4);
+  // rows sorted by combo id (stable), their mix powers mix_start * mix^i in that order
+  std::vector<uint32_t> rows, pows, seg{0}, seg_combo;
+  std::vector<FpExt> pw(input_size);
   FpExt cur = mix_start;
   for (size_t i = 0; i < input_size; i++) {
-    for (int k = 0; k < 4; k++) pows[4 * i + k] = cur.c[k];
+    pw[i] = cur;
     cur = fe_mul(cur, mix);
   }
-  uint32_t* dpows = static_cast<uint32_t*>(scratch(pows.size() * 4, 1));
-  upload_async(dpows, pows.data(), pows.size() * 4);
-  dim3 grid(div_up(count, kThreads));
-  if (maxc < 2) hipLaunchKernelGGL(mix_kernel<2>, grid, dim3(kThreads), 0, s, out, in, combos_dev, dpows, uint32_t(input_size), uint64_t(count), used);
-  else if (maxc < 4) hipLaunchKernelGGL(mix_kernel<4>, grid, dim3(kThreads), 0, s, out, in, combos_dev, dpows, uint32_t(input_size), uint64_t(count), used);
-  else if (maxc < kMaxCombos) hipLaunchKernelGGL(mix_kernel<kMaxCombos>, grid, dim3(kThreads), 0, s, out, in, combos_dev, dpows, uint32_t(input_size), uint64_t(count), used);
-  else R0_REQUIRE(false, "mix_poly_coeffs: more than 8 combos");
+  for (uint32_t k = 0; k <= maxc; k++) {
+    if (!(used >> k & 1)) continue;
+    for (size_t i = 0; i < input_size; i++) {
+      if (combos_host[i] != k) continue;
+      rows.push_back(uint32_t(i));
+      for (int w = 0; w < 4; w++) pows.push_back(pw[i].c[w]);
+    }
+    seg.push_back(uint32_t(rows.size()));
+    seg_combo.push_back(k);
+  }
+  (void)combos_dev;  // the device copy of the ids is the ABI's; the sorted tables replace it
+  uint32_t* d_rows = static_cast<uint32_t*>(scratch(rows.size() * 4, 40));
+  uint32_t* d_pows = static_cast<uint32_t*>(scratch(pows.size() * 4, 41));
+  uint32_t* d_seg = static_cast<uint32_t*>(scratch(seg.size() * 4, 42));
+  uint32_t* d_seg_combo = static_cast<uint32_t*>(scratch(seg_combo.size() * 4, 43));
+  upload_async(d_rows, rows.data(), rows.size() * 4);
+  upload_async(d_pows, pows.data(), pows.size() * 4);
+  upload_async(d_seg, seg.data(), seg.size() * 4);
+  upload_async(d_seg_combo, seg_combo.data(), seg_combo.size() * 4);
+  hipLaunchKernelGGL(mix_kernel, dim3(div_up(count, kThreads)), dim3(kThreads), 0, s, out, in, d_rows, d_pows,
+                     d_seg, d_seg_combo, uint32_t(seg_combo.size()), uint64_t(count));
   HIP_OK(hipGetLastError());
 }
 
