@@ -142,9 +142,12 @@ const char* r0hip_recursion_accum(const uint32_t* d_ctrl, const uint32_t* d_glob
 /* ---- segment pipeline (r0vm's per-GPU worker queue, r0vm/src/actors/worker.rs:75-76, over the
  * zkvm's per-segment prove loop, zkvm/src/host/server/prove/prover_impl.rs:84-94) ----
  * Proves njobs segments of one (circuit, suite, po2) from HOST witness buffers: an uploader
- * thread copies the next job's groups into one of in_flight+1 device buffer sets while
- * in_flight prover threads run r0hip_prove_segment's core on their own streams. Host
- * buffers should be page-locked (r0hip_host_alloc) for full PCIe rate. Per job: seal into
+ * thread copies each job's groups, in 48-column chunks, into one of in_flight+1 device buffer
+ * sets while in_flight prover threads run r0hip_prove_segment's core on their own streams; a
+ * prover starts a job at once and commits each group chunk by chunk as it lands (Poseidon2
+ * and SHA-256; Poseidon254 waits for whole groups). Seals equal r0hip_prove_segment's. Host
+ * buffers must stay valid until the call returns and should be page-locked
+ * (r0hip_host_alloc) for full PCIe rate. Per job: seal into
  * h_seal (seal_cap words), its length in seal_len, mix values into h_mix_out (optional),
  * and error = NULL or a malloc'd message (free() it). Returns NULL when every job succeeded. */
 typedef struct r0hip_segment_job {
