@@ -68,7 +68,14 @@ def main():
     import risc0_amd as r
     with open(os.path.join(ROOT, "risc0_amd", "circuits", args.circuit + ".taps.json")) as f:
         circ = json.load(f)
-    hal = r.HipHal(args.hashfn, device=local_rank)
+    device = local_rank
+    if os.environ.get("R0_BENCH_SHARE_GPUS") == "1":
+        # rehearsal of the N-rank path on fewer GPUs (tools/gpu_ranks.sh): ranks share the
+        # visible devices round-robin; never set for a measurement
+        import torch
+        device = local_rank % max(1, torch.cuda.device_count())
+        print(f"rank {rank}: R0_BENCH_SHARE_GPUS=1, device {device}", file=sys.stderr)
+    hal = r.HipHal(args.hashfn, device=device)
     version = 2 if args.circuit == "rv32im" else None
 
     # inputs resident in HBM before the timed region: one witness set per rank
