@@ -18,7 +18,11 @@ def main(d):
     cs = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Direction"].replace("MEMORY_COPY_", ""))
                 for r in csv.DictReader(open(cf)))
     big = [c for c in cs if c[1] - c[0] > 1e6]
-    base = big[-2][0]  # the last segment's data-group copy (then its accum copy)
+    # the last segment's copies: the last run of large copies with < 20 ms between them
+    first = len(big) - 1
+    while first > 0 and big[first][0] - big[first - 1][1] < 20e6:
+        first -= 1
+    base = big[first][0]
     for c in cs:
         if c[0] >= base - 1e6:
             print(f"copy {(c[0] - base) / 1e6:+8.2f} .. {(c[1] - base) / 1e6:+8.2f} ms  {c[2]}")
