@@ -280,6 +280,26 @@ def test_rv32im_accum_finalize(hal, oracle, po2, last):
     assert np.array_equal(d.to_numpy(), ref)
 
 
+@pytest.mark.parametrize("po2,last", [(10, 1024), (12, 3000), (14, 1 << 14)])
+def test_rv32im_accum_finalize_matches_reference(hal, po2, last):
+    """Phases 2-3 on the GPU against the compiled reference itself: the reference's phase-1
+    output (stepAccum on random data rows, accum allocated all-INVALID as the prover does)
+    finished by r0hip_rv32im_accum_finalize equals the reference's whole
+    risc0_circuit_rv32im_cpu_accum (ffi.cpp:313-368)."""
+    import rv32im_accum_ref as R
+    if not R.available():
+        pytest.skip("oracle/_ref/libref_rv32im_accum.so not built")
+    rows = 1 << po2
+    rng = np.random.default_rng(po2 * 7 + last)
+    draw = lambda n: rng.integers(0, R.P, n, dtype=np.uint64).astype(np.uint32)
+    data, glob, mix = draw(R.DATA_COLS * rows), draw(R.GLOBAL_WORDS), draw(R.MIX_WORDS)
+    p1 = R.accum(data, glob, mix, rows, last, phase1_only=True)
+    full = R.accum(data, glob, mix, rows, last)
+    d = dev(hal, p1)
+    hal.rv32im_accum_finalize(d, rows, R.ACCUM_COLS, last)
+    assert np.array_equal(d.to_numpy(), full)
+
+
 def test_combos_prepare_and_divide(hal, oracle):
     # hal/mod.rs:202-257: prepare, then divide by (x - z*w^-back); remainders must vanish.
     # Build combos whose rows have the required roots by construction.
