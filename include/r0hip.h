@@ -205,6 +205,10 @@ const char* r0hip_last_profile(char* buf, size_t cap);
  * reserved bytes, number of hipMalloc calls}. Peaks are since the last reset. Host-only. */
 const char* r0hip_mem_stats(uint64_t* out);
 const char* r0hip_mem_reset_peak(void);
+/* Release the idle device memory the library holds: the calling thread's free pool and
+ * the blocks exited threads left (pool and scratch). Blocks in use are untouched. For a
+ * caller switching segment sizes, and for tests that need a clean pool. */
+const char* r0hip_trim(void);
 
 #ifdef __cplusplus
 }

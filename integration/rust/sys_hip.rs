@@ -222,4 +222,5 @@ unsafe extern "C" {
     pub fn r0hip_last_profile(buf: *mut c_char, cap: usize) -> *const c_char;
     pub fn r0hip_mem_stats(out: *mut u64) -> *const c_char;
     pub fn r0hip_mem_reset_peak() -> *const c_char;
+    pub fn r0hip_trim() -> *const c_char;
 }

@@ -353,4 +353,8 @@ const char* r0hip_mem_reset_peak(void) {
   return wrap_nosync([&] { mem_reset_peak(); });
 }
 
+const char* r0hip_trim(void) {
+  return wrap([&] { dev_trim(); });
+}
+
 }  // extern "C"

@@ -89,6 +89,7 @@ def _declare(L):
         "r0hip_kernel_times": [C.c_char_p, sz],
         "r0hip_mem_stats": [C.POINTER(C.c_uint64)],
         "r0hip_mem_reset_peak": [],
+        "r0hip_trim": [],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -452,3 +453,8 @@ def mem_stats():
 
 def mem_reset_peak():
     check(lib().r0hip_mem_reset_peak())
+
+
+def trim():
+    """r0hip_trim: release idle pooled device memory (this thread's and exited threads')."""
+    check(lib().r0hip_trim())

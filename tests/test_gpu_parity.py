@@ -667,6 +667,9 @@ def test_steady_state_proving_makes_no_hipmalloc(oracle):
     globs = [dev(h, glob) for _ in range(2)]
     version = 2 if case["circuit"] == "rv32im" else None
     seals = {}
+    # start from a clean pool: blocks other tests' threads left (other sizes) would be
+    # matched up to 25% larger in whatever order threads race for them
+    r.trim()
 
     def batch(tag):
         def run(i):
