@@ -124,8 +124,17 @@ const char* r0hip_prove_segment(const char* circuit, int suite, uint32_t po2, co
  * stepAccum kernel, rv32im-sys/kernels/cuda/ffi.cu:480-509; CPU ffi.cpp:326-360): inclusive
  * prefix sums of the last 4 accum columns over rows [0, last_cycle), then every row adds the
  * previous row's prefix values to the machine columns [23, cols - 4). d_accum is the accum
- * group, column-major with `rows` rows (the per-cycle stepAccum phase stays the caller's). */
+ * group, column-major with `rows` rows, after the per-cycle phase (r0hip_rv32im_accum runs both). */
 const char* r0hip_rv32im_accum_finalize(uint32_t* d_accum, size_t rows, size_t cols, size_t last_cycle);
+/* ---- rv32im witness side: the whole accumulation (risc0_circuit_rv32im_cuda_accum,
+ * rv32im-sys/kernels/cuda/ffi.cu:362-514; CPU risc0_circuit_rv32im_cpu_accum, ffi.cpp:313-368):
+ * phase 1, the per-cycle accumulation step (stepAccum, ffi.cpp:238-247, generated from the
+ * reference's step_TopAccum), for cycles [0, last_cycle), then phases 2-3 as above. d_data is
+ * the data group (211 columns), d_accum the accum group (cols = 103) as the prover allocates
+ * it (every word INVALID, 0xFFFFFFFF); d_global (90 words) and d_mix (36 words) as in
+ * AccumBuffers (witgen.h). Columns are `rows` long. */
+const char* r0hip_rv32im_accum(const uint32_t* d_data, uint32_t* d_accum, const uint32_t* d_global,
+                               const uint32_t* d_mix, size_t rows, size_t cols, size_t last_cycle);
 
 /* ---- recursion witness side: the accumulation step (risc0_circuit_recursion_cuda_accum,
  * recursion-sys/kernels/cuda/ffi.cu; CPU driver recursion-sys/kernels/cxx/ffi.cpp:160-217,

@@ -152,6 +152,15 @@ unsafe extern "C" {
     ) -> *const c_char;
     pub fn r0hip_rv32im_accum_finalize(d_accum: *mut u32, rows: usize, cols: usize, last_cycle: usize)
         -> *const c_char;
+    pub fn r0hip_rv32im_accum(
+        d_data: *const u32,
+        d_accum: *mut u32,
+        d_global: *const u32,
+        d_mix: *const u32,
+        rows: usize,
+        cols: usize,
+        last_cycle: usize,
+    ) -> *const c_char;
     pub fn r0hip_recursion_accum(
         d_ctrl: *const u32,
         d_global: *const u32,

@@ -10,6 +10,7 @@
 // consecutive rows; every load and store is a coalesced 64-byte-per-lane run.
 #include "bb31.h"
 #include "devmem.h"
+#include "accum_gen.h"
 #include "runtime.h"
 
 namespace r0 {
@@ -108,6 +109,32 @@ __global__ __launch_bounds__(kT) void finalize_kernel(uint32_t* accum, uint64_t 
 }
 
 }  // namespace
+
+// The whole accumulation (risc0_circuit_rv32im_cuda_accum, rv32im-sys/kernels/cuda/ffi.cu:
+// 362-514; CPU ffi.cpp:313-368): phase 1 runs the per-cycle step generated from
+// risc0_amd/circuits/rv32im.accum.ir (tools/gen_rv32im_accum_ir.py -> tools/gen_accum.py;
+// one lane per cycle, its stores guarded by the instruction arm the cycle selects), then
+// phases 2-3 above. `accum` arrives as the prover allocates it (INVALID words).
+void rv32im_accum(hipStream_t s, const uint32_t* data, uint32_t* accum, const uint32_t* global,
+                  const uint32_t* mix, size_t rows, size_t cols, size_t last) {
+  R0_REQUIRE(rows >= 4 && (rows & (rows - 1)) == 0 && rows <= (size_t(1) << 26),
+             "rv32im_accum: rows must be a power of two in [4, 2^26]");
+  R0_REQUIRE(last <= rows, "rv32im_accum: last_cycle > rows");
+  R0_REQUIRE(cols == 103, "rv32im_accum: the rv32im accum group has 103 columns");
+  if (last == 0) return;
+  {
+    KScope ks("accum_step", double(last) * 4 * (211 + 2 * 103));
+    AccArgs A{};
+    A.a[0] = const_cast<uint32_t*>(data);
+    A.a[1] = accum;
+    A.a[2] = const_cast<uint32_t*>(global);
+    A.a[3] = const_cast<uint32_t*>(mix);
+    A.steps = uint32_t(last);
+    A.cycles = uint32_t(rows);
+    rv32im_accum_compute(s, A);
+  }
+  rv32im_accum_finalize(s, accum, rows, cols, 23, last);
+}
 
 void rv32im_accum_finalize(hipStream_t s, uint32_t* accum, size_t rows, size_t cols, size_t split, size_t last) {
   R0_REQUIRE(cols >= 4 && split <= cols - 4 && last <= rows, "accum_finalize: bad shape");

@@ -254,6 +254,10 @@ const char* r0hip_rv32im_accum_finalize(uint32_t* d_accum, size_t rows, size_t c
   // layout.cpp.inc:6993-6999): the first machine accumulator column
   return wrap([&] { rv32im_accum_finalize(stream(), d_accum, rows, cols, 23, last_cycle); });
 }
+const char* r0hip_rv32im_accum(const uint32_t* d_data, uint32_t* d_accum, const uint32_t* d_global,
+                               const uint32_t* d_mix, size_t rows, size_t cols, size_t last_cycle) {
+  return wrap([&] { rv32im_accum(stream(), d_data, d_accum, d_global, d_mix, rows, cols, last_cycle); });
+}
 const char* r0hip_recursion_accum(const uint32_t* d_ctrl, const uint32_t* d_global, const uint32_t* d_data,
                                   const uint32_t* d_mix, uint32_t* d_accum, size_t work_cycles,
                                   size_t total_cycles) {

@@ -126,7 +126,7 @@ void recursion_accum(hipStream_t s, const uint32_t* ctrl, const uint32_t* global
   uint4* prods = static_cast<uint4*>(scratch(size_t(ntiles) * 16, 61));
   hipLaunchKernelGGL(fill_one_kernel, dim3(div_up(steps, kT)), dim3(kT), 0, s, vals, uint64_t(steps));
   HIP_OK(hipGetLastError());
-  rec_accum::AccArgs A;
+  AccArgs A;
   A.a[0] = const_cast<uint32_t*>(ctrl);
   A.a[1] = const_cast<uint32_t*>(global);
   A.a[2] = const_cast<uint32_t*>(data);

@@ -137,6 +137,8 @@ void eltwise_copy(hipStream_t s, uint32_t* out, const uint32_t* in, size_t n);
 void eltwise_zeroize(hipStream_t s, uint32_t* io, size_t n);
 void fill_uniform(hipStream_t s, uint32_t* out, size_t n, uint64_t seed);
 void rv32im_accum_finalize(hipStream_t s, uint32_t* accum, size_t rows, size_t cols, size_t split, size_t last);
+void rv32im_accum(hipStream_t s, const uint32_t* data, uint32_t* accum, const uint32_t* global,
+                  const uint32_t* mix, size_t rows, size_t cols, size_t last);
 // recursion circuit accumulation (recursion_accum.hip): compute, prefix product, verify
 void recursion_accum(hipStream_t s, const uint32_t* ctrl, const uint32_t* global, const uint32_t* data,
                      const uint32_t* mix, uint32_t* accum, size_t steps, size_t cycles);

@@ -55,6 +55,7 @@ def _declare(L):
         "r0hip_host_free": [vp],
         "r0hip_fill_uniform": [vp, sz, C.c_uint64],
         "r0hip_rv32im_accum_finalize": [vp, sz, sz, sz],
+        "r0hip_rv32im_accum": [vp, vp, vp, vp, sz, sz, sz],
         "r0hip_recursion_accum": [vp, vp, vp, vp, vp, sz, sz],
         "r0hip_prove_segments": [C.c_char_p, C.c_int, C.c_uint32, C.c_int, C.c_uint32, C.c_void_p, sz, C.c_uint32],
         "r0hip_verify_seal": [C.c_char_p, C.c_int, u32p, sz, u32p, sz, u32p, C.POINTER(C.c_uint32)],
@@ -294,6 +295,11 @@ class HipHal:
     def rv32im_accum_finalize(self, accum, rows, cols, last_cycle):
         """accumulation phases 2-3 of risc0_circuit_rv32im_cuda_accum (ffi.cu:480-509)"""
         check(lib().r0hip_rv32im_accum_finalize(accum.ptr, rows, cols, last_cycle))
+
+    def rv32im_accum(self, data, accum, glob, mix, rows, last_cycle):
+        """the whole rv32im accumulation, phases 1-3 (risc0_circuit_rv32im_cuda_accum,
+        ffi.cu:362-514): `accum` (103 columns of `rows`) starts all-INVALID"""
+        check(lib().r0hip_rv32im_accum(data.ptr, accum.ptr, glob.ptr, mix.ptr, rows, 103, last_cycle))
 
     def recursion_accum(self, ctrl, glob, data, mix, accum, work_cycles, total_cycles):
         """CircuitAccumulator::accumulate of the recursion circuit (witgen.rs:162-170 ->

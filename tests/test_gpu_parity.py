@@ -300,6 +300,29 @@ def test_rv32im_accum_finalize_matches_reference(hal, po2, last):
     assert np.array_equal(d.to_numpy(), full)
 
 
+@pytest.mark.parametrize("po2,last", [(10, 1024), (12, 3000), (20, 1 << 20)])
+def test_rv32im_accum_matches_reference(hal, po2, last):
+    """The whole rv32im accumulation on the GPU (r0hip_rv32im_accum: the generated
+    per-cycle step, then the scan and finalize) against the compiled reference's
+    risc0_circuit_rv32im_cpu_accum (ffi.cpp:313-368) on random data rows, each taking one of
+    the 13 instruction arms (tests/test_rv32im_accum_ir.py:rows_for_arms)."""
+    import rv32im_accum_ref as R
+    from test_rv32im_accum_ir import rows_for_arms
+    if not R.available():
+        pytest.skip("oracle/_ref/libref_rv32im_accum.so not built")
+    rows = 1 << po2
+    rng = np.random.default_rng(po2 * 31 + last)
+    data = rows_for_arms(rng, rows, list(rng.integers(0, 13, rows)))
+    glob = rng.integers(0, R.P, R.GLOBAL_WORDS, dtype=np.uint64).astype(np.uint32)
+    mix = rng.integers(0, R.P, R.MIX_WORDS, dtype=np.uint64).astype(np.uint32)
+    ref = R.accum(data, glob, mix, rows, last)
+    d_acc = dev(hal, np.full(R.ACCUM_COLS * rows, R.INVALID, np.uint32))
+    hal.rv32im_accum(dev(hal, data), d_acc, dev(hal, glob), dev(hal, mix), rows, last)
+    got = d_acc.to_numpy()
+    bad = np.nonzero(got != ref)[0]
+    assert bad.size == 0, f"{bad.size} words differ, first at column {bad[0] // rows} row {bad[0] % rows}"
+
+
 def test_combos_prepare_and_divide(hal, oracle):
     # hal/mod.rs:202-257: prepare, then divide by (x - z*w^-back); remainders must vanish.
     # Build combos whose rows have the required roots by construction.

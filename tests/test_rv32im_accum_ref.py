@@ -44,3 +44,14 @@ def test_zero_rows_stop_at_an_unreachable_mux_arm():
             "np.zeros(R.MIX_WORDS, np.uint32), 16, 16, phase1_only=True)") % __import__("os").path.dirname(__file__)
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "unreachable mux arm" in r.stderr
+
+
+def test_reference_accum_rate():
+    """the compiled reference's whole accumulation at 2^14 rows (sizes the GPU parity test)"""
+    import time
+    rows = 1 << 14
+    rng = np.random.default_rng(5)
+    data, glob, mix = inputs(rows, 5)
+    t = time.perf_counter()
+    R.accum(data, glob, mix, rows, rows)
+    print(f"reference rv32im cpu_accum: {rows / (time.perf_counter() - t):.0f} rows/s")

@@ -1,20 +1,22 @@
 #!/usr/bin/env python3
-"""Emit the gfx950 kernels of the recursion circuit's accumulation step from its block IR
-(risc0_amd/circuits/recursion.accum.ir, tools/gen_accum_ir.py):
+"""Emit the gfx950 kernels of a circuit's accumulation step from its block IR:
 
-  compute : per cycle, the accumulator factor (recursion-sys step_compute_accum.cpp)
-  verify  : per cycle, the accum-group registers from the prefix product
-            (recursion-sys step_verify_accum.cpp)
+  recursion (risc0_amd/circuits/recursion.accum.ir, tools/gen_accum_ir.py):
+    compute : per cycle, the accumulator factor (recursion-sys step_compute_accum.cpp)
+    verify  : per cycle, the accum-group registers from the prefix product
+              (recursion-sys step_verify_accum.cpp)
+  rv32im (risc0_amd/circuits/rv32im.accum.ir, tools/gen_rv32im_accum_ir.py):
+    compute : per cycle, phase 1 of the accumulation (rv32im-sys steps.cpp step_TopAccum)
 
 One lane per cycle, values are canonical Montgomery words in VGPRs, `if (x != 0)` blocks
-stay branches (the control columns are one-hot per cycle, so a wave takes a few arms).
+stay branches (selectors are one-hot per cycle, so a wave takes a few arms).
 Each function is cut into kernels of at most LIMIT operations along its block structure:
 a piece re-evaluates the pure definitions it uses from enclosing blocks (loads, constants,
 arithmetic) and runs under the conjunction of its enclosing guards. Pieces run in program
 order, so every register write of a cycle lands in the order the reference makes it.
 
-  gen_accum.py OUTDIR [LIMIT]
-Writes OUTDIR/accum_k<i>.hip and OUTDIR/accum.hip (launchers of both functions).
+  gen_accum.py CIRCUIT OUTDIR [LIMIT]
+Writes OUTDIR/accum_k<i>.hip and OUTDIR/accum.hip (launchers of the functions).
 """
 import os
 import sys
@@ -23,9 +25,9 @@ ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 P = 15 * 2**27 + 1
 
 
-def load():
+def load(circuit):
     fns, cur = {}, None
-    for line in open(os.path.join(ROOT, "risc0_amd", "circuits", "recursion.accum.ir")):
+    for line in open(os.path.join(ROOT, "risc0_amd", "circuits", circuit + ".accum.ir")):
         if line.startswith("#") or not line.strip():
             continue
         t = line.split()
@@ -77,7 +79,7 @@ def chunks(children, guards, limit, out):
         out.append((guards, cur))
 
 
-DEFS = {"c", "l", "g", "+", "-", "*", "n", "i", "ra"}
+DEFS = {"c", "l", "g", "+", "-", "*", "n", "i", "z", "ra"}
 
 
 def defined(ins):
@@ -90,7 +92,7 @@ def used(ins):
     op = ins[0]
     if op in "+-*":
         return [ins[2], ins[3]]
-    if op in ("n", "i"):
+    if op in ("n", "i", "z"):
         return [ins[2]]
     if op == "w":
         return [ins[3]]
@@ -159,6 +161,8 @@ def emit_fn(name, prog, limit, kbase):
                 w(f"{ind}const uint32_t v{ins[1]} = fp_neg(v{ins[2]});")
             elif op == "i":
                 w(f"{ind}const uint32_t v{ins[1]} = fp_inv(v{ins[2]});")
+            elif op == "z":
+                w(f"{ind}const uint32_t v{ins[1]} = v{ins[2]} == 0u ? kOne : 0u;")
             elif op == "ra":
                 w(f"{ind}const uint4 r{ins[1]} = A.vals[cycle];")
                 for k, c in enumerate("xyzw"):
@@ -192,21 +196,28 @@ def emit_fn(name, prog, limit, kbase):
     return kernels
 
 
-HEAD = """// GENERATED by tools/gen_accum.py from risc0_amd/circuits/recursion.accum.ir — do not edit.
-#include "accum_gen.h"
-namespace r0 {
-namespace rec_accum {
-"""
+CIRCUITS = {  # namespace, functions in launch order, launcher prefix
+    "recursion": ("rec_accum", ("compute", "verify"), "recursion_accum_"),
+    "rv32im": ("rv_accum", ("compute",), "rv32im_accum_"),
+}
+
+
+def head(circuit):
+    ns = CIRCUITS[circuit][0]
+    return (f"// GENERATED by tools/gen_accum.py from risc0_amd/circuits/{circuit}.accum.ir — do not edit.\n"
+            f"#include \"accum_gen.h\"\nnamespace r0 {{\nnamespace {ns} {{\n")
 
 
 def main():
-    outdir = sys.argv[1]
-    limit = int(sys.argv[2]) if len(sys.argv) > 2 else 1200
-    fns = load()
+    circuit, outdir = sys.argv[1], sys.argv[2]
+    limit = int(sys.argv[3]) if len(sys.argv) > 3 else 1200
+    ns, names, prefix = CIRCUITS[circuit]
+    HEAD = head(circuit)
+    fns = load(circuit)
     os.makedirs(outdir, exist_ok=True)
     launch = {}
     k = 0
-    for name in ("compute", "verify"):
+    for name in names:
         launch[name] = []
         for L in emit_fn(name, fns[name], limit, k):
             src = [HEAD, f"__global__ __launch_bounds__(256) void k{k}(AccArgs A) {{",
@@ -216,7 +227,7 @@ def main():
             src += L
             src += ["}", f"void launch_k{k}(hipStream_t s, const AccArgs& A) {{",
                     f"  hipLaunchKernelGGL(k{k}, dim3(div_up(A.steps, 256)), dim3(256), 0, s, A);",
-                    "  HIP_OK(hipGetLastError());", "}", "}  // namespace rec_accum", "}  // namespace r0"]
+                    "  HIP_OK(hipGetLastError());", "}", f"}}  // namespace {ns}", "}  // namespace r0"]
             with open(os.path.join(outdir, f"accum_k{k}.hip"), "w") as f:
                 f.write("\n".join(src) + "\n")
             launch[name].append(k)
@@ -224,16 +235,16 @@ def main():
     L = [HEAD]
     for i in range(k):
         L.append(f"void launch_k{i}(hipStream_t s, const AccArgs& A);")
-    L.append("}  // namespace rec_accum")
-    for name in ("compute", "verify"):
-        L.append(f"void recursion_accum_{name}(hipStream_t s, const rec_accum::AccArgs& A) {{")
+    L.append(f"}}  // namespace {ns}")
+    for name in names:
+        L.append(f"void {prefix}{name}(hipStream_t s, const AccArgs& A) {{")
         for i in launch[name]:
-            L.append(f"  rec_accum::launch_k{i}(s, A);")
+            L.append(f"  {ns}::launch_k{i}(s, A);")
         L.append("}")
     L.append("}  // namespace r0")
     with open(os.path.join(outdir, "accum.hip"), "w") as f:
         f.write("\n".join(L) + "\n")
-    print(f"recursion accum: {len(launch['compute'])} compute + {len(launch['verify'])} verify kernels")
+    print(f"{circuit} accum: " + " + ".join(f"{len(launch[n])} {n}" for n in names) + " kernels")
 
 
 if __name__ == "__main__":

@@ -20,7 +20,9 @@ symbolically, inlining every call:
   * a load of a location stored earlier in the same cycle returns the stored value; loads
     of machine accum columns (col >= kUserAccumSplit) at back > 0 read 0, as the
     reference's MutableBufObj(accum, zeroBack) does (ffi.cpp:243);
-  * values feeding only checks are dropped (dead-code elimination from the stores).
+  * values feeding only checks are dropped (dead-code elimination from the stores), and
+    the arms' pure definitions are hoisted out of their `if` blocks (the merged values are
+    used after the mux), so the blocks hold only stores.
 
 IR (one statement per line; buffers: 0 data, 1 accum, 2 global, 3 mix):
   c ID VALUE | l ID BUF COL BACK | g ID BUF IDX | + - * ID A B | n ID A | i ID A (inv, 0 -> 0)
@@ -738,6 +740,30 @@ def dce(ops):
     return res
 
 
+def hoist(ops):
+    """move every pure definition made inside a mux arm in front of the arm's outermost
+    `if` (order kept): arm values are merged after the mux, so they must be in scope
+    there; only the stores stay guarded"""
+    out, held, depth, pos = [], [], 0, 0
+    for op in ops:
+        if op[0] == "if":
+            if depth == 0:
+                pos = len(out)
+            depth += 1
+            out.append(op)
+        elif op[0] == "end":
+            depth -= 1
+            out.append(op)
+            if depth == 0 and held:
+                out[pos:pos] = held
+                held = []
+        elif op[0] == "w" or depth == 0:
+            out.append(op)
+        else:
+            held.append(op)
+    return out
+
+
 def main():
     ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
     steps = open(f"{ref}/{SRC}steps.cpp").read()
@@ -748,7 +774,7 @@ def main():
     ctx = Ctx(funcs, lay, split)
     ev = Ev(ctx)
     ev.call(funcs["step_TopAccum"], ["accum", "data", "global", "mix"])
-    ops = dce(ctx.ir.ops)
+    ops = dce(hoist(ctx.ir.ops))
     print("# rv32im accumulation step (phase 1) flattened by tools/gen_rv32im_accum_ir.py from the reference's")
     print("# rv32im-sys/kernels/cxx/steps.cpp step_TopAccum; buffers 0 data, 1 accum, 2 global, 3 mix")
     print(f"# kUserAccumSplit {split}")
