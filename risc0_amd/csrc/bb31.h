@@ -70,7 +70,21 @@ R0_HD uint32_t fp_pow(uint32_t x, uint64_t n) {
   }
   return tot;
 }
-R0_HD uint32_t fp_inv(uint32_t x) { return fp_pow(x, kP - 2); }
+// x^(p-2) (inv(0) = 0): p - 2 = 0x77FFFFFF = 0b1110111 then 24 ones, so x^7, then
+// x^119 = (x^7)^16 * x^7, then eight 3-bit windows r = r^8 * x^7: 30 squarings and 11
+// multiplies instead of square-and-multiply's 31 + 30
+R0_HD uint32_t fp_inv(uint32_t x) {
+  const uint32_t x2 = fp_mul(x, x), x3 = fp_mul(x2, x), x7 = fp_mul(fp_mul(x3, x3), x);
+  uint32_t r = x7;
+  for (int i = 0; i < 4; i++) r = fp_mul(r, r);
+  r = fp_mul(r, x7);
+  for (int w = 0; w < 8; w++) {
+    r = fp_mul(r, r);
+    r = fp_mul(r, r);
+    r = fp_mul(fp_mul(r, r), x7);
+  }
+  return r;
+}
 
 struct FpExt {
   uint32_t c[4];
