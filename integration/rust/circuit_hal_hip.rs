@@ -20,12 +20,12 @@
 use std::{ffi::CString, rc::Rc};
 
 use anyhow::Result;
-use risc0_circuit_rv32im_sys::{
-    RawAccumBuffers, RawBuffer, RawExecBuffers, RawPreflightTrace, risc0_circuit_rv32im_cpu_accum,
-    risc0_circuit_rv32im_cpu_witgen,
-};
+use risc0_circuit_rv32im_sys::{RawBuffer, RawExecBuffers, RawPreflightTrace, risc0_circuit_rv32im_cpu_witgen};
 use risc0_core::{field::ExtElem as _, scope};
-use risc0_sys::{ffi_wrap, hip::r0hip_eval_check};
+use risc0_sys::{
+    ffi_wrap,
+    hip::{r0hip_eval_check, r0hip_rv32im_accum},
+};
 use risc0_zkp::hal::{
     AccumPreflight, Buffer, CircuitHal,
     hip::{BufferImpl as HipBuffer, HipHal, HipHash, HipHashPoseidon2},
@@ -115,14 +115,22 @@ impl<HS: HipHash> CircuitAccumulator<HipHal<HS>> for HipCircuitHal<HS> {
     ) -> Result<()> {
         scope!("accumulate");
         let cycles = preflight.cycles.len();
-        let (d, a, g, m) = (HostRows::of(data), HostRows::of(accum), HostRows::of(global), HostRows::of(mix));
-        let buffers = RawAccumBuffers { data: d.raw(), accum: a.raw(), global: g.raw(), mix: m.raw() };
-        let pf = raw_preflight(preflight);
-        // all three phases of ffi.cpp:262-368 on the host (phases 2-3 alone also exist on
-        // the device: r0hip_rv32im_accum_finalize)
-        ffi_wrap(|| unsafe { risc0_circuit_rv32im_cpu_accum(&buffers, &pf, cycles as u32) })?;
-        a.store(accum);
-        Ok(())
+        // all three phases of risc0_circuit_rv32im_cuda_accum (ffi.cu:362-514) on the device:
+        // the per-cycle stepAccum generated from the reference's step_TopAccum, the scan and
+        // finalizeAccum. `accum` arrives INVALID-filled as the CUDA HAL allocates it; the
+        // accumulation step reads no preflight data.
+        assert_eq!(accum.rows, data.rows);
+        ffi_wrap(|| unsafe {
+            r0hip_rv32im_accum(
+                data.buf.dev(),
+                accum.buf.dev(),
+                global.buf.dev(),
+                mix.buf.dev(),
+                accum.rows,
+                accum.cols,
+                cycles,
+            )
+        })
     }
 }
 
