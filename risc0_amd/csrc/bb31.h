@@ -86,6 +86,28 @@ R0_HD uint32_t fp_inv(uint32_t x) {
   return r;
 }
 
+// x[i] <- x[i]^-1 for N independent values (inv(0) = 0, as fp_inv): Montgomery's trick, one
+// addition chain and 3(N-1) multiplies; zeros enter the running product as one
+template <int N>
+R0_HD void fp_inv_batch(uint32_t (&x)[N]) {
+  uint32_t pre[N];
+  uint32_t acc = x[0] == 0u ? kOne : x[0];
+#pragma unroll
+  for (int i = 1; i < N; i++) {
+    pre[i] = acc;
+    acc = fp_mul(acc, x[i] == 0u ? kOne : x[i]);
+  }
+  uint32_t inv = fp_inv(acc);
+#pragma unroll
+  for (int i = N - 1; i > 0; i--) {
+    const uint32_t xi = x[i];
+    const uint32_t o = fp_mul(inv, pre[i]);
+    inv = fp_mul(inv, xi == 0u ? kOne : xi);
+    x[i] = xi == 0u ? 0u : o;
+  }
+  x[0] = x[0] == 0u ? 0u : inv;
+}
+
 struct FpExt {
   uint32_t c[4];
 };

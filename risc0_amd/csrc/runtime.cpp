@@ -180,8 +180,13 @@ void* scratch(size_t bytes, int slot) {
   Scratch& s = t_ctx.scratch[slot];
   if (s.bytes < bytes) {
     if (s.p) {
-      HIP_OK(hipStreamSynchronize(t_ctx.stream));  // last user of the old block must be done
-      counted_free(s.p, s.bytes);
+      // the last user of the old block must be done; the block goes back to the slot's
+      // orphans (some slots hold data-dependent sizes, e.g. upload vectors, so a thread that
+      // took another thread's smaller leftover grows here; freeing it would make the next
+      // thread hipMalloc again). dev_trim releases orphans under memory pressure.
+      HIP_OK(hipStreamSynchronize(t_ctx.stream));
+      std::lock_guard<std::mutex> lk(g_mu);
+      g_scratch_orphans[slot].emplace(s.bytes, s.p);
       live_sub(s.bytes);
     }
     size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;

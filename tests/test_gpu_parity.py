@@ -703,7 +703,11 @@ def test_steady_state_proving_makes_no_hipmalloc(oracle):
         for t in ts:
             t.join()
 
+    # two warm batches: per-proof upload sizes differ between the two seals, so the first
+    # steady thread to reach a slot may take the other thread's block; after both threads
+    # have left blocks of both patterns the pool covers either order
     batch("warm")
+    batch("warm2")
     r.mem_reset_peak()
     before = r.mem_stats()
     batch("steady")

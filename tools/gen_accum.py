@@ -15,7 +15,7 @@ a piece re-evaluates the pure definitions it uses from enclosing blocks (loads, 
 arithmetic) and runs under the conjunction of its enclosing guards. Pieces run in program
 order, so every register write of a cycle lands in the order the reference makes it.
 
-  gen_accum.py CIRCUIT OUTDIR [LIMIT]
+  gen_accum.py CIRCUIT OUTDIR [LIMIT [INV_BATCH]]
 Writes OUTDIR/accum_k<i>.hip and OUTDIR/accum.hip (launchers of the functions).
 """
 import os
@@ -111,7 +111,72 @@ def flat(nodes):
             yield ("end",)
 
 
-def emit_fn(name, prog, limit, kbase):
+def batch_inverses(run, width, written=()):
+    """Reorder one straight-line run of a kernel (its prelude, or the statements between two
+    control markers of its body) so its field inverses run in batches of `width`
+    (Montgomery's trick, fp_inv_batch: 3 multiplies per inverse plus one addition chain
+    instead of 41 multiplies each). An inverse's level is the number of inverses on its
+    longest input path within the run; the inverses of one level are independent, so each
+    batch is preceded by the not-yet-emitted cone of its inputs and followed by whatever is
+    left, in program order. Only definitions move, and only earlier; a batch whose cone
+    would lift a load of a `written` array (or a vals read) above a store of the run is not
+    formed. Returns the run with ("ib", [(out, in), ...]) pseudo-ops."""
+    if width <= 1 or sum(ins[0] == "i" for ins in run) < 2:
+        return run
+    by_val = {d: ins for ins in run for d in defined(ins)}
+    pos = {id(ins): k for k, ins in enumerate(run)}
+    first_store = next((k for k, ins in enumerate(run) if ins[0] in ("w", "wa")), len(run))
+
+    def pinned(ins):
+        return pos[id(ins)] > first_store and (ins[0] == "ra" or (ins[0] == "l" and ins[2] in written))
+
+    level = {}
+    for ins in run:
+        lv = max((level.get(u, 0) for u in used(ins)), default=0)
+        for d in defined(ins):
+            level[d] = lv + (1 if ins[0] == "i" else 0)
+    invs = [ins for ins in run if ins[0] == "i"]
+    groups = []
+    for lv in sorted(set(level[i[1]] for i in invs)):
+        same = [i for i in invs if level[i[1]] == lv]
+        groups += [same[k:k + width] for k in range(0, len(same), width)]
+    done, out = set(), []
+    for g in groups:
+        if len(g) == 1:
+            continue
+        cone, stack = {}, [i[2] for i in g]
+        while stack:
+            v = stack.pop()
+            ins = by_val.get(v)
+            if ins is None or id(ins) in done or id(ins) in cone:
+                continue
+            cone[id(ins)] = ins
+            stack += used(ins)
+        if any(pinned(ins) for ins in cone.values()):
+            continue
+        for ins in sorted(cone.values(), key=lambda i: pos[id(i)]):
+            out.append(ins)
+            done.add(id(ins))
+        out.append(("ib", [(i[1], i[2]) for i in g]))
+        done.update(id(i) for i in g)
+    out += [ins for ins in run if id(ins) not in done]
+    return out
+
+
+def batch_body(body, width, written):
+    """batch_inverses over every straight-line run of a kernel body"""
+    out, run = [], []
+    for ins in body + [("end",)]:
+        if ins[0] in ("if", "end"):
+            out += batch_inverses(run, width, written)
+            run = []
+            out.append(ins)
+        else:
+            run.append(ins)
+    return out[:-1]
+
+
+def emit_fn(name, prog, limit, kbase, inv_batch=1):
     defs = {}
     order = {}
     for pos, ins in enumerate(prog):
@@ -140,7 +205,8 @@ def emit_fn(name, prog, limit, kbase):
                 continue
             pre[id(ins)] = ins
             stack += [u for u in used(ins) if u not in have]
-        pre = sorted(pre.values(), key=lambda i: order[id(i)])
+        pre = batch_inverses(sorted(pre.values(), key=lambda i: order[id(i)]), inv_batch)
+        body = batch_body(body, inv_batch, {ins[1] for ins in body if ins[0] == "w"})
         L = []
         w = L.append
         ind = "  "
@@ -163,6 +229,13 @@ def emit_fn(name, prog, limit, kbase):
                 w(f"{ind}const uint32_t v{ins[1]} = fp_inv(v{ins[2]});")
             elif op == "z":
                 w(f"{ind}const uint32_t v{ins[1]} = v{ins[2]} == 0u ? kOne : 0u;")
+            elif op == "ib":
+                n = len(ins[1])
+                tag = ins[1][0][0]
+                w(f"{ind}uint32_t ib{tag}[{n}] = {{{', '.join(f'v{x}' for _, x in ins[1])}}};")
+                w(f"{ind}fp_inv_batch(ib{tag});")
+                for k, (o, _) in enumerate(ins[1]):
+                    w(f"{ind}const uint32_t v{o} = ib{tag}[{k}];")
             elif op == "ra":
                 w(f"{ind}const uint4 r{ins[1]} = A.vals[cycle];")
                 for k, c in enumerate("xyzw"):
@@ -211,6 +284,7 @@ def head(circuit):
 def main():
     circuit, outdir = sys.argv[1], sys.argv[2]
     limit = int(sys.argv[3]) if len(sys.argv) > 3 else 1200
+    inv_batch = int(sys.argv[4]) if len(sys.argv) > 4 else 16
     ns, names, prefix = CIRCUITS[circuit]
     HEAD = head(circuit)
     fns = load(circuit)
@@ -219,7 +293,7 @@ def main():
     k = 0
     for name in names:
         launch[name] = []
-        for L in emit_fn(name, fns[name], limit, k):
+        for L in emit_fn(name, fns[name], limit, k, inv_batch):
             src = [HEAD, f"__global__ __launch_bounds__(256) void k{k}(AccArgs A) {{",
                    "  const uint32_t cycle = blockIdx.x * 256u + threadIdx.x;",
                    "  if (cycle >= A.steps) return;",

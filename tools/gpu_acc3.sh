@@ -1,0 +1,5 @@
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/acc3
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 400 --timeout-method thread -k "accum or golden or seal or hipmalloc" > gpurun_out/acc3/p.log 2>&1 || { tail -20 gpurun_out/acc3/p.log; exit 1; }
+tail -1 gpurun_out/acc3/p.log
+timeout -k 10 300 python3 -u tools/micro/accum_bench.py 20
