@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=6,
                     help="segments of the end-to-end (pinned host witness -> H2D -> seal) leg; 0 = skip")
+    ap.add_argument("--accum-steps", type=int, default=4,
+                    help="segments of the leg that also runs the rv32im accumulation inside the prover "
+                         "(r0hip_prove_segment_accum); 0 = skip")
     ap.add_argument("--cpu-po2", type=int, default=None,
                     help="segment size of the CPU baseline proof (default: the bench's own po2, at most 20)")
     ap.add_argument("--inflight", type=int, default=None,
@@ -147,6 +150,7 @@ def main():
     roofline = None
     cpu = None
     e2e = None
+    acc_leg = None
     if rank == 0:
         kt = kernel_roofline(r, hal, args, circ, dc, dd, da, dg, version)
         roofline = kt
@@ -154,6 +158,8 @@ def main():
         print(json.dumps({"phases_ms": phases, "seal_words": int(seal.size)}), file=sys.stderr)
         if args.e2e_steps > 0 and host_witness is not None:
             e2e = end_to_end(r, hal, args, host_witness, k, version)
+        if args.accum_steps > 0 and args.circuit == "rv32im" and host_witness is not None:
+            acc_leg = with_accumulation(r, hal, args, host_witness, k, version)
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args, circ)
     del host_witness
@@ -183,6 +189,8 @@ def main():
         }
         if e2e:
             line["end_to_end"] = e2e
+        if acc_leg:
+            line["with_accumulation"] = acc_leg
         print(json.dumps(line))
     if dist:
         dist.destroy_process_group()
@@ -274,6 +282,57 @@ def pmc_valu(family, args):
     if tot == 0:
         return None, None, None
     return insts, round(busy / tot, 3), os.path.relpath(files[-1], ROOT)
+
+
+def with_accumulation(r, hal, args, witness, k, version):
+    """The prove core as the reference's rv32im prove_core runs it (prove/hal/mod.rs:205-212):
+    commit code and data, draw mix, run the accumulation on the device (all three phases,
+    r0hip_prove_segment_accum), commit accum, finalize. The accum group starts INVALID as
+    the witness generator allocates it (a device fill inside the timed region). Data rows are
+    the bench's uniform words with the instruction selectors (data columns 1..13) zeroed so
+    each cycle takes one random instruction arm (mixed arms in every wavefront, the
+    accumulation step's divergent case). Reported beside `value`, never as it."""
+    import threading
+    n = 1 << args.po2
+    code, data, _accum, glob = witness
+    rng = np.random.default_rng(0x41434355)
+    arms = rng.integers(0, 13, n)
+    data = data.reshape(211, n).copy()
+    for j, col in enumerate(range(1, 14)):
+        data[col, arms > j] = 0  # the first nonzero selector wins (if / else-if mux)
+    data[32, arms == 12] = 0     # the big-integer arm's polyOp decodes one-hot (0 = nop)
+    dc, dd = hal.copy_from_elem("code", code), hal.copy_from_elem("data", data.reshape(-1))
+    accs = [hal.alloc_elem("accum", 103 * n) for _ in range(k)]
+    globs = [hal.copy_from_elem("global", glob) for _ in range(k)]
+    acc_ms = []
+
+    def run(slot, count):
+        for _ in range(count):
+            r.check(r.lib().r0hip_memset32(accs[slot].ptr, 0xFFFFFFFF, accs[slot].size))
+            r.prove_segment_accum(hal, "rv32im", args.po2, dc, dd, accs[slot], n, globs[slot], version=version)
+            acc_ms.append(r.last_profile().get("accumulate", 0.0))
+
+    def batch(count):
+        share = [count // k + (1 if i < count % k else 0) for i in range(k)]
+        ts = [threading.Thread(target=run, args=(i, share[i])) for i in range(k) if share[i]]
+        for t_ in ts:
+            t_.start()
+        for t_ in ts:
+            t_.join()
+
+    batch(k)  # warm
+    acc_ms.clear()
+    hal.synchronize()
+    t0 = time.perf_counter()
+    batch(args.accum_steps)
+    hal.synchronize()
+    t = time.perf_counter() - t0
+    return {"value": round(args.accum_steps * n / t, 1), "unit": "cycles/s",
+            "ms_per_step": round(1000 * t / args.accum_steps, 3), "steps": args.accum_steps,
+            "segments_in_flight_per_gpu": k,
+            "accumulate_phase_ms": round(sum(acc_ms) / max(1, len(acc_ms)), 3),
+            "note": "prove core including the rv32im accumulation on the device (r0hip_prove_segment_accum); "
+                    "data rows take one random instruction arm per cycle"}
 
 
 def end_to_end(r, hal, args, witness, k, version):

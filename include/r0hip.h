@@ -120,6 +120,20 @@ const char* r0hip_prove_segment(const char* circuit, int suite, uint32_t po2, co
                                 const uint32_t* d_data, const uint32_t* d_accum, uint32_t* d_global,
                                 int write_version, uint32_t version, uint32_t* h_seal, size_t seal_cap,
                                 size_t* seal_len, uint32_t* h_mix_out);
+/* ---- whole segment proof with the accumulation on the device: the prove_core sequence above,
+ * with the circuit's accumulation between the mix draw and the accum commit, as the reference
+ * runs it (rv32im: WitnessGenerator::accum, circuit/rv32im/src/prove/witgen/mod.rs:178-221, over
+ * risc0_circuit_rv32im_cuda_accum; recursion: prove/witgen.rs:138-177 over
+ * risc0_circuit_recursion_cuda_accum). d_accum is the accum group as the witness generator
+ * allocated it: every word INVALID (0xFFFFFFFF), plus for recursion the ZK noise rows the caller
+ * draws (witgen.rs:143-158); BigInt back injection (rv32im witgen/mod.rs:187-205) stays the
+ * caller's. It is accumulated over work_cycles cycles (rv32im: the preflight cycle count,
+ * 2^po2; recursion: work_cycles), INVALID words are zeroized, and the group is committed.
+ * The other arguments are r0hip_prove_segment's. */
+const char* r0hip_prove_segment_accum(const char* circuit, int suite, uint32_t po2, const uint32_t* d_code,
+                                      const uint32_t* d_data, uint32_t* d_accum, size_t work_cycles,
+                                      uint32_t* d_global, int write_version, uint32_t version, uint32_t* h_seal,
+                                      size_t seal_cap, size_t* seal_len, uint32_t* h_mix_out);
 /* ---- rv32im witness side: accumulation phases 2-3 (risc0_circuit_rv32im_cuda_accum after its
  * stepAccum kernel, rv32im-sys/kernels/cuda/ffi.cu:480-509; CPU ffi.cpp:326-360): inclusive
  * prefix sums of the last 4 accum columns over rows [0, last_cycle), then every row adds the

@@ -187,6 +187,23 @@ unsafe extern "C" {
         seal_len: *mut usize,
         h_mix_out: *mut u32,
     ) -> *const c_char;
+    /// prove_core with WitnessGenerator::accum inside (accum group given as witgen allocated it)
+    pub fn r0hip_prove_segment_accum(
+        circuit: *const c_char,
+        suite: c_int,
+        po2: u32,
+        d_code: *const u32,
+        d_data: *const u32,
+        d_accum: *mut u32,
+        work_cycles: usize,
+        d_global: *mut u32,
+        write_version: c_int,
+        version: u32,
+        h_seal: *mut u32,
+        seal_cap: usize,
+        seal_len: *mut usize,
+        h_mix_out: *mut u32,
+    ) -> *const c_char;
     pub fn r0hip_prove_segments(
         circuit: *const c_char,
         suite: c_int,

@@ -142,16 +142,16 @@ void rv32im_accum_finalize(hipStream_t s, uint32_t* accum, size_t rows, size_t c
   const uint32_t ntiles = uint32_t((last + kTile - 1) / kTile);
   const size_t groups = (cols - split) / 4;
   KScope ks("accum_finalize", double(last) * 4 * (4 * 2 + 4 + 8 * 4 * (groups ? groups - 1 : 0)));
-  DevBuf sums(size_t(4) * ntiles);
+  // per-thread scratch, reused only on this thread's stream: no host sync before returning
+  uint32_t* sums = static_cast<uint32_t*>(scratch(size_t(4) * ntiles * 4, 62));
   hipLaunchKernelGGL(tile_sums_kernel, dim3(ntiles, 4), dim3(kT), 0, s, accum, uint64_t(rows), uint32_t(cols),
-                     uint64_t(last), sums.p, ntiles);
-  hipLaunchKernelGGL(scan_sums_kernel, dim3(4), dim3(kT), 0, s, sums.p, ntiles);
+                     uint64_t(last), sums, ntiles);
+  hipLaunchKernelGGL(scan_sums_kernel, dim3(4), dim3(kT), 0, s, sums, ntiles);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(ntiles, 4), dim3(kT), 0, s, accum, uint64_t(rows), uint32_t(cols),
-                     uint64_t(last), sums.p, ntiles);
+                     uint64_t(last), sums, ntiles);
   hipLaunchKernelGGL(finalize_kernel, dim3(div_up(last, kT)), dim3(kT), 0, s, accum, uint64_t(rows), uint32_t(cols),
                      uint32_t(split), uint64_t(last));
   HIP_OK(hipGetLastError());
-  HIP_OK(hipStreamSynchronize(s));  // `sums` is freed to the pool on return
 }
 
 }  // namespace r0

@@ -22,7 +22,7 @@ void run_eval_check(const CircuitDef& c, uint32_t* check, const uint32_t* const*
 std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2, const uint32_t* code,
                                     const uint32_t* data, const uint32_t* accum, uint32_t* global,
                                     bool write_version, uint32_t version, std::vector<uint32_t>* mix_out,
-                                    const UploadGate* uploads = nullptr);
+                                    const UploadGate* uploads = nullptr, const AccumStep* acc = nullptr);
 std::string last_profile();
 }  // namespace r0
 
@@ -306,6 +306,26 @@ const char* r0hip_prove_segment(const char* circuit, int suite, uint32_t po2, co
     std::vector<uint32_t> mix;
     std::vector<uint32_t> seal = prove_segment(*c, suite, po2, d_code, d_data, d_accum, d_global, write_version != 0,
                                                version, &mix);
+    if (seal_len) *seal_len = seal.size();
+    if (h_mix_out) memcpy(h_mix_out, mix.data(), mix.size() * 4);
+    if (h_seal) {
+      R0_REQUIRE(seal.size() <= seal_cap, "seal buffer too small");
+      memcpy(h_seal, seal.data(), seal.size() * 4);
+    }
+  });
+}
+
+const char* r0hip_prove_segment_accum(const char* circuit, int suite, uint32_t po2, const uint32_t* d_code,
+                                      const uint32_t* d_data, uint32_t* d_accum, size_t work_cycles,
+                                      uint32_t* d_global, int write_version, uint32_t version, uint32_t* h_seal,
+                                      size_t seal_cap, size_t* seal_len, uint32_t* h_mix_out) {
+  return wrap([&] {
+    const CircuitDef* c = find_circuit(circuit ? circuit : "");
+    R0_REQUIRE(c, std::string("unknown circuit ") + (circuit ? circuit : "(null)"));
+    std::vector<uint32_t> mix;
+    const AccumStep acc{d_accum, work_cycles};
+    std::vector<uint32_t> seal = prove_segment(*c, suite, po2, d_code, d_data, nullptr, d_global, write_version != 0,
+                                               version, &mix, nullptr, &acc);
     if (seal_len) *seal_len = seal.size();
     if (h_mix_out) memcpy(h_mix_out, mix.data(), mix.size() * 4);
     if (h_seal) {

@@ -31,7 +31,7 @@ namespace r0 {
 std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2, const uint32_t* code,
                                     const uint32_t* data, const uint32_t* accum, uint32_t* global,
                                     bool write_version, uint32_t version, std::vector<uint32_t>* mix_out,
-                                    const UploadGate* uploads);
+                                    const UploadGate* uploads, const AccumStep* acc = nullptr);
 
 namespace {
 

@@ -556,8 +556,10 @@ std::string last_profile() { return g_last_profile; }
 std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2, const uint32_t* code,
                                     const uint32_t* data, const uint32_t* accum, uint32_t* global,
                                     bool write_version, uint32_t version, std::vector<uint32_t>* mix_out,
-                                    const UploadGate* uploads) {
+                                    const UploadGate* uploads, const AccumStep* acc) {
   R0_REQUIRE(suite >= 0 && suite <= 2, "unknown hash suite");
+  R0_REQUIRE(!acc || (acc->accum && !accum), "prove_segment: give the accum group or an accumulation, not both");
+  R0_REQUIRE(!acc || !uploads, "prove_segment: the accumulation runs on resident groups");
   R0_REQUIRE(po2 >= 2 && po2 <= 24, "po2 out of range");
   Span span("prove_core");
   hipStream_t s = stream();
@@ -605,6 +607,21 @@ std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2
   if (mix_out) *mix_out = mix;
   DevBuf dmix(mix.size() ? mix.size() : 1);
   upload_async(dmix.p, mix.data(), mix.size() * 4);
+  if (acc) {
+    Span acc_span("accumulate");
+    const size_t rows = p.cycles, cols = c.group_size(0);
+    const std::string name = c.name;
+    if (name == "rv32im") {
+      rv32im_accum(s, data, acc->accum, global, dmix.p, rows, cols, acc->work_cycles);
+    } else if (name == "recursion") {
+      recursion_accum(s, code, global, data, dmix.p, acc->accum, acc->work_cycles, rows);
+    } else {
+      R0_REQUIRE(false, "prove_segment: no device accumulation for circuit " + name);
+    }
+    eltwise_zeroize(s, acc->accum, rows * cols);
+    prof.mark("accumulate");
+    accum = acc->accum;
+  }
   commit(0, 2, accum);
   prof.mark("commit_accum");
   p.finalize(dmix.p, global);

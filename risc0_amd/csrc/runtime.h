@@ -139,6 +139,14 @@ void fill_uniform(hipStream_t s, uint32_t* out, size_t n, uint64_t seed);
 void rv32im_accum_finalize(hipStream_t s, uint32_t* accum, size_t rows, size_t cols, size_t split, size_t last);
 void rv32im_accum(hipStream_t s, const uint32_t* data, uint32_t* accum, const uint32_t* global,
                   const uint32_t* mix, size_t rows, size_t cols, size_t last);
+// The accumulation a segment prover runs between the mix draw and the accum commit
+// (rv32im prove/witgen/mod.rs:178-221, recursion prove/witgen.rs:138-177): `accum` holds the
+// group as the witness generator left it (INVALID words, plus the recursion ZK noise rows);
+// the circuit's accumulation fills it for `work_cycles` cycles, then INVALID words become 0.
+struct AccumStep {
+  uint32_t* accum;
+  size_t work_cycles;
+};
 // recursion circuit accumulation (recursion_accum.hip): compute, prefix product, verify
 void recursion_accum(hipStream_t s, const uint32_t* ctrl, const uint32_t* global, const uint32_t* data,
                      const uint32_t* mix, uint32_t* accum, size_t steps, size_t cycles);

@@ -85,6 +85,8 @@ def _declare(L):
         "r0hip_eval_check": [C.c_char_p, vp, C.POINTER(vp), vp, vp, u32p, C.c_uint32],
         "r0hip_prove_segment": [C.c_char_p, C.c_int, C.c_uint32, vp, vp, vp, vp, C.c_int, C.c_uint32, u32p, sz,
                                 C.POINTER(sz), u32p],
+        "r0hip_prove_segment_accum": [C.c_char_p, C.c_int, C.c_uint32, vp, vp, vp, sz, vp, C.c_int, C.c_uint32,
+                                      u32p, sz, C.POINTER(sz), u32p],
         "r0hip_last_profile": [C.c_char_p, sz],
         "r0hip_set_kernel_timing": [C.c_int],
         "r0hip_kernel_times": [C.c_char_p, sz],
@@ -344,6 +346,23 @@ def prove_segment(hal, circuit, po2, code, data, accum, glob, version=None, seal
     check(lib().r0hip_prove_segment(circuit.encode(), hal.suite, po2, code.ptr, data.ptr, accum.ptr, glob.ptr,
                                     int(version is not None), version or 0, seal.ctypes.data_as(u32p), seal_cap,
                                     C.byref(n), mix.ctypes.data_as(u32p)))
+    return seal[: n.value].copy(), mix
+
+
+def prove_segment_accum(hal, circuit, po2, code, data, accum, work_cycles, glob, version=None, seal_cap=1 << 24):
+    """Prove one segment with the circuit's accumulation on the device between the mix draw and
+    the accum commit (r0hip_prove_segment_accum): `accum` holds the group as the witness
+    generator allocated it (INVALID words) and is filled in place. Returns (seal, mix)."""
+    from json import load
+    with open(os.path.join(_HERE, "circuits", circuit + ".taps.json")) as f:
+        mix_size = load(f)["mix_size"]
+    seal = np.zeros(seal_cap, dtype=np.uint32)
+    n = C.c_size_t(0)
+    mix = np.zeros(mix_size, dtype=np.uint32)
+    check(lib().r0hip_prove_segment_accum(circuit.encode(), hal.suite, po2, code.ptr, data.ptr, accum.ptr,
+                                          work_cycles, glob.ptr, int(version is not None), version or 0,
+                                          seal.ctypes.data_as(u32p), seal_cap, C.byref(n),
+                                          mix.ctypes.data_as(u32p)))
     return seal[: n.value].copy(), mix
 
 

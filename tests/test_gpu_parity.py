@@ -760,3 +760,56 @@ def test_recursion_accum_matches_reference(hal, oracle, po2, short):
     hal.recursion_accum(dev(hal, ctrl), dev(hal, glob), dev(hal, data), dev(hal, mix), dacc, steps, n)
     got = dacc.to_numpy()
     assert np.array_equal(got, ref), int((got != ref).sum())
+
+
+@pytest.mark.parametrize("circuit,suite,po2", [("rv32im", "poseidon2", 10), ("rv32im", "sha-256", 9),
+                                               ("recursion", "poseidon2", 9)])
+def test_prove_segment_accum_matches_reference(hal, hal_sha, oracle, circuit, suite, po2):
+    """The prove core with the accumulation on the device (r0hip_prove_segment_accum: commit
+    code and data, draw mix, accumulate, zeroize, commit accum, finalize), as the reference's
+    prove_core runs it (rv32im prove/hal/mod.rs:205-212, recursion prove/mod.rs:212-218).
+    Checked in two halves against the reference: the device-filled accum group equals the
+    compiled reference accumulation (oracle/_ref) run on the same rows with the mix the
+    transcript drew, INVALID words zeroized; and the seal equals the oracle prover's on that
+    accum group."""
+    import risc0_amd as r
+    if oracle.ref_lib() is None:
+        pytest.skip("oracle/_ref not built")
+    h, s = H(suite), S(oracle, suite)
+    d = oracle.load_circuit_json(circuit)
+    gs = d["group_sizes"]
+    n = 1 << po2
+    rng = np.random.default_rng(0x41434355 + po2)
+    INVALID = 0xFFFFFFFF
+    if circuit == "rv32im":
+        import rv32im_accum_ref as R
+        from test_rv32im_accum_ir import rows_for_arms
+        if not R.available():
+            pytest.skip("oracle/_ref/libref_rv32im_accum.so not built")
+        code = oracle.rand_elems(rng, gs[1] * n)
+        data = rows_for_arms(rng, n, list(rng.integers(0, 13, n)))
+        glob = oracle.rand_elems(rng, d["output_size"])
+        acc0 = np.full(gs[0] * n, INVALID, np.uint32)
+        work, version = n, 2
+    else:
+        import accum_ir as A
+        code, glob, data, _ = A.synthetic(rng, oracle, po2, gs, d["output_size"], d["mix_size"])
+        acc0 = np.full(gs[0] * n, INVALID, np.uint32).reshape(gs[0], n)
+        acc0[:, n - 8:] = oracle.rand_elems(rng, gs[0] * 8).reshape(gs[0], 8)  # ZK noise rows
+        acc0 = acc0.reshape(-1)
+        work, version = n - 8, None
+    dacc = dev(h, acc0)
+    seal, mix = r.prove_segment_accum(h, circuit, po2, dev(h, code), dev(h, data), dacc, work, dev(h, glob),
+                                      version=version)
+    glob_z = np.where(glob == INVALID, 0, glob).astype(np.uint32)
+    if circuit == "rv32im":
+        ref_acc = R.accum(data, glob_z, mix, n, work)
+    else:
+        ref_acc = acc0.copy()
+        A.ref_accum(code, glob_z, data, mix, ref_acc, work, n)
+    ref_acc = np.where(ref_acc == INVALID, 0, ref_acc).astype(np.uint32)
+    got = dacc.to_numpy()
+    assert np.array_equal(got, ref_acc), int((got != ref_acc).sum())
+    ref_seal, ref_mix, _ = oracle.prove_segment(circuit, s, po2, code, data, ref_acc, glob, version=version)
+    assert np.array_equal(mix, ref_mix)
+    assert np.array_equal(seal, ref_seal)
