@@ -205,8 +205,34 @@ def emit_fn(name, prog, limit, kbase, inv_batch=1):
                 continue
             pre[id(ins)] = ins
             stack += [u for u in used(ins) if u not in have]
-        pre = batch_inverses(sorted(pre.values(), key=lambda i: order[id(i)]), inv_batch)
-        body = batch_body(body, inv_batch, {ins[1] for ins in body if ins[0] == "w"})
+        written = {ins[1] for ins in body if ins[0] == "w"}
+        vals_written = any(ins[0] == "wa" for ins in body)
+        pinned = lambda ins: (ins[0] == "l" and ins[2] in written) or (ins[0] == "ra" and vals_written)
+        # the value pool: the prelude and the body's top-level pure definitions, emitted on
+        # demand; the items: everything else at the top level of the body, in order
+        pool = sorted(pre.values(), key=lambda i: order[id(i)])
+        items, lv, cur = [], 0, None
+        for ins in body:
+            if lv == 0 and ins[0] in DEFS and not pinned(ins):
+                pool.append(ins)
+            elif lv == 0 and ins[0] != "if":
+                items.append([ins])
+            else:
+                if lv == 0:
+                    cur = []
+                    items.append(cur)
+                cur.append(ins)
+            lv += {"if": 1, "end": -1}.get(ins[0], 0)
+        split = []
+        for it in items:
+            if it[0][0] == "if" and all(x[0] == "w" for x in it[1:-1]):
+                split += [[it[0], x, it[-1]] for x in it[1:-1]]  # one guarded store per item
+            elif it[0][0] == "if":
+                split.append([it[0]] + batch_body(it[1:-1], inv_batch, written) + [it[-1]])
+            else:
+                split.append(it)
+        items = split
+        pre = batch_inverses(pool, inv_batch)
         L = []
         w = L.append
         ind = "  "
@@ -248,21 +274,51 @@ def emit_fn(name, prog, limit, kbase, inv_batch=1):
             else:
                 raise ValueError(op)
 
-        for ins in pre:
-            stmt(ins, ind)
+        # pool values are emitted depth-first, each just before the first top-level item that
+        # needs it (short live ranges: program order kept every value live from its
+        # definition to its last store and spilled); stores keep their order
+        node_of = {}
+        for k, ins in enumerate(pre):
+            for d in ([o for o, _ in ins[1]] if ins[0] == "ib" else defined(ins)):
+                node_of[d] = k
+        uses_of = lambda ins: [x for _, x in ins[1]] if ins[0] == "ib" else used(ins)
+        done = set()
+
+        def need(vals, ind):
+            stack = [(node_of[v], False) for v in reversed(list(vals)) if v in node_of]
+            while stack:
+                k, expanded = stack.pop()
+                if k in done:
+                    continue
+                if expanded:
+                    done.add(k)
+                    stmt(pre[k], ind)
+                    continue
+                stack.append((k, True))
+                for u in reversed(uses_of(pre[k])):
+                    if u in node_of and node_of[u] not in done:
+                        stack.append((node_of[u], False))
+
+        need(guards, ind)
         if guards:
             w(f"  if ({' && '.join(f'v{g} != 0u' for g in guards)}) {{")
             ind = "    "
         depth = ind
-        for ins in body:
-            if ins[0] == "if":
-                w(f"{depth}if (v{ins[1]} != 0u) {{")
-                depth += "  "
-            elif ins[0] == "end":
-                depth = depth[:-2]
-                w(f"{depth}}}")
-            else:
-                stmt(ins, depth)
+        for item in items:
+            vals = []
+            for it in item:
+                vals += [it[1]] if it[0] == "if" else ([] if it[0] == "end" else uses_of(it))
+            need(vals, ind)
+            for ins in item:
+                if ins[0] == "if":
+                    w(f"{depth}if (v{ins[1]} != 0u) {{")
+                    depth += "  "
+                elif ins[0] == "end":
+                    depth = depth[:-2]
+                    w(f"{depth}}}")
+                else:
+                    stmt(ins, depth)
+        need([d for ins in pre for d in defined(ins) if ins[0] != "ib"], ind)  # unused pool values
         if guards:
             w("  }")
         kernels.append(L)
@@ -284,7 +340,7 @@ def head(circuit):
 def main():
     circuit, outdir = sys.argv[1], sys.argv[2]
     limit = int(sys.argv[3]) if len(sys.argv) > 3 else 1200
-    inv_batch = int(sys.argv[4]) if len(sys.argv) > 4 else 16
+    inv_batch = int(sys.argv[4]) if len(sys.argv) > 4 else 8
     ns, names, prefix = CIRCUITS[circuit]
     HEAD = head(circuit)
     fns = load(circuit)
