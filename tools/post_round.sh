@@ -6,10 +6,12 @@ TAG=$1; R=${2:-$TAG}
 O=gpurun_out/$TAG
 cd "$(dirname "$0")/.."
 f() { find $O/$1 -name "$2" | head -1; }
-python3 tools/rocprof_families.py "$(f stats '*kernel_stats.csv')" 9 > profiles/${R}_rocprof_families.txt
+# proofs per profiled run (tools/gpu_round.sh): stats 9, PMC runs 6; override for older runs
+NS=${3:-9}; NP=${4:-6}
+python3 tools/rocprof_families.py "$(f stats '*kernel_stats.csv')" $NS > profiles/${R}_rocprof_families.txt
 cp "$(f stats '*kernel_stats.csv')" profiles/${R}_rocprof_kernel_stats.csv
 python3 tools/pmc_summary.py "$(f valu '*counter_collection.csv')" profiles/${R}_pmc_valu.json > profiles/${R}_pmc_valu.txt
-python3 tools/pmc_traffic.py "$(f fetch '*counter_collection.csv')" "$(f write '*counter_collection.csv')" 6 > profiles/${R}_pmc_traffic.json
+python3 tools/pmc_traffic.py "$(f fetch '*counter_collection.csv')" "$(f write '*counter_collection.csv')" $NP > profiles/${R}_pmc_traffic.json
 cp $O/bench.json profiles/${R}_bench.json
 cp $O/pytest_gpu.log profiles/${R}_pytest_gpu.log
 head -30 profiles/${R}_rocprof_families.txt
