@@ -38,7 +38,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=6,
                     help="segments of the end-to-end (pinned host witness -> H2D -> seal) leg; 0 = skip")
-    ap.add_argument("--accum-steps", type=int, default=4,
+    ap.add_argument("--accum-steps", type=int, default=6,
                     help="segments of the leg that also runs the rv32im accumulation inside the prover "
                          "(r0hip_prove_segment_accum); 0 = skip")
     ap.add_argument("--cpu-po2", type=int, default=None,
@@ -320,7 +320,7 @@ def with_accumulation(r, hal, args, witness, k, version):
         for t_ in ts:
             t_.join()
 
-    batch(k)  # warm
+    batch(2 * k)  # warm every thread's stream, pool and scratch
     acc_ms.clear()
     hal.synchronize()
     t0 = time.perf_counter()

@@ -15,7 +15,7 @@ a piece re-evaluates the pure definitions it uses from enclosing blocks (loads, 
 arithmetic) and runs under the conjunction of its enclosing guards. Pieces run in program
 order, so every register write of a cycle lands in the order the reference makes it.
 
-  gen_accum.py CIRCUIT OUTDIR [LIMIT [INV_BATCH]]
+  gen_accum.py CIRCUIT OUTDIR [LIMIT [INV_BATCH [LOAD_AHEAD]]]
 Writes OUTDIR/accum_k<i>.hip and OUTDIR/accum.hip (launchers of the functions).
 """
 import os
@@ -176,7 +176,7 @@ def batch_body(body, width, written):
     return out[:-1]
 
 
-def emit_fn(name, prog, limit, kbase, inv_batch=1):
+def emit_fn(name, prog, limit, kbase, inv_batch=1, load_ahead=0):
     defs = {}
     order = {}
     for pos, ins in enumerate(prog):
@@ -284,7 +284,7 @@ def emit_fn(name, prog, limit, kbase, inv_batch=1):
         uses_of = lambda ins: [x for _, x in ins[1]] if ins[0] == "ib" else used(ins)
         done = set()
 
-        def need(vals, ind):
+        def need(vals, seq):
             stack = [(node_of[v], False) for v in reversed(list(vals)) if v in node_of]
             while stack:
                 k, expanded = stack.pop()
@@ -292,24 +292,45 @@ def emit_fn(name, prog, limit, kbase, inv_batch=1):
                     continue
                 if expanded:
                     done.add(k)
-                    stmt(pre[k], ind)
+                    seq.append(("node", k))
                     continue
                 stack.append((k, True))
                 for u in reversed(uses_of(pre[k])):
                     if u in node_of and node_of[u] not in done:
                         stack.append((node_of[u], False))
 
-        need(guards, ind)
-        if guards:
-            w(f"  if ({' && '.join(f'v{g} != 0u' for g in guards)}) {{")
-            ind = "    "
-        depth = ind
+        gseq, seq = [], []
+        need(guards, gseq)
         for item in items:
             vals = []
             for it in item:
                 vals += [it[1]] if it[0] == "if" else ([] if it[0] == "end" else uses_of(it))
-            need(vals, ind)
-            for ins in item:
+            need(vals, seq)
+            seq.append(("item", item))
+        need([d for ins in pre for d in defined(ins) if ins[0] != "ib"], seq)  # unused pool values
+        for _, k in gseq:
+            stmt(pre[k], ind)
+        if guards:
+            w(f"  if ({' && '.join(f'v{g} != 0u' for g in guards)}) {{")
+            ind = "    "
+        # trace loads run `load_ahead` loads ahead of their depth-first position, so a wave
+        # has that many in flight instead of waiting on each right before its use
+        loads = [k for t, k in seq if t == "node" and pre[k][0] == "l"]
+        issued, seen = set(), 0
+        depth = ind
+        for t, x in seq:
+            if t == "node" and pre[x][0] == "l":
+                seen += 1
+            for k in loads[:seen + load_ahead]:
+                if k not in issued:
+                    issued.add(k)
+                    stmt(pre[k], ind)
+            if t == "node":
+                if x not in issued:
+                    issued.add(x)
+                    stmt(pre[x], ind)
+                continue
+            for ins in x:
                 if ins[0] == "if":
                     w(f"{depth}if (v{ins[1]} != 0u) {{")
                     depth += "  "
@@ -318,7 +339,6 @@ def emit_fn(name, prog, limit, kbase, inv_batch=1):
                     w(f"{depth}}}")
                 else:
                     stmt(ins, depth)
-        need([d for ins in pre for d in defined(ins) if ins[0] != "ib"], ind)  # unused pool values
         if guards:
             w("  }")
         kernels.append(L)
@@ -341,6 +361,7 @@ def main():
     circuit, outdir = sys.argv[1], sys.argv[2]
     limit = int(sys.argv[3]) if len(sys.argv) > 3 else 1200
     inv_batch = int(sys.argv[4]) if len(sys.argv) > 4 else 8
+    load_ahead = int(sys.argv[5]) if len(sys.argv) > 5 else 64
     ns, names, prefix = CIRCUITS[circuit]
     HEAD = head(circuit)
     fns = load(circuit)
@@ -349,7 +370,7 @@ def main():
     k = 0
     for name in names:
         launch[name] = []
-        for L in emit_fn(name, fns[name], limit, k, inv_batch):
+        for L in emit_fn(name, fns[name], limit, k, inv_batch, load_ahead):
             src = [HEAD, f"__global__ __launch_bounds__(256) void k{k}(AccArgs A) {{",
                    "  const uint32_t cycle = blockIdx.x * 256u + threadIdx.x;",
                    "  if (cycle >= A.steps) return;",
