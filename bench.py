@@ -284,6 +284,18 @@ def pmc_valu(family, args):
     return insts, round(busy / tot, 3), os.path.relpath(files[-1], ROOT)
 
 
+def mixed_arm_rows(data, n):
+    """The bench's uniform rv32im data rows with the instruction selectors (data columns
+    1..13) zeroed so each cycle takes one random instruction arm of the accumulation step."""
+    rng = np.random.default_rng(0x41434355)
+    arms = rng.integers(0, 13, n)
+    data = data.reshape(211, n).copy()
+    for j, col in enumerate(range(1, 14)):
+        data[col, arms > j] = 0  # the first nonzero selector wins (if / else-if mux)
+    data[32, arms == 12] = 0     # the big-integer arm's polyOp decodes one-hot (0 = nop)
+    return data.reshape(-1)
+
+
 def with_accumulation(r, hal, args, witness, k, version):
     """The prove core as the reference's rv32im prove_core runs it (prove/hal/mod.rs:205-212):
     commit code and data, draw mix, run the accumulation on the device (all three phases,
@@ -295,22 +307,20 @@ def with_accumulation(r, hal, args, witness, k, version):
     import threading
     n = 1 << args.po2
     code, data, _accum, glob = witness
-    rng = np.random.default_rng(0x41434355)
-    arms = rng.integers(0, 13, n)
-    data = data.reshape(211, n).copy()
-    for j, col in enumerate(range(1, 14)):
-        data[col, arms > j] = 0  # the first nonzero selector wins (if / else-if mux)
-    data[32, arms == 12] = 0     # the big-integer arm's polyOp decodes one-hot (0 = nop)
-    dc, dd = hal.copy_from_elem("code", code), hal.copy_from_elem("data", data.reshape(-1))
+    data = mixed_arm_rows(data, n)
+    dc, dd = hal.copy_from_elem("code", code), hal.copy_from_elem("data", data)
     accs = [hal.alloc_elem("accum", 103 * n) for _ in range(k)]
     globs = [hal.copy_from_elem("global", glob) for _ in range(k)]
-    acc_ms = []
+    acc_ms, per = [], []
 
     def run(slot, count):
         for _ in range(count):
             r.check(r.lib().r0hip_memset32(accs[slot].ptr, 0xFFFFFFFF, accs[slot].size))
+            t0 = time.perf_counter()
             r.prove_segment_accum(hal, "rv32im", args.po2, dc, dd, accs[slot], n, globs[slot], version=version)
-            acc_ms.append(r.last_profile().get("accumulate", 0.0))
+            prof = r.last_profile()
+            acc_ms.append(prof.get("accumulate", 0.0))
+            per.append((slot, round(1000 * (time.perf_counter() - t0), 1), {k_: round(v, 1) for k_, v in prof.items()}))
 
     def batch(count):
         share = [count // k + (1 if i < count % k else 0) for i in range(k)]
@@ -323,14 +333,18 @@ def with_accumulation(r, hal, args, witness, k, version):
     batch(2 * k)  # warm every thread's stream, pool and scratch
     acc_ms.clear()
     hal.synchronize()
+    m0 = r.mem_stats()["mallocs"]
     t0 = time.perf_counter()
     batch(args.accum_steps)
     hal.synchronize()
     t = time.perf_counter() - t0
+    mallocs = r.mem_stats()["mallocs"] - m0
+    print(json.dumps({"with_accumulation_proofs": per[-args.accum_steps:]}), file=sys.stderr)
     return {"value": round(args.accum_steps * n / t, 1), "unit": "cycles/s",
             "ms_per_step": round(1000 * t / args.accum_steps, 3), "steps": args.accum_steps,
             "segments_in_flight_per_gpu": k,
             "accumulate_phase_ms": round(sum(acc_ms) / max(1, len(acc_ms)), 3),
+            "hipmallocs_in_timed_region": mallocs,
             "note": "prove core including the rv32im accumulation on the device (r0hip_prove_segment_accum); "
                     "data rows take one random instruction arm per cycle"}
 
@@ -359,6 +373,25 @@ def end_to_end(r, hal, args, witness, k, version):
         t0 = time.perf_counter()
         r.prove_segments(hal, args.circuit, args.po2, jobs(args.e2e_steps), version=version, in_flight=k)
         t = time.perf_counter() - t0
+        dev_acc = None
+        if args.circuit == "rv32im":
+            # witgen's output only (code, data with mixed instruction arms, globals): each
+            # prover accumulates on the device, the accum group never crosses PCIe
+            p = ctypes.c_void_p()
+            r.check(lib.r0hip_host_alloc(ctypes.byref(p), witness[1].size * 4))
+            hosts.append(p.value)
+            np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint32)),
+                                  shape=(witness[1].size,))[:] = mixed_arm_rows(witness[1], 1 << args.po2)
+            ajobs = lambda n: [(hosts[0], p.value, None, hosts[3])] * n
+            r.prove_segments(hal, args.circuit, args.po2, ajobs(k), version=version, in_flight=k)  # warm
+            t0 = time.perf_counter()
+            r.prove_segments(hal, args.circuit, args.po2, ajobs(args.e2e_steps), version=version, in_flight=k)
+            ta = time.perf_counter() - t0
+            dev_acc = {"value": round(args.e2e_steps * (1 << args.po2) / ta, 1), "unit": "cycles/s",
+                       "ms_per_step": round(1000.0 * ta / args.e2e_steps, 3),
+                       "h2d_bytes_per_segment": int(witness[0].size * 4 + witness[1].size * 4 + witness[3].size * 4),
+                       "note": "code, data (mixed instruction arms) and globals from pinned host memory; the "
+                               "accumulation runs on the device inside each proof (job h_accum = NULL)"}
     finally:
         for hp in hosts:
             r.check(lib.r0hip_host_free(hp))
@@ -367,7 +400,8 @@ def end_to_end(r, hal, args, witness, k, version):
             "h2d_bytes_per_segment": int(h2d_bytes), "ms_one_segment_unpipelined": round(1000.0 * t_one, 1),
             "note": f"witness in pinned host memory; native pipeline (r0hip_prove_segments): an uploader fills "
                     f"{k + 1} device buffer sets ahead of {k} prover threads, so H2D overlaps proving; a prover "
-                    f"starts a segment while its later witness groups still upload (per-group gate)"}
+                    f"starts a segment while its later witness groups still upload (per-group gate)",
+            **({"with_device_accumulation": dev_acc} if dev_acc else {})}
 
 
 def pmc_traffic(family, calls, args):

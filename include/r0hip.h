@@ -176,7 +176,8 @@ const char* r0hip_recursion_accum(const uint32_t* d_ctrl, const uint32_t* d_glob
 typedef struct r0hip_segment_job {
   const uint32_t* h_code;
   const uint32_t* h_data;
-  const uint32_t* h_accum;
+  const uint32_t* h_accum;  /* rv32im: NULL = accumulate on the device (as r0hip_prove_segment_accum,
+                               work cycles 2^po2); the group then never crosses PCIe */
   const uint32_t* h_global; /* output_size words; zeroized on the device copy only */
   uint32_t* h_seal;
   size_t seal_cap;

@@ -125,6 +125,7 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
     ensure_init();
     if (njobs == 0) return nullptr;
     const size_t k = std::max<size_t>(1, std::min<size_t>(in_flight ? in_flight : 2, njobs));
+    const bool device_accum_ok = std::string(c->name) == "rv32im";
     const size_t n = size_t(1) << po2;
     // group_sizes: accum 0, code 1, data 2 (the reference's register-group order)
     const size_t words[4] = {c->group_sizes[1] * n, c->group_sizes[2] * n, c->group_sizes[0] * n, c->output_size};
@@ -166,8 +167,10 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
           for (auto& q : b.queued) q = 0;  // the set is free: no prover waits on it
         }
         const uint32_t* src[4] = {jobs[i].h_code, jobs[i].h_data, jobs[i].h_accum, jobs[i].h_global};
+        // rv32im without an accum group: the prover accumulates on the device
+        const bool dev_accum = !src[2] && device_accum_ok;
         bool null_group = false;
-        for (int g = 0; g < 4; g++) null_group |= !src[g];
+        for (int g = 0; g < 4; g++) null_group |= !src[g] && !(g == 2 && dev_accum);
         if (null_group) jobs[i].error = dup_msg("witness group pointer is NULL");  // before the hand-over
         ready_q.put(s);  // a prover may start now; it waits per group (BufSet::wait)
         if (null_group) {
@@ -179,6 +182,10 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
           // in the order the prover first touches them (globals, code, data, accum), each in
           // column chunks, so a segment's commits run while its later columns still upload
           for (int g : {3, 0, 1, 2}) {
+            if (g == 2 && dev_accum) {
+              b.mark(g, b.chunks(g));  // nothing to upload; the prover never waits on it
+              continue;
+            }
             for (size_t k = 0; k < b.chunks(g); k++) {
               const size_t c0 = k * kChunkCols, cc = std::min(kChunkCols, b.cols[g] - c0);
               HIP_OK(hipMemcpyAsync(b.g[g].p + c0 * b.col_words[g], src[g] + c0 * b.col_words[g],
@@ -215,8 +222,11 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
             try {
               ensure_init();
               std::vector<uint32_t> mix;
-              std::vector<uint32_t> seal = prove_segment(*c, suite, po2, b.g[0].p, b.g[1].p, b.g[2].p, b.g[3].p,
-                                                         write_version != 0, version, &mix, &b);
+              const bool dev_accum = !j.h_accum;  // (rv32im only: checked by the uploader)
+              const AccumStep acc{b.g[2].p, n, true};
+              std::vector<uint32_t> seal =
+                  prove_segment(*c, suite, po2, b.g[0].p, b.g[1].p, dev_accum ? nullptr : b.g[2].p, b.g[3].p,
+                                write_version != 0, version, &mix, &b, dev_accum ? &acc : nullptr);
               HIP_OK(hipStreamSynchronize(stream()));
               if (!failed()) {  // an upload error leaves the proof meaningless: drop it
                 j.seal_len = seal.size();

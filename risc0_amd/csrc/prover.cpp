@@ -559,7 +559,6 @@ std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2
                                     const UploadGate* uploads, const AccumStep* acc) {
   R0_REQUIRE(suite >= 0 && suite <= 2, "unknown hash suite");
   R0_REQUIRE(!acc || (acc->accum && !accum), "prove_segment: give the accum group or an accumulation, not both");
-  R0_REQUIRE(!acc || !uploads, "prove_segment: the accumulation runs on resident groups");
   R0_REQUIRE(po2 >= 2 && po2 <= 24, "po2 out of range");
   Span span("prove_core");
   hipStream_t s = stream();
@@ -611,6 +610,7 @@ std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2
     Span acc_span("accumulate");
     const size_t rows = p.cycles, cols = c.group_size(0);
     const std::string name = c.name;
+    if (acc->fill_invalid) HIP_OK(hipMemsetD32Async(acc->accum, 0xFFFFFFFFu, rows * cols, s));
     if (name == "rv32im") {
       rv32im_accum(s, data, acc->accum, global, dmix.p, rows, cols, acc->work_cycles);
     } else if (name == "recursion") {
@@ -620,9 +620,10 @@ std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2
     }
     eltwise_zeroize(s, acc->accum, rows * cols);
     prof.mark("accumulate");
-    accum = acc->accum;
+    p.commit_group(0, acc->accum);  // nothing to wait for: the group never uploads
+  } else {
+    commit(0, 2, accum);
   }
-  commit(0, 2, accum);
   prof.mark("commit_accum");
   p.finalize(dmix.p, global);
   HIP_OK(hipStreamSynchronize(s));

@@ -146,6 +146,7 @@ void rv32im_accum(hipStream_t s, const uint32_t* data, uint32_t* accum, const ui
 struct AccumStep {
   uint32_t* accum;
   size_t work_cycles;
+  bool fill_invalid = false;  // the buffer is reused: fill it with INVALID words first
 };
 // recursion circuit accumulation (recursion_accum.hip): compute, prefix product, verify
 void recursion_accum(hipStream_t s, const uint32_t* ctrl, const uint32_t* global, const uint32_t* data,

@@ -376,7 +376,9 @@ class SegmentJob(C.Structure):
 def prove_segments(hal, circuit, po2, witnesses, version=None, in_flight=2, seal_cap=1 << 24):
     """The native segment pipeline (r0hip_prove_segments): `witnesses` is a list of
     (code, data, accum, global) host arrays (numpy uint32, ideally views of page-locked
-    memory) or raw host pointers; returns [(seal, mix)] in job order."""
+    memory) or raw host pointers; returns [(seal, mix)] in job order. For rv32im, accum may
+    be None: the prover then runs the accumulation on the device (r0hip_prove_segment_accum's
+    path) and nothing of that group crosses PCIe."""
     from json import load
     with open(os.path.join(_HERE, "circuits", circuit + ".taps.json")) as f:
         mix_size = load(f)["mix_size"]
@@ -390,7 +392,7 @@ def prove_segments(hal, circuit, po2, witnesses, version=None, in_flight=2, seal
                 keep.append(a)
                 ptrs.append(a.ctypes.data)
             else:
-                ptrs.append(int(a))
+                ptrs.append(0 if a is None else int(a))
         j.h_code, j.h_data, j.h_accum, j.h_global = ptrs
         seals.append(np.zeros(seal_cap, dtype=np.uint32))
         mixes.append(np.zeros(mix_size, dtype=np.uint32))

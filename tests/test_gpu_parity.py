@@ -813,3 +813,31 @@ def test_prove_segment_accum_matches_reference(hal, hal_sha, oracle, circuit, su
     ref_seal, ref_mix, _ = oracle.prove_segment(circuit, s, po2, code, data, ref_acc, glob, version=version)
     assert np.array_equal(mix, ref_mix)
     assert np.array_equal(seal, ref_seal)
+
+
+@pytest.mark.parametrize("suite,po2", [("poseidon2", 10), ("sha-256", 9)])
+def test_prove_segments_device_accum_matches_fused(hal, hal_sha, oracle, suite, po2):
+    """The segment pipeline with no host accum group (rv32im): each prover accumulates on
+    the device after the mix draw. Seals equal r0hip_prove_segment_accum's on the same
+    witness (which test_prove_segment_accum_matches_reference pins to the reference), for
+    more jobs than buffer sets, so sets are reused and refilled with INVALID words."""
+    import risc0_amd as r
+    from test_rv32im_accum_ir import rows_for_arms
+    h = H(suite)
+    d = oracle.load_circuit_json("rv32im")
+    n = 1 << po2
+    jobs, want = [], []
+    for i in range(4):
+        rng = np.random.default_rng(0x50495045 + 7 * po2 + i)
+        code = oracle.rand_elems(rng, d["group_sizes"][1] * n)
+        data = rows_for_arms(rng, n, list(rng.integers(0, 13, n)))
+        glob = oracle.rand_elems(rng, d["output_size"])
+        dacc = dev(h, np.full(d["group_sizes"][0] * n, 0xFFFFFFFF, np.uint32))
+        seal, mix = r.prove_segment_accum(h, "rv32im", po2, dev(h, code), dev(h, data), dacc, n, dev(h, glob),
+                                          version=2)
+        want.append((seal, mix))
+        jobs.append((code, data, None, glob))
+    got = r.prove_segments(h, "rv32im", po2, jobs, version=2, in_flight=2)
+    for (s1, m1), (s2, m2) in zip(got, want):
+        assert np.array_equal(m1, m2)
+        assert np.array_equal(s1, s2)
