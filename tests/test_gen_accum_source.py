@@ -1,0 +1,49 @@
+"""The generated rv32im accumulation kernels, run from their HIP source text by a numpy
+interpreter of the emitted C subset (tests/gen_src_eval.py), equal the IR interpreter
+(tests/rv32im_accum_ir.py, itself pinned to the compiled reference's stepAccum) on random
+rows over all 13 instruction arms: the generator's rewrites — inverse batches, depth-first
+emission with split guarded stores, load look-ahead, kernel cuts — keep the program's
+meaning, checked on the CPU for the build's settings and for the unbatched program-order
+baseline."""
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import gen_src_eval as GS
+import rv32im_accum_ir as IRI
+from test_rv32im_accum_ir import rows_for_arms
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _generate(tmp, limit, inv_batch, ahead):
+    out = os.path.join(tmp, f"rv_{limit}_{inv_batch}_{ahead}")
+    subprocess.check_call([sys.executable, os.path.join(ROOT, "tools", "gen_accum.py"), "rv32im", out,
+                           str(limit), str(inv_batch), str(ahead)], stdout=subprocess.DEVNULL)
+    launcher = open(os.path.join(out, "accum.hip")).read()
+    order = re.findall(r"rv_accum::launch_k(\d+)\(s, A\);", launcher)
+    return [open(os.path.join(out, f"accum_k{k}.hip")).read() for k in order]
+
+
+@pytest.mark.parametrize("limit,inv_batch,ahead", [(1200, 8, 64), (1200, 1, 0), (600, 16, 0)])
+@pytest.mark.parametrize("rows,last", [(64, 64), (64, 50)])
+def test_generated_source_matches_ir(tmp_path, limit, inv_batch, ahead, rows, last):
+    kernels = _generate(str(tmp_path), limit, inv_batch, ahead)
+    rng = np.random.default_rng(rows + last + limit + inv_batch)
+    data = rows_for_arms(rng, rows, list(rng.integers(0, 13, rows)))
+    glob = rng.integers(0, GS.P, 90, dtype=np.uint64).astype(np.uint32)
+    mix = rng.integers(0, GS.P, 36, dtype=np.uint64).astype(np.uint32)
+    want = np.full(103 * rows, 0xFFFFFFFF, np.uint32)
+    IRI.run(data.copy(), want, glob, mix, rows, last)
+    got = np.full(103 * rows, 0xFFFFFFFF, np.uint32)
+    bufs = [data.copy(), got, glob, mix]
+    for src in kernels:
+        GS.run_kernel(src, bufs, rows, last)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} words differ; first at col {bad[0] // rows} row {bad[0] % rows}"
+    if inv_batch > 1:
+        assert any("fp_inv_batch" in k for k in kernels)
