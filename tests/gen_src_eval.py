@@ -25,6 +25,9 @@ _PATTERNS = [
     ("if", re.compile(r"if \((v\d+ != 0u(?: && v\d+ != 0u)*)\) \{$")),
     ("end", re.compile(r"\}$")),
     ("store", re.compile(r"A\.a\[(\d+)\]\[uint64_t\((\d+)u\) \* A\.cycles \+ cycle\] = v(\d+);$")),
+    ("vread", re.compile(r"const uint4 r(\d+) = A\.vals\[cycle\];$")),
+    ("vget", re.compile(r"const uint32_t v(\d+) = r(\d+)\.([xyzw]);$")),
+    ("vwrite", re.compile(r"A\.vals\[cycle\] = make_uint4\(v(\d+), v(\d+), v(\d+), v(\d+)\);$")),
 ]
 _SKIP = re.compile(r"^(const uint32_t (cycle|mask) = .*|if \(cycle >= A\.steps\) return;)$")
 
@@ -41,11 +44,12 @@ def _inv(x):
     return np.array([pow(int(a), P - 2, P) * R % P * R % P if a else 0 for a in x], np.int64)
 
 
-def run_kernel(src, bufs, rows, steps):
+def run_kernel(src, bufs, rows, steps, vals=None):
     """Execute one generated kernel's statements for cycles [0, steps); bufs are the AccArgs
-    arrays (numpy uint32, updated in place by the stores)."""
+    arrays (numpy uint32, updated in place by the stores); vals (recursion) the per-cycle
+    FpExt of A.vals, int64 Montgomery words of shape (steps, 4)."""
     cyc = np.arange(steps, dtype=np.int64)
-    v, ib = {}, {}
+    v, ib, rr = {}, {}, {}
     mask = [np.ones(steps, bool)]
     for st in kernel_body(src):
         if _SKIP.match(st):
@@ -88,6 +92,14 @@ def run_kernel(src, bufs, rows, steps):
             mask.append(m_)
         elif kind == "end":
             mask.pop()
+        elif kind == "vread":
+            rr[int(g[0])] = vals.copy()
+        elif kind == "vget":
+            v[int(g[0])] = rr[int(g[1])][:, "xyzw".index(g[2])].copy()
+        elif kind == "vwrite":
+            sel = mask[-1]
+            for k in range(4):
+                vals[sel, k] = v[int(g[k])][sel]
         elif kind == "store":
             b, col, i = int(g[0]), int(g[1]), int(g[2])
             sel = mask[-1]

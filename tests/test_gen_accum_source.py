@@ -47,3 +47,46 @@ def test_generated_source_matches_ir(tmp_path, limit, inv_batch, ahead, rows, la
     assert bad.size == 0, f"{bad.size} words differ; first at col {bad[0] // rows} row {bad[0] % rows}"
     if inv_batch > 1:
         assert any("fp_inv_batch" in k for k in kernels)
+
+
+def _generate_recursion(tmp, ahead):
+    out = os.path.join(tmp, f"rec_{ahead}")
+    subprocess.check_call([sys.executable, os.path.join(ROOT, "tools", "gen_accum.py"), "recursion", out,
+                           "1200", "8", str(ahead)], stdout=subprocess.DEVNULL)
+    launcher = open(os.path.join(out, "accum.hip")).read()
+    fns = {}
+    for name, body in re.findall(r"void recursion_accum_(\w+)\(hipStream_t s, const AccArgs& A\) \{(.*?)\}",
+                                 launcher, re.S):
+        fns[name] = [open(os.path.join(out, f"accum_k{k}.hip")).read()
+                     for k in re.findall(r"launch_k(\d+)\(s, A\);", body)]
+    return fns
+
+
+@pytest.mark.parametrize("ahead", [64, 0])
+def test_generated_recursion_source_matches_ir(tmp_path, oracle, ahead):
+    """Recursion: compute kernels, the FpExt prefix product, verify kernels, from source,
+    equal tests/accum_ir.py's interpretation of the IR (pinned to the compiled reference)."""
+    import accum_ir as A
+    fns = _generate_recursion(str(tmp_path), ahead)
+    d = A.circuit()
+    gs = d["group_sizes"]
+    po2 = 6
+    n = 1 << po2
+    steps = n - 3
+    rng = np.random.default_rng(77 + ahead)
+    ctrl, glob, data, mix = A.synthetic(rng, oracle, po2, gs, d["output_size"], d["mix_size"])
+    acc0 = np.full(gs[0] * n, 0xFFFFFFFF, np.uint32)
+    want = A.accum(ctrl, glob, data, mix, acc0, steps, n)
+    got = acc0.copy()
+    bufs = [ctrl, glob, data, mix, got]
+    vals = np.zeros((steps, 4), np.int64)
+    vals[:, 0] = GS.R
+    for src in fns["compute"]:
+        GS.run_kernel(src, bufs, n, steps, vals)
+    acc = [1, 0, 0, 0]
+    for c in range(steps):  # the inclusive product scan, on plain values
+        acc = A._emul(acc, [int(x) * GS.RINV % GS.P for x in vals[c]])
+        vals[c] = [x * GS.R % GS.P for x in acc]
+    for src in fns["verify"]:
+        GS.run_kernel(src, bufs, n, steps, vals)
+    assert np.array_equal(got, want), int((got != want).sum())
