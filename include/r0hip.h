@@ -120,20 +120,49 @@ const char* r0hip_prove_segment(const char* circuit, int suite, uint32_t po2, co
                                 const uint32_t* d_data, const uint32_t* d_accum, uint32_t* d_global,
                                 int write_version, uint32_t version, uint32_t* h_seal, size_t seal_cap,
                                 size_t* seal_len, uint32_t* h_mix_out);
+/* ---- rv32im BigInt accumulator states (the witness generator's accum injection,
+ * circuit/rv32im/src/prove/witgen/mod.rs:178-205) ----
+ * One Back::BigInt record of the preflight trace (witgen/preflight.rs:55-56, 471-479), holding
+ * the fields of BigIntState (witgen/bigint.rs:36-44) that BigIntAccum::step reads: the cycle
+ * (row), poly_op (PolyOp, bigint.rs:62-70: 0 Reset, 1 Shift, 2 SetTerm, 3 AddTotal, 4 Carry1,
+ * 5 Carry2, 6 EqZero), coeff (BigIntState::coeff = the instruction's coefficient + 4) and the
+ * 16 bytes. Records are passed in trace order (strictly increasing rows). */
+typedef struct r0hip_bigint_back {
+  uint32_t row;
+  uint32_t poly_op;
+  uint32_t coeff;
+  uint8_t bytes[16];
+} r0hip_bigint_back;
+/* BigIntAccum::new(final mix) then ::step per record (witgen/byte_poly.rs:381-470): the state
+ * after each record, 12 Montgomery words (poly, term, total; BigIntAccumState::as_array) per
+ * record into h_states. h_mix is the whole rv32im mix (36 words; the last 4 are the final
+ * mix). Fails as the reference does on an EqZero whose goal is nonzero ("Invalid eqz in
+ * bigint accum"). Host-only. */
+const char* r0hip_rv32im_bigint_accum_states(const uint32_t* h_mix, const r0hip_bigint_back* h_backs, size_t n,
+                                             size_t rows, uint32_t* h_states);
+/* The states above scattered into accum columns 0..11 (BigIntAccumState::offsets,
+ * byte_poly.rs:362-377) of each record's row of d_accum (column-major, `rows` rows): what
+ * WitnessGenerator::accum does before step_accum (witgen/mod.rs:187-205). */
+const char* r0hip_rv32im_bigint_accum_inject(uint32_t* d_accum, size_t rows, const uint32_t* h_mix,
+                                             const r0hip_bigint_back* h_backs, size_t n);
+
 /* ---- whole segment proof with the accumulation on the device: the prove_core sequence above,
  * with the circuit's accumulation between the mix draw and the accum commit, as the reference
  * runs it (rv32im: WitnessGenerator::accum, circuit/rv32im/src/prove/witgen/mod.rs:178-221, over
  * risc0_circuit_rv32im_cuda_accum; recursion: prove/witgen.rs:138-177 over
  * risc0_circuit_recursion_cuda_accum). d_accum is the accum group as the witness generator
  * allocated it: every word INVALID (0xFFFFFFFF), plus for recursion the ZK noise rows the caller
- * draws (witgen.rs:143-158); BigInt back injection (rv32im witgen/mod.rs:187-205) stays the
- * caller's. It is accumulated over work_cycles cycles (rv32im: the preflight cycle count,
- * 2^po2; recursion: work_cycles), INVALID words are zeroized, and the group is committed.
- * The other arguments are r0hip_prove_segment's. */
+ * draws (witgen.rs:143-158). rv32im: h_bigint/n_bigint are the trace's BigInt backs; their
+ * accumulator states, computed with the mix this call draws, are injected before the step
+ * (r0hip_rv32im_bigint_accum_inject; witgen/mod.rs:182-205). Recursion takes none. The group is
+ * accumulated over work_cycles cycles (rv32im: the preflight cycle count, 2^po2; recursion:
+ * work_cycles), INVALID words are zeroized, and the group is committed. The other arguments
+ * are r0hip_prove_segment's. */
 const char* r0hip_prove_segment_accum(const char* circuit, int suite, uint32_t po2, const uint32_t* d_code,
                                       const uint32_t* d_data, uint32_t* d_accum, size_t work_cycles,
-                                      uint32_t* d_global, int write_version, uint32_t version, uint32_t* h_seal,
-                                      size_t seal_cap, size_t* seal_len, uint32_t* h_mix_out);
+                                      const r0hip_bigint_back* h_bigint, size_t n_bigint, uint32_t* d_global,
+                                      int write_version, uint32_t version, uint32_t* h_seal, size_t seal_cap,
+                                      size_t* seal_len, uint32_t* h_mix_out);
 /* ---- rv32im witness side: accumulation phases 2-3 (risc0_circuit_rv32im_cuda_accum after its
  * stepAccum kernel, rv32im-sys/kernels/cuda/ffi.cu:480-509; CPU ffi.cpp:326-360): inclusive
  * prefix sums of the last 4 accum columns over rows [0, last_cycle), then every row adds the
@@ -179,6 +208,8 @@ typedef struct r0hip_segment_job {
   const uint32_t* h_accum;  /* rv32im: NULL = accumulate on the device (as r0hip_prove_segment_accum,
                                work cycles 2^po2); the group then never crosses PCIe */
   const uint32_t* h_global; /* output_size words; zeroized on the device copy only */
+  const r0hip_bigint_back* h_bigint; /* device accumulation only: the trace's BigInt backs, as */
+  size_t n_bigint;                   /* r0hip_prove_segment_accum takes them (NULL, 0 if none) */
   uint32_t* h_seal;
   size_t seal_cap;
   size_t seal_len;

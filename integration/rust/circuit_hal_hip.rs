@@ -4,11 +4,12 @@
 // Both are shown here; split them at the marked line.
 //
 // eval_check runs on the device (r0hip_eval_check: the constraint program generated for
-// gfx950 from the circuit, tools/gen_eval_check.py), and so does the recursion circuit's
-// accumulation (r0hip_recursion_accum). Witness generation of both circuits and the rv32im
-// per-cycle accumulation step stay on the host CPU code of the circuit crates (the same C++
-// the CPU HAL calls), and their results are uploaded once: a GPU stepExec/stepAccum for
-// rv32im is SURVEY.md §8(f) rank 1 and is not part of libr0hip.
+// gfx950 from the circuit, tools/gen_eval_check.py), and so do both circuits' accumulations:
+// rv32im's three phases (r0hip_rv32im_accum: stepAccum generated from the reference's
+// step_TopAccum, the scan and finalizeAccum) and the recursion circuit's
+// (r0hip_recursion_accum). Witness generation (stepExec) of both circuits stays on the host
+// CPU code of the circuit crates (the same C++ the CPU HAL calls), and its result is uploaded
+// once: a GPU stepExec for rv32im is SURVEY.md §8(f) rank 1.
 //
 // Selection (one arm each):
 //   circuit/rv32im/src/prove/mod.rs:45-55       if #[cfg(feature = "hip")] { self::hal::hip::segment_prover() }
@@ -117,8 +118,10 @@ impl<HS: HipHash> CircuitAccumulator<HipHal<HS>> for HipCircuitHal<HS> {
         let cycles = preflight.cycles.len();
         // all three phases of risc0_circuit_rv32im_cuda_accum (ffi.cu:362-514) on the device:
         // the per-cycle stepAccum generated from the reference's step_TopAccum, the scan and
-        // finalizeAccum. `accum` arrives INVALID-filled as the CUDA HAL allocates it; the
-        // accumulation step reads no preflight data.
+        // finalizeAccum. `accum` arrives INVALID-filled as the CUDA HAL allocates it, except
+        // accum columns 0..11 of every BigInt cycle: WitnessGenerator::accum has already
+        // scattered the BigIntAccumState there (witgen/mod.rs:182-205), and the step reads the
+        // previous cycle's state from them at back 1. The step reads no other preflight data.
         assert_eq!(accum.rows, data.rows);
         ffi_wrap(|| unsafe {
             r0hip_rv32im_accum(

@@ -26,6 +26,15 @@ pub const R0HIP_POSEIDON2: c_int = 0;
 pub const R0HIP_SHA256: c_int = 1;
 pub const R0HIP_POSEIDON254: c_int = 2;
 
+/// One Back::BigInt record of the rv32im preflight trace (struct r0hip_bigint_back).
+#[repr(C)]
+pub struct R0HipBigIntBack {
+    pub row: u32,
+    pub poly_op: u32,
+    pub coeff: u32,
+    pub bytes: [u8; 16],
+}
+
 /// One job of r0hip_prove_segments (host witness in, seal out).
 #[repr(C)]
 pub struct R0HipSegmentJob {
@@ -33,6 +42,8 @@ pub struct R0HipSegmentJob {
     pub h_data: *const u32,
     pub h_accum: *const u32,
     pub h_global: *const u32,
+    pub h_bigint: *const R0HipBigIntBack,
+    pub n_bigint: usize,
     pub h_seal: *mut u32,
     pub seal_cap: usize,
     pub seal_len: usize,
@@ -196,6 +207,8 @@ unsafe extern "C" {
         d_data: *const u32,
         d_accum: *mut u32,
         work_cycles: usize,
+        h_bigint: *const R0HipBigIntBack,
+        n_bigint: usize,
         d_global: *mut u32,
         write_version: c_int,
         version: u32,
@@ -203,6 +216,21 @@ unsafe extern "C" {
         seal_cap: usize,
         seal_len: *mut usize,
         h_mix_out: *mut u32,
+    ) -> *const c_char;
+    /// WitnessGenerator::accum's BigInt state injection (witgen/mod.rs:178-205)
+    pub fn r0hip_rv32im_bigint_accum_states(
+        h_mix: *const u32,
+        h_backs: *const R0HipBigIntBack,
+        n: usize,
+        rows: usize,
+        h_states: *mut u32,
+    ) -> *const c_char;
+    pub fn r0hip_rv32im_bigint_accum_inject(
+        d_accum: *mut u32,
+        rows: usize,
+        h_mix: *const u32,
+        h_backs: *const R0HipBigIntBack,
+        n: usize,
     ) -> *const c_char;
     pub fn r0hip_prove_segments(
         circuit: *const c_char,

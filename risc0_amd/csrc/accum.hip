@@ -108,7 +108,26 @@ __global__ __launch_bounds__(kT) void finalize_kernel(uint32_t* accum, uint64_t 
   }
 }
 
+// BigInt accumulator states (bigint.cpp): record k's 12 words into accum columns 0..11 of its
+// row (BigIntAccumState::offsets, rv32im witgen/byte_poly.rs:362-377)
+__global__ __launch_bounds__(kT) void bigint_scatter_kernel(uint32_t* accum, uint64_t rows, const uint32_t* row_of,
+                                                            const uint32_t* states, uint64_t n) {
+  const uint64_t k = uint64_t(blockIdx.x) * kT + threadIdx.x;
+  if (k >= n) return;
+  const uint64_t row = row_of[k];
+#pragma unroll
+  for (int c = 0; c < 12; c++) accum[uint64_t(c) * rows + row] = states[k * 12 + c];
+}
+
 }  // namespace
+
+void bigint_scatter(hipStream_t s, uint32_t* accum, size_t rows, const uint32_t* d_rows, const uint32_t* d_states,
+                    size_t n) {
+  if (n == 0) return;
+  hipLaunchKernelGGL(bigint_scatter_kernel, dim3(div_up(n, kT)), dim3(kT), 0, s, accum, uint64_t(rows), d_rows,
+                     d_states, uint64_t(n));
+  HIP_OK(hipGetLastError());
+}
 
 // The whole accumulation (risc0_circuit_rv32im_cuda_accum, rv32im-sys/kernels/cuda/ffi.cu:
 // 362-514; CPU ffi.cpp:313-368): phase 1 runs the per-cycle step generated from
@@ -143,7 +162,7 @@ void rv32im_accum_finalize(hipStream_t s, uint32_t* accum, size_t rows, size_t c
   const size_t groups = (cols - split) / 4;
   KScope ks("accum_finalize", double(last) * 4 * (4 * 2 + 4 + 8 * 4 * (groups ? groups - 1 : 0)));
   // per-thread scratch, reused only on this thread's stream: no host sync before returning
-  uint32_t* sums = static_cast<uint32_t*>(scratch(size_t(4) * ntiles * 4, 62));
+  uint32_t* sums = static_cast<uint32_t*>(scratch(size_t(4) * ntiles * 4, kSlotAccTileSums));
   hipLaunchKernelGGL(tile_sums_kernel, dim3(ntiles, 4), dim3(kT), 0, s, accum, uint64_t(rows), uint32_t(cols),
                      uint64_t(last), sums, ntiles);
   hipLaunchKernelGGL(scan_sums_kernel, dim3(4), dim3(kT), 0, s, sums, ntiles);

@@ -147,7 +147,7 @@ const char* r0hip_mix_poly_coeffs(uint32_t* d_out, const uint32_t* d_in, const u
                                   size_t count) {
   return wrap([&] {
     std::vector<uint32_t> combos(h_combos, h_combos + input_size);
-    uint32_t* d = static_cast<uint32_t*>(scratch(input_size * 4 + 16, 50));
+    uint32_t* d = static_cast<uint32_t*>(scratch(input_size * 4 + 16, kSlotApiMixWhich));
     upload_async(d, combos.data(), input_size * 4);
     mix_poly_coeffs(stream(), d_out, d_in, d, combos, fe(h_mix_start), fe(h_mix), input_size, count);
   });
@@ -180,7 +180,7 @@ const char* r0hip_combos_prepare(uint32_t* d_combos, const uint32_t* h_coeff_u, 
       pos++;
       cur = fe_mul(cur, mix);
     }
-    uint32_t* dd = static_cast<uint32_t*>(scratch(deltas.size() * 16, 51));
+    uint32_t* dd = static_cast<uint32_t*>(scratch(deltas.size() * 16, kSlotApiDeltas));
     upload_async(dd, deltas.data(), deltas.size() * 16);
     combos_sub(stream(), d_combos, dd, combo_count + 1, width, cycles);
   });
@@ -189,7 +189,7 @@ const char* r0hip_combos_prepare(uint32_t* d_combos, const uint32_t* h_coeff_u, 
 const char* r0hip_poly_divide(uint32_t* d_poly, size_t size, uint32_t* h_remainder, const uint32_t* h_z) {
   return wrap([&] {
     std::vector<std::vector<FpExt>> zs{{fe(h_z)}};
-    uint32_t* rem = static_cast<uint32_t*>(scratch(16, 52));
+    uint32_t* rem = static_cast<uint32_t*>(scratch(16, kSlotApiRem));
     poly_divide_rows(stream(), d_poly, size, zs, rem);
     HIP_OK(hipMemcpyAsync(h_remainder, rem, 16, hipMemcpyDeviceToHost, stream()));
   });
@@ -205,7 +205,7 @@ const char* r0hip_combos_divide(uint32_t* d_combos, size_t nchunks, const uint32
       maxz = std::max(maxz, zs[i].size());
     }
     std::vector<uint32_t> h(nchunks * std::max<size_t>(maxz, 1) * 4, 0);
-    uint32_t* rem = static_cast<uint32_t*>(scratch(h.size() * 4 + 16, 53));
+    uint32_t* rem = static_cast<uint32_t*>(scratch(h.size() * 4 + 16, kSlotApiRems));
     HIP_OK(hipMemsetAsync(rem, 0, h.size() * 4, stream()));
     poly_divide_rows(stream(), d_combos, cycles, zs, rem);
     HIP_OK(hipMemcpyAsync(h.data(), rem, h.size() * 4, hipMemcpyDeviceToHost, stream()));
@@ -257,6 +257,22 @@ const char* r0hip_rv32im_accum_finalize(uint32_t* d_accum, size_t rows, size_t c
 const char* r0hip_rv32im_accum(const uint32_t* d_data, uint32_t* d_accum, const uint32_t* d_global,
                                const uint32_t* d_mix, size_t rows, size_t cols, size_t last_cycle) {
   return wrap([&] { rv32im_accum(stream(), d_data, d_accum, d_global, d_mix, rows, cols, last_cycle); });
+}
+const char* r0hip_rv32im_bigint_accum_states(const uint32_t* h_mix, const r0hip_bigint_back* h_backs, size_t n,
+                                             size_t rows, uint32_t* h_states) {
+  return wrap_nosync([&] {
+    R0_REQUIRE(h_mix && (n == 0 || (h_backs && h_states)), "r0hip_rv32im_bigint_accum_states: null argument");
+    const std::vector<uint32_t> st = rv32im_bigint_accum_states(h_mix, h_backs, n, rows);
+    if (n) memcpy(h_states, st.data(), st.size() * 4);
+  });
+}
+const char* r0hip_rv32im_bigint_accum_inject(uint32_t* d_accum, size_t rows, const uint32_t* h_mix,
+                                             const r0hip_bigint_back* h_backs, size_t n) {
+  return wrap([&] {
+    R0_REQUIRE(d_accum && h_mix, "r0hip_rv32im_bigint_accum_inject: null argument");
+    stage_reset();
+    rv32im_bigint_inject(stream(), d_accum, rows, h_mix, h_backs, n);
+  });
 }
 const char* r0hip_recursion_accum(const uint32_t* d_ctrl, const uint32_t* d_global, const uint32_t* d_data,
                                   const uint32_t* d_mix, uint32_t* d_accum, size_t work_cycles,
@@ -317,13 +333,15 @@ const char* r0hip_prove_segment(const char* circuit, int suite, uint32_t po2, co
 
 const char* r0hip_prove_segment_accum(const char* circuit, int suite, uint32_t po2, const uint32_t* d_code,
                                       const uint32_t* d_data, uint32_t* d_accum, size_t work_cycles,
-                                      uint32_t* d_global, int write_version, uint32_t version, uint32_t* h_seal,
-                                      size_t seal_cap, size_t* seal_len, uint32_t* h_mix_out) {
+                                      const r0hip_bigint_back* h_bigint, size_t n_bigint, uint32_t* d_global,
+                                      int write_version, uint32_t version, uint32_t* h_seal, size_t seal_cap,
+                                      size_t* seal_len, uint32_t* h_mix_out) {
   return wrap([&] {
     const CircuitDef* c = find_circuit(circuit ? circuit : "");
     R0_REQUIRE(c, std::string("unknown circuit ") + (circuit ? circuit : "(null)"));
+    R0_REQUIRE(n_bigint == 0 || h_bigint, "prove_segment_accum: h_bigint is NULL with n_bigint > 0");
     std::vector<uint32_t> mix;
-    const AccumStep acc{d_accum, work_cycles};
+    const AccumStep acc{d_accum, work_cycles, false, h_bigint, n_bigint};
     std::vector<uint32_t> seal = prove_segment(*c, suite, po2, d_code, d_data, nullptr, d_global, write_version != 0,
                                                version, &mix, nullptr, &acc);
     if (seal_len) *seal_len = seal.size();

@@ -519,10 +519,10 @@ void mix_poly_coeffs(hipStream_t s, uint32_t* out, const uint32_t* in, const uin
     seg_combo.push_back(k);
   }
   (void)combos_dev;  // the device copy of the ids is the ABI's; the sorted tables replace it
-  uint32_t* d_rows = static_cast<uint32_t*>(scratch(rows.size() * 4, 40));
-  uint32_t* d_pows = static_cast<uint32_t*>(scratch(pows.size() * 4, 41));
-  uint32_t* d_seg = static_cast<uint32_t*>(scratch(seg.size() * 4, 42));
-  uint32_t* d_seg_combo = static_cast<uint32_t*>(scratch(seg_combo.size() * 4, 43));
+  uint32_t* d_rows = static_cast<uint32_t*>(scratch(rows.size() * 4, kSlotMixRows));
+  uint32_t* d_pows = static_cast<uint32_t*>(scratch(pows.size() * 4, kSlotMixPows));
+  uint32_t* d_seg = static_cast<uint32_t*>(scratch(seg.size() * 4, kSlotMixSeg));
+  uint32_t* d_seg_combo = static_cast<uint32_t*>(scratch(seg_combo.size() * 4, kSlotMixSegCombo));
   upload_async(d_rows, rows.data(), rows.size() * 4);
   upload_async(d_pows, pows.data(), pows.size() * 4);
   upload_async(d_seg, seg.data(), seg.size() * 4);
@@ -554,14 +554,14 @@ void batch_evaluate_any_host(hipStream_t s, const uint32_t* coeffs, size_t poly_
   // one read of each evaluated polynomial; per coefficient and evaluation 4 products
   KScope ks("batch_evaluate_any", double(groups.size()) * n * 4, double(eval_count) * n * 4);
   R0_REQUIRE(groups.size() < 65536, "batch_evaluate_any: too many polynomials");
-  uint32_t* d_gpoly = static_cast<uint32_t*>(scratch(gpoly.size() * 4, 9));
-  uint32_t* d_gbegin = static_cast<uint32_t*>(scratch(gbegin.size() * 4, 10));
-  uint32_t* d_geval = static_cast<uint32_t*>(scratch(geval.size() * 4, 11));
+  uint32_t* d_gpoly = static_cast<uint32_t*>(scratch(gpoly.size() * 4, kSlotEvalPoly));
+  uint32_t* d_gbegin = static_cast<uint32_t*>(scratch(gbegin.size() * 4, kSlotEvalBegin));
+  uint32_t* d_geval = static_cast<uint32_t*>(scratch(geval.size() * 4, kSlotEvalIdx));
   upload_async(d_gpoly, gpoly.data(), gpoly.size() * 4);
   upload_async(d_gbegin, gbegin.data(), gbegin.size() * 4);
   upload_async(d_geval, geval.data(), geval.size() * 4);
-  uint32_t* tab = static_cast<uint32_t*>(scratch(eval_count * kEvTab * 16, 12));
-  uint32_t* partial = static_cast<uint32_t*>(scratch(eval_count * npieces * 16, 2));
+  uint32_t* tab = static_cast<uint32_t*>(scratch(eval_count * kEvTab * 16, kSlotEvalTable));
+  uint32_t* partial = static_cast<uint32_t*>(scratch(eval_count * npieces * 16, kSlotEvalPartial));
   hipLaunchKernelGGL(eval_tables_kernel, dim3(div_up(eval_count * kEvTab, kThreads)), dim3(kThreads), 0, s, xs,
                      uint32_t(eval_count), tab);
   HIP_OK(hipGetLastError());
@@ -601,9 +601,9 @@ void poly_divide_rows(hipStream_t s, uint32_t* io, size_t n, const std::vector<s
         ids.push_back(uint32_t(r));
       }
     uint32_t nr = uint32_t(rs.size());
-    DivRow* drows = static_cast<DivRow*>(scratch(rs.size() * sizeof(DivRow), 3 + int(k % 2) * 100));
+    DivRow* drows = static_cast<DivRow*>(scratch(rs.size() * sizeof(DivRow), k % 2 ? kSlotDivRowsAlt : kSlotDivRows));
     upload_async(drows, rs.data(), rs.size() * sizeof(DivRow));
-    uint32_t* rem = static_cast<uint32_t*>(scratch(size_t(nr) * 16, 4));
+    uint32_t* rem = static_cast<uint32_t*>(scratch(size_t(nr) * 16, kSlotDivRem));
     if (n % kDivPer != 0) {
       hipLaunchKernelGGL(div_serial_kernel, dim3(div_up(nr, kThreads)), dim3(kThreads), 0, s, drows, uint64_t(n),
                          rem, nr);
@@ -611,10 +611,10 @@ void poly_divide_rows(hipStream_t s, uint32_t* io, size_t n, const std::vector<s
     } else {
       uint32_t nlanes = uint32_t(n / kDivPer);
       uint32_t nblocks = div_up(nlanes, kThreads);
-      uint32_t* lanev = static_cast<uint32_t*>(scratch(size_t(nr) * nlanes * 16, 5));
-      uint32_t* lanem = static_cast<uint32_t*>(scratch(size_t(nr) * nlanes * 16, 6));
-      uint32_t* blockv = static_cast<uint32_t*>(scratch(size_t(nr) * nblocks * 16, 7));
-      uint32_t* blockm = static_cast<uint32_t*>(scratch(size_t(nr) * nblocks * 16, 8));
+      uint32_t* lanev = static_cast<uint32_t*>(scratch(size_t(nr) * nlanes * 16, kSlotDivLaneV));
+      uint32_t* lanem = static_cast<uint32_t*>(scratch(size_t(nr) * nlanes * 16, kSlotDivLaneM));
+      uint32_t* blockv = static_cast<uint32_t*>(scratch(size_t(nr) * nblocks * 16, kSlotDivBlockV));
+      uint32_t* blockm = static_cast<uint32_t*>(scratch(size_t(nr) * nblocks * 16, kSlotDivBlockM));
       hipLaunchKernelGGL(div_local_kernel, dim3(nblocks, nr), dim3(kThreads), 0, s, drows, nlanes, lanev);
       HIP_OK(hipGetLastError());
       hipLaunchKernelGGL(div_block_kernel, dim3(nblocks, nr), dim3(kThreads), 0, s, drows, nlanes, lanev, lanem,

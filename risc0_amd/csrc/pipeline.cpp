@@ -172,6 +172,10 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
         bool null_group = false;
         for (int g = 0; g < 4; g++) null_group |= !src[g] && !(g == 2 && dev_accum);
         if (null_group) jobs[i].error = dup_msg("witness group pointer is NULL");  // before the hand-over
+        else if (jobs[i].n_bigint && (!dev_accum || !jobs[i].h_bigint))
+          // the states need the mix drawn inside the proof: only a device accumulation takes them
+          jobs[i].error = dup_msg("BigInt backs given without a device accumulation (h_accum must be NULL, rv32im)");
+        null_group |= jobs[i].error != nullptr;
         ready_q.put(s);  // a prover may start now; it waits per group (BufSet::wait)
         if (null_group) {
           b.mark_all();
@@ -199,9 +203,16 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
             std::lock_guard<std::mutex> lk(b.mu);
             if (!jobs[i].error) jobs[i].error = dup_msg(e.what());
           }
+          // the job's earlier chunks may still be copying: no prover waits on them now, and
+          // the set goes back to the free queue once the prover sees the error
+          drain_after_error();
           b.mark_all();  // release a waiting prover; the job reports the error
         }
       }
+      // every copy done before the call can return: a prover that failed early never waited
+      // on its job's events, and the caller may free its host buffers once we return (free
+      // on the success path, where every event was waited on)
+      drain_after_error();
       for (size_t t = 0; t < k; t++) ready_q.put(-1);  // one stop token per prover
     });
 
@@ -223,7 +234,7 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
               ensure_init();
               std::vector<uint32_t> mix;
               const bool dev_accum = !j.h_accum;  // (rv32im only: checked by the uploader)
-              const AccumStep acc{b.g[2].p, n, true};
+              const AccumStep acc{b.g[2].p, n, true, j.h_bigint, j.n_bigint};
               std::vector<uint32_t> seal =
                   prove_segment(*c, suite, po2, b.g[0].p, b.g[1].p, dev_accum ? nullptr : b.g[2].p, b.g[3].p,
                                 write_version != 0, version, &mix, &b, dev_accum ? &acc : nullptr);

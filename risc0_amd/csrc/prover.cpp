@@ -243,15 +243,15 @@ void run_eval_check(const CircuitDef& c, uint32_t* check, const uint32_t* const*
   // one base pointer per column the generated program reads (saddr-form tap loads)
   std::vector<const uint32_t*> colptr(info.ncols);
   for (int i = 0; i < info.ncols; i++) colptr[i] = args[info.col_arg[i]] + size_t(info.col_idx[i]) * domain;
-  e.colptr = reinterpret_cast<const uint32_t* const*>(upload(colptr, 26));
-  e.poly_mix = upload(pm, 20);
+  e.colptr = reinterpret_cast<const uint32_t* const*>(upload(colptr, kSlotEcColPtr));
+  e.poly_mix = upload(pm, kSlotEcPolyMix);
   std::vector<FpExt> pmn(pm.size());
   for (size_t i = 0; i < pm.size(); i++) pmn[i] = fe_mul_fp(pm[i], kNBeta);
-  e.poly_mix_nb = upload(pmn, 25);
-  e.vinv = upload(vinv, 21);
-  e.acc = static_cast<uint32_t*>(scratch(domain * 16, 22));
-  e.mat_fp = static_cast<uint32_t*>(scratch(size_t(info.mat_fp) * domain * 4 + 16, 23));
-  e.mat_ext = static_cast<uint32_t*>(scratch(size_t(info.mat_ext) * domain * 16 + 16, 24));
+  e.poly_mix_nb = upload(pmn, kSlotEcPolyMixNb);
+  e.vinv = upload(vinv, kSlotEcVinv);
+  e.acc = static_cast<uint32_t*>(scratch(domain * 16, kSlotEcAcc));
+  e.mat_fp = static_cast<uint32_t*>(scratch(size_t(info.mat_fp) * domain * 4 + 16, kSlotEcMatFp));
+  e.mat_ext = static_cast<uint32_t*>(scratch(size_t(info.mat_ext) * domain * 16 + 16, kSlotEcMatExt));
   e.check = check;
   e.domain = uint32_t(domain);
   {
@@ -353,7 +353,7 @@ struct Prover {
       DevBuf out((total + CHECK_SIZE) * 4);
       size_t off = 0;
       for (size_t id = 0; id < 3; id++) {
-        uint32_t* dx = upload(xss[id], 33 + int(id));
+        uint32_t* dx = upload(xss[id], kSlotTapXs + int(id));
         batch_evaluate_any_host(s, groups[id]->coeffs.p, groups[id]->count, uint32_t(po2), whichs[id], dx,
                                 out.p + off * 4);
         off += whichs[id].size();
@@ -377,7 +377,7 @@ struct Prover {
       for (size_t i = 0; i < CHECK_SIZE; i++) which[i] = uint32_t(i);
       std::vector<FpExt> xs(CHECK_SIZE, z_pow);
       DevBuf out(CHECK_SIZE * 4);
-      batch_evaluate_any_host(s, check_group.coeffs.p, CHECK_SIZE, uint32_t(po2), which, upload(xs, 37), out.p);
+      batch_evaluate_any_host(s, check_group.coeffs.p, CHECK_SIZE, uint32_t(po2), which, upload(xs, kSlotCheckXs), out.p);
       std::vector<uint32_t> h(CHECK_SIZE * 4);
       d2h(h.data(), out.p, h.size() * 4);
       for (size_t i = 0; i < CHECK_SIZE; i++) coeff_u.push_back(fe_from_words(&h[4 * i]));
@@ -398,11 +398,11 @@ struct Prover {
         std::vector<uint32_t> which;
         c.regs(c.group_begin[id], c.group_begin[id + 1], [&](size_t cur) { which.push_back(c.tap(cur).combo); });
         R0_REQUIRE(which.size() == gs, "group registers != group size");
-        mix_poly_coeffs(s, combos.p, groups[id]->coeffs.p, upload(which, 38), which, cur_mix, mix_fri, gs, cycles);
+        mix_poly_coeffs(s, combos.p, groups[id]->coeffs.p, upload(which, kSlotMixWhich), which, cur_mix, mix_fri, gs, cycles);
         cur_mix = fe_mul(cur_mix, fe_pow(mix_fri, gs));
       }
       std::vector<uint32_t> which(CHECK_SIZE, uint32_t(combo_count));
-      mix_poly_coeffs(s, combos.p, check_group.coeffs.p, upload(which, 39), which, cur_mix, mix_fri, CHECK_SIZE,
+      mix_poly_coeffs(s, combos.p, check_group.coeffs.p, upload(which, kSlotMixWhichCheck), which, cur_mix, mix_fri, CHECK_SIZE,
                       cycles);
     }
     if (prof) prof->mark("mix");
@@ -426,7 +426,7 @@ struct Prover {
         cur_pos++;
         cur = fe_mul(cur, mix_fri);
       }
-      combos_sub(s, combos.p, upload(deltas, 40), combo_count + 1, width, cycles);
+      combos_sub(s, combos.p, upload(deltas, kSlotCombosDeltas), combo_count + 1, width, cycles);
       // combos_divide (hal/mod.rs:236-257; cuda.rs:1034-1048)
       std::vector<std::vector<FpExt>> zs(combo_count + 1);
       for (size_t i = 0; i < combo_count; i++)
@@ -534,8 +534,8 @@ struct Prover {
       }
     }
     DevBuf words(offs.size());
-    const uint32_t* const* dbases = reinterpret_cast<const uint32_t* const*>(upload(bases, 41));
-    gather_words(s, words.p, dbases, upload(base_id, 42), reinterpret_cast<const uint64_t*>(upload(offs, 43)),
+    const uint32_t* const* dbases = reinterpret_cast<const uint32_t* const*>(upload(bases, kSlotQueryBases));
+    gather_words(s, words.p, dbases, upload(base_id, kSlotQueryIds), reinterpret_cast<const uint64_t*>(upload(offs, kSlotQueryOffs)),
                  offs.size());
     std::vector<uint32_t> h(offs.size());
     d2h(h.data(), words.p, h.size() * 4);
@@ -612,8 +612,11 @@ std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2
     const std::string name = c.name;
     if (acc->fill_invalid) HIP_OK(hipMemsetD32Async(acc->accum, 0xFFFFFFFFu, rows * cols, s));
     if (name == "rv32im") {
+      // witgen/mod.rs:182-205: the BigInt states with the final mix, then the step
+      rv32im_bigint_inject(s, acc->accum, rows, mix.data(), acc->bigint, acc->n_bigint);
       rv32im_accum(s, data, acc->accum, global, dmix.p, rows, cols, acc->work_cycles);
     } else if (name == "recursion") {
+      R0_REQUIRE(acc->n_bigint == 0, "prove_segment: BigInt backs are an rv32im trace record");
       recursion_accum(s, code, global, data, dmix.p, acc->accum, acc->work_cycles, rows);
     } else {
       R0_REQUIRE(false, "prove_segment: no device accumulation for circuit " + name);

@@ -121,9 +121,9 @@ void recursion_accum(hipStream_t s, const uint32_t* ctrl, const uint32_t* global
              "recursion_accum: cycles must be a power of two in [4, 2^26]");
   R0_REQUIRE(steps >= 1 && steps <= cycles, "recursion_accum: need 1 <= steps <= cycles");
   KScope ks("recursion_accum", double(steps) * (23 + 128 + 12 + 8) * 4);
-  uint4* vals = static_cast<uint4*>(scratch(steps * 16, 60));
+  uint4* vals = static_cast<uint4*>(scratch(steps * 16, kSlotRecAccVals));
   const uint32_t ntiles = uint32_t((steps + kTile - 1) / kTile);
-  uint4* prods = static_cast<uint4*>(scratch(size_t(ntiles) * 16, 61));
+  uint4* prods = static_cast<uint4*>(scratch(size_t(ntiles) * 16, kSlotRecAccProds));
   hipLaunchKernelGGL(fill_one_kernel, dim3(div_up(steps, kT)), dim3(kT), 0, s, vals, uint64_t(steps));
   HIP_OK(hipGetLastError());
   AccArgs A;

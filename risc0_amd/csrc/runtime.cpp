@@ -197,7 +197,10 @@ void* scratch(size_t bytes, int slot) {
       std::lock_guard<std::mutex> lk(g_mu);
       auto& orph = g_scratch_orphans[slot];
       auto ot = orph.lower_bound(bytes);
-      if (ot != orph.end()) {
+      // at most twice the block this request would allocate: a po2=10 proof must not pin a
+      // po2=24 block (it would stay live and count in mem_stats); the bench's threads ask
+      // for identical sizes, so they still find theirs
+      if (ot != orph.end() && ot->first <= 2 * want) {
         s.p = ot->second;
         want = ot->first;
         orph.erase(ot);

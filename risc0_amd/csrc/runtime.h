@@ -13,6 +13,8 @@
 
 #include "bb31.h"
 
+struct r0hip_bigint_back;  // include/r0hip.h
+
 #define HIP_OK(expr)                                                                          \
   do {                                                                                        \
     hipError_t e_ = (expr);                                                                   \
@@ -36,8 +38,63 @@ void ensure_init();
 // string; `gen` runs on the host once per key.
 const uint32_t* dev_table(const std::string& key, const std::function<std::vector<uint32_t>()>& gen);
 
+// Per-thread scratch slots. A slot is one buffer reused across calls in stream order (a
+// later use on the thread's stream runs after every earlier kernel that read it); two
+// buffers that are live at the same time need two slots. Every slot id is named here.
+enum ScratchSlot : int {
+  kSlotDefault = 0,
+  // batch_evaluate_any (eltwise.hip)
+  kSlotEvalPartial = 2,
+  kSlotEvalPoly = 9,
+  kSlotEvalBegin = 10,
+  kSlotEvalIdx = 11,
+  kSlotEvalTable = 12,
+  // poly_divide_rows (eltwise.hip): row tables alternate between two slots per batch
+  kSlotDivRows = 3,
+  kSlotDivRowsAlt = 103,
+  kSlotDivRem = 4,
+  kSlotDivLaneV = 5,
+  kSlotDivLaneM = 6,
+  kSlotDivBlockV = 7,
+  kSlotDivBlockM = 8,
+  // eval_check (prover.cpp)
+  kSlotEcPolyMix = 20,
+  kSlotEcVinv = 21,
+  kSlotEcAcc = 22,
+  kSlotEcMatFp = 23,
+  kSlotEcMatExt = 24,
+  kSlotEcPolyMixNb = 25,
+  kSlotEcColPtr = 26,
+  // prover uploads (prover.cpp): evaluation points per group (3 groups), check points,
+  // mix_poly_coeffs row lists, combos deltas, query gather tables
+  kSlotTapXs = 33,  // .. 35
+  kSlotCheckXs = 37,
+  kSlotMixWhich = 38,
+  kSlotMixWhichCheck = 39,
+  kSlotCombosDeltas = 44,
+  kSlotQueryBases = 45,
+  kSlotQueryIds = 46,
+  kSlotQueryOffs = 47,
+  // mix_poly_coeffs (eltwise.hip)
+  kSlotMixRows = 40,
+  kSlotMixPows = 41,
+  kSlotMixSeg = 42,
+  kSlotMixSegCombo = 43,
+  // per-op ABI (api.cpp)
+  kSlotApiMixWhich = 50,
+  kSlotApiDeltas = 51,
+  kSlotApiRem = 52,
+  kSlotApiRems = 53,
+  // accumulation (recursion_accum.hip, accum.hip, bigint.cpp)
+  kSlotRecAccVals = 60,
+  kSlotRecAccProds = 61,
+  kSlotAccTileSums = 62,
+  kSlotBigIntRows = 63,
+  kSlotBigIntStates = 64,
+};
+
 // Scratch buffer reused across calls (grown on demand; stream-ordered use only).
-void* scratch(size_t bytes, int slot = 0);
+void* scratch(size_t bytes, int slot = kSlotDefault);
 // After an error: wait for whatever this thread already queued on its stream (ignoring the
 // status), so no buffer is reused or handed to another thread while kernels still use it.
 // Only a thread that has a stream drains; it never creates one.
@@ -147,7 +204,20 @@ struct AccumStep {
   uint32_t* accum;
   size_t work_cycles;
   bool fill_invalid = false;  // the buffer is reused: fill it with INVALID words first
+  // rv32im: the trace's Back::BigInt records, whose accumulator states are injected with the
+  // final mix before the step (witgen/mod.rs:178-205)
+  const r0hip_bigint_back* bigint = nullptr;
+  size_t n_bigint = 0;
 };
+// BigIntAccum::step over the records (byte_poly.rs:403-470): 12 words per record (poly, term,
+// total), in record order; throws on an invalid EqZero as the reference does
+std::vector<uint32_t> rv32im_bigint_accum_states(const uint32_t* mix, const r0hip_bigint_back* backs, size_t n,
+                                                 size_t rows);
+// the states scattered into accum columns 0..11 of each record's row (witgen/mod.rs:187-205)
+void rv32im_bigint_inject(hipStream_t s, uint32_t* accum, size_t rows, const uint32_t* mix,
+                          const r0hip_bigint_back* backs, size_t n);
+void bigint_scatter(hipStream_t s, uint32_t* accum, size_t rows, const uint32_t* d_rows, const uint32_t* d_states,
+                    size_t n);
 // recursion circuit accumulation (recursion_accum.hip): compute, prefix product, verify
 void recursion_accum(hipStream_t s, const uint32_t* ctrl, const uint32_t* global, const uint32_t* data,
                      const uint32_t* mix, uint32_t* accum, size_t steps, size_t cycles);

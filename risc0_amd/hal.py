@@ -85,8 +85,10 @@ def _declare(L):
         "r0hip_eval_check": [C.c_char_p, vp, C.POINTER(vp), vp, vp, u32p, C.c_uint32],
         "r0hip_prove_segment": [C.c_char_p, C.c_int, C.c_uint32, vp, vp, vp, vp, C.c_int, C.c_uint32, u32p, sz,
                                 C.POINTER(sz), u32p],
-        "r0hip_prove_segment_accum": [C.c_char_p, C.c_int, C.c_uint32, vp, vp, vp, sz, vp, C.c_int, C.c_uint32,
-                                      u32p, sz, C.POINTER(sz), u32p],
+        "r0hip_prove_segment_accum": [C.c_char_p, C.c_int, C.c_uint32, vp, vp, vp, sz, vp, sz, vp, C.c_int,
+                                      C.c_uint32, u32p, sz, C.POINTER(sz), u32p],
+        "r0hip_rv32im_bigint_accum_states": [u32p, vp, sz, sz, u32p],
+        "r0hip_rv32im_bigint_accum_inject": [vp, sz, u32p, vp, sz],
         "r0hip_last_profile": [C.c_char_p, sz],
         "r0hip_set_kernel_timing": [C.c_int],
         "r0hip_kernel_times": [C.c_char_p, sz],
@@ -349,10 +351,52 @@ def prove_segment(hal, circuit, po2, code, data, accum, glob, version=None, seal
     return seal[: n.value].copy(), mix
 
 
-def prove_segment_accum(hal, circuit, po2, code, data, accum, work_cycles, glob, version=None, seal_cap=1 << 24):
+class BigIntBack(C.Structure):
+    """struct r0hip_bigint_back (include/r0hip.h): one Back::BigInt record of the rv32im
+    preflight trace (witgen/preflight.rs:55-56; BigIntState, witgen/bigint.rs:36-44)"""
+    _fields_ = [("row", C.c_uint32), ("poly_op", C.c_uint32), ("coeff", C.c_uint32), ("bytes", C.c_uint8 * 16)]
+
+
+def bigint_backs(records):
+    """ctypes array of BigIntBack from [(row, poly_op, coeff, bytes16), ...] (None/[] -> None)"""
+    if records is None or len(records) == 0:
+        return None
+    arr = (BigIntBack * len(records))()
+    for a, (row, op, coeff, by) in zip(arr, records):
+        a.row, a.poly_op, a.coeff = int(row), int(op), int(coeff)
+        for i, b in enumerate(by):
+            a.bytes[i] = int(b)
+    return arr
+
+
+def bigint_accum_states(mix, records, rows):
+    """r0hip_rv32im_bigint_accum_states (host-only): BigIntAccum::step over the records with the
+    final mix (byte_poly.rs:381-470); returns (len(records), 12) Montgomery words"""
+    arr = bigint_backs(records)
+    n = 0 if arr is None else len(arr)
+    m, mp = _h(mix)
+    out = np.zeros(max(1, n * 12), np.uint32)
+    check(lib().r0hip_rv32im_bigint_accum_states(mp, None if arr is None else C.cast(arr, C.c_void_p), n, rows,
+                                                 out.ctypes.data_as(u32p)))
+    return out[: n * 12].reshape(n, 12)
+
+
+def bigint_accum_inject(accum, rows, mix, records):
+    """r0hip_rv32im_bigint_accum_inject: the states scattered into accum columns 0..11"""
+    arr = bigint_backs(records)
+    m, mp = _h(mix)
+    check(lib().r0hip_rv32im_bigint_accum_inject(accum.ptr, rows, mp, None if arr is None else C.cast(arr, C.c_void_p),
+                                                 0 if arr is None else len(arr)))
+
+
+def prove_segment_accum(hal, circuit, po2, code, data, accum, work_cycles, glob, version=None, seal_cap=1 << 24,
+                        bigint=None):
     """Prove one segment with the circuit's accumulation on the device between the mix draw and
     the accum commit (r0hip_prove_segment_accum): `accum` holds the group as the witness
-    generator allocated it (INVALID words) and is filled in place. Returns (seal, mix)."""
+    generator allocated it (INVALID words) and is filled in place; `bigint` (rv32im) is the
+    trace's BigInt backs [(row, poly_op, coeff, bytes16)], injected with the drawn mix.
+    Returns (seal, mix)."""
+    backs = bigint_backs(bigint)
     from json import load
     with open(os.path.join(_HERE, "circuits", circuit + ".taps.json")) as f:
         mix_size = load(f)["mix_size"]
@@ -360,7 +404,9 @@ def prove_segment_accum(hal, circuit, po2, code, data, accum, work_cycles, glob,
     n = C.c_size_t(0)
     mix = np.zeros(mix_size, dtype=np.uint32)
     check(lib().r0hip_prove_segment_accum(circuit.encode(), hal.suite, po2, code.ptr, data.ptr, accum.ptr,
-                                          work_cycles, glob.ptr, int(version is not None), version or 0,
+                                          work_cycles, None if backs is None else C.cast(backs, C.c_void_p),
+                                          0 if backs is None else len(backs), glob.ptr, int(version is not None),
+                                          version or 0,
                                           seal.ctypes.data_as(u32p), seal_cap, C.byref(n),
                                           mix.ctypes.data_as(u32p)))
     return seal[: n.value].copy(), mix
@@ -369,7 +415,7 @@ def prove_segment_accum(hal, circuit, po2, code, data, accum, work_cycles, glob,
 class SegmentJob(C.Structure):
     """struct r0hip_segment_job (include/r0hip.h)"""
     _fields_ = [("h_code", C.c_void_p), ("h_data", C.c_void_p), ("h_accum", C.c_void_p), ("h_global", C.c_void_p),
-                ("h_seal", C.c_void_p),
+                ("h_bigint", C.c_void_p), ("n_bigint", C.c_size_t), ("h_seal", C.c_void_p),
                 ("seal_cap", C.c_size_t), ("seal_len", C.c_size_t), ("h_mix_out", C.c_void_p), ("error", C.c_void_p)]
 
 
@@ -378,7 +424,8 @@ def prove_segments(hal, circuit, po2, witnesses, version=None, in_flight=2, seal
     (code, data, accum, global) host arrays (numpy uint32, ideally views of page-locked
     memory) or raw host pointers; returns [(seal, mix)] in job order. For rv32im, accum may
     be None: the prover then runs the accumulation on the device (r0hip_prove_segment_accum's
-    path) and nothing of that group crosses PCIe."""
+    path) and nothing of that group crosses PCIe; a 5th element then gives the job's BigInt
+    backs [(row, poly_op, coeff, bytes16)]."""
     from json import load
     with open(os.path.join(_HERE, "circuits", circuit + ".taps.json")) as f:
         mix_size = load(f)["mix_size"]
@@ -386,7 +433,11 @@ def prove_segments(hal, circuit, po2, witnesses, version=None, in_flight=2, seal
     keep, seals, mixes = [], [], []
     for j, w in zip(jobs, witnesses):
         ptrs = []
-        for a in w:
+        backs = bigint_backs(w[4]) if len(w) > 4 else None
+        if backs is not None:
+            keep.append(backs)
+            j.h_bigint, j.n_bigint = C.cast(backs, C.c_void_p).value, len(backs)
+        for a in w[:4]:
             if isinstance(a, np.ndarray):
                 a = np.ascontiguousarray(a, dtype=np.uint32)
                 keep.append(a)

@@ -53,14 +53,19 @@ def _check(err):
         raise RuntimeError(C.cast(err, C.c_char_p).value.decode())
 
 
-def accum(data, glob, mix, rows, last_cycle, phase1_only=False):
+def accum(data, glob, mix, rows, last_cycle, phase1_only=False, accum_init=None):
     """Accum group (column-major, ACCUM_COLS x rows, raw Montgomery words) the reference
     computes from `data` (DATA_COLS x rows), starting from an all-INVALID buffer as the
-    prover allocates it."""
+    prover allocates it, or from `accum_init` (e.g. with the BigInt states injected, as
+    WitnessGenerator::accum hands it to step_accum, witgen/mod.rs:187-215)."""
     data = np.ascontiguousarray(data, np.uint32)
     glob = np.ascontiguousarray(glob, np.uint32)
     mix = np.ascontiguousarray(mix, np.uint32)
-    out = np.full(ACCUM_COLS * rows, INVALID, np.uint32)
+    if accum_init is None:
+        out = np.full(ACCUM_COLS * rows, INVALID, np.uint32)
+    else:
+        out = np.array(accum_init, dtype=np.uint32).reshape(-1)
+        assert out.size == ACCUM_COLS * rows
     bufs = _buffers(data, out, glob, mix, rows)
     lib = _lib()
     if phase1_only:

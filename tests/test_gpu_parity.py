@@ -841,3 +841,133 @@ def test_prove_segments_device_accum_matches_fused(hal, hal_sha, oracle, suite, 
     for (s1, m1), (s2, m2) in zip(got, want):
         assert np.array_equal(m1, m2)
         assert np.array_equal(s1, s2)
+
+
+# ---- rv32im BigInt cycles: the accumulator states WitnessGenerator::accum injects with the
+# final mix before the step (witgen/mod.rs:178-205; tests/bigint_accum.py) ----
+
+def _bigint_witness(po2, seed, calls):
+    import bigint_accum as B
+    rng = np.random.default_rng(seed)
+    n = 1 << po2
+    data, recs = B.lay_out(rng, n, calls)
+    return rng, data, recs
+
+
+@pytest.mark.parametrize("po2,calls", [(10, 60), (20, 1500)])
+def test_rv32im_accum_bigint_matches_reference(hal, po2, calls):
+    """r0hip_rv32im_bigint_accum_inject + r0hip_rv32im_accum against the compiled reference
+    accumulation (risc0_circuit_rv32im_cpu_accum) on rows whose arm-12 cycles run every PolyOp,
+    both starting from the group with the reference's injected states. Without the injection
+    the device result differs (the step reads the previous cycle's state at back 1)."""
+    import risc0_amd as r
+    import bigint_accum as B
+    import rv32im_accum_ref as R
+    if not R.available():
+        pytest.skip("oracle/_ref/libref_rv32im_accum.so not built")
+    n = 1 << po2
+    rng, data, recs = _bigint_witness(po2, 0xB1 + po2, calls)
+    assert {rec[1] for rec in recs} == set(range(7))
+    glob = rng.integers(0, R.P, R.GLOBAL_WORDS, dtype=np.uint64).astype(np.uint32)
+    mix = rng.integers(0, R.P, R.MIX_WORDS, dtype=np.uint64).astype(np.uint32)
+    acc0 = np.full(R.ACCUM_COLS * n, R.INVALID, np.uint32)
+    ref = R.accum(data, glob, mix, n, n, accum_init=B.inject(acc0.copy(), n, mix, recs))
+    dd, dg, dm = dev(hal, data), dev(hal, glob), dev(hal, mix)
+    d_acc = dev(hal, acc0)
+    r.bigint_accum_inject(d_acc, n, mix, recs)
+    hal.rv32im_accum(dd, d_acc, dg, dm, n, n)
+    got = d_acc.to_numpy()
+    bad = np.nonzero(got != ref)[0]
+    assert bad.size == 0, f"{bad.size} words differ, first at column {bad[0] // n} row {bad[0] % n}"
+    if po2 <= 12:
+        d_plain = dev(hal, acc0)
+        hal.rv32im_accum(dd, d_plain, dg, dm, n, n)
+        assert not np.array_equal(d_plain.to_numpy(), ref)
+
+
+@pytest.mark.parametrize("suite,po2,calls", [("poseidon2", 10, 60), ("sha-256", 9, 30), ("poseidon2", 20, 1500)])
+def test_prove_segment_accum_bigint_matches_reference(hal, hal_sha, oracle, suite, po2, calls):
+    """r0hip_prove_segment_accum with the trace's BigInt backs: the states are computed with
+    the mix the transcript draws inside the call and injected before the step. The device
+    accum group equals the compiled reference accumulation on the same rows with the
+    reference's injection; the seal equals the oracle prover's on that group (po2 <= 12), and
+    at po2 20 the seal passes the verifier's structural checks."""
+    import risc0_amd as r
+    import bigint_accum as B
+    import rv32im_accum_ref as R
+    if oracle.ref_lib() is None or not R.available():
+        pytest.skip("oracle/_ref not built")
+    h, s = H(suite), S(oracle, suite)
+    d = oracle.load_circuit_json("rv32im")
+    n = 1 << po2
+    rng, data, recs = _bigint_witness(po2, 0xB2 + po2, calls)
+    code = oracle.rand_elems(rng, d["group_sizes"][1] * n)
+    glob = oracle.rand_elems(rng, d["output_size"])
+    acc0 = np.full(d["group_sizes"][0] * n, R.INVALID, np.uint32)
+    dacc = dev(h, acc0)
+    seal, mix = r.prove_segment_accum(h, "rv32im", po2, dev(h, code), dev(h, data), dacc, n, dev(h, glob),
+                                      version=2, bigint=recs)
+    glob_z = np.where(glob == R.INVALID, 0, glob).astype(np.uint32)
+    ref_acc = R.accum(data, glob_z, mix, n, n, accum_init=B.inject(acc0.copy(), n, mix, recs))
+    ref_acc = np.where(ref_acc == R.INVALID, 0, ref_acc).astype(np.uint32)
+    got = dacc.to_numpy()
+    assert np.array_equal(got, ref_acc), int((got != ref_acc).sum())
+    if po2 <= 12:
+        ref_seal, ref_mix, _ = oracle.prove_segment("rv32im", s, po2, code, data, ref_acc, glob, version=2)
+        assert np.array_equal(mix, ref_mix)
+        assert np.array_equal(seal, ref_seal)
+    else:
+        assert r.verify_seal("rv32im", s, seal, check_validity=False) == po2
+
+
+def test_prove_segment_accum_rejects_invalid_bigint_eqz(hal, oracle):
+    """An EqZero whose integer identity fails stops the proof with the reference's error
+    (byte_poly.rs:458 "Invalid eqz in bigint accum"), as WitnessGenerator::accum does."""
+    import risc0_amd as r
+    import bigint_accum as B
+    po2 = 8
+    n = 1 << po2
+    d = oracle.load_circuit_json("rv32im")
+    rng, data, recs = _bigint_witness(po2, 0xB3, 6)
+    recs = [[row, op, c, list(by)] for row, op, c, by in recs]
+    eqz = next(i for i, rec in enumerate(recs) if rec[1] == B.EQ_ZERO)
+    recs[eqz][3][0] ^= 1
+    code = oracle.rand_elems(rng, d["group_sizes"][1] * n)
+    glob = oracle.rand_elems(rng, d["output_size"])
+    dacc = dev(hal, np.full(d["group_sizes"][0] * n, 0xFFFFFFFF, np.uint32))
+    with pytest.raises(r.R0HipError, match="Invalid eqz in bigint accum"):
+        r.prove_segment_accum(hal, "rv32im", po2, dev(hal, code), dev(hal, data), dacc, n, dev(hal, glob),
+                              version=2, bigint=recs)
+    # the library stays usable after the error
+    seal, _ = r.prove_segment_accum(hal, "rv32im", po2, dev(hal, code), dev(hal, data),
+                                    dev(hal, np.full(d["group_sizes"][0] * n, 0xFFFFFFFF, np.uint32)), n,
+                                    dev(hal, glob), version=2, bigint=[tuple(x) for x in recs[:eqz]])
+    assert seal.size > 0
+
+
+@pytest.mark.parametrize("suite,po2", [("poseidon2", 10), ("sha-256", 9)])
+def test_prove_segments_bigint_matches_fused(hal, hal_sha, oracle, suite, po2):
+    """The segment pipeline's device accumulation with per-job BigInt backs equals
+    r0hip_prove_segment_accum on the same jobs (4 jobs over 3 reused buffer sets; one job
+    without BigInt cycles), and a job that gives backs with a host accum group is refused."""
+    import risc0_amd as r
+    h = H(suite)
+    d = oracle.load_circuit_json("rv32im")
+    n = 1 << po2
+    jobs, want = [], []
+    for i in range(4):
+        rng, data, recs = _bigint_witness(po2, 0x50 + 7 * po2 + i, 0 if i == 2 else 40)
+        code = oracle.rand_elems(rng, d["group_sizes"][1] * n)
+        glob = oracle.rand_elems(rng, d["output_size"])
+        dacc = dev(h, np.full(d["group_sizes"][0] * n, 0xFFFFFFFF, np.uint32))
+        want.append(r.prove_segment_accum(h, "rv32im", po2, dev(h, code), dev(h, data), dacc, n, dev(h, glob),
+                                          version=2, bigint=recs))
+        jobs.append((code, data, None, glob, recs))
+    got = r.prove_segments(h, "rv32im", po2, jobs, version=2, in_flight=2)
+    for (s1, m1), (s2, m2) in zip(got, want):
+        assert np.array_equal(m1, m2)
+        assert np.array_equal(s1, s2)
+    code, data, _, glob, recs = jobs[0]
+    acc = np.zeros(d["group_sizes"][0] * n, np.uint32)
+    with pytest.raises(r.R0HipError, match="without a device accumulation"):
+        r.prove_segments(h, "rv32im", po2, [(code, data, acc, glob, recs)], version=2)

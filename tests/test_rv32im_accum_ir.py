@@ -22,8 +22,10 @@ def rows_for_arms(rng, rows, arms):
         if a == 12:
             # the big-integer arm's polyOp (data column 32) must decode one-hot (EQZ at
             # one_hot.zir:9); 0 selects BigIntPolyOpNop. The other ops read the previous
-            # cycle's big-integer state (back 1), written by the same phase in the reference
-            # too, so their result depends on cycle order there as here.
+            # cycle's BigInt accumulator state (back 1), which the witness generator injects
+            # before the step (witgen/mod.rs:178-205): rows running them come from
+            # tests/bigint_accum.py with their states (tests/test_bigint_accum.py and the
+            # *_bigint_* GPU tests).
             data[32, r] = 0
     return data.reshape(-1)
 
