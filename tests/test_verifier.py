@@ -92,6 +92,50 @@ def test_native_poly_ext_matches_restatement(oracle, circuit):
         assert got == want
 
 
+def _poly_ext_golden_inputs(oracle, n):
+    import poly_ext_def as D
+    d = oracle.load_circuit_json("recursion")
+    return D.inputs(oracle, n, verifier.Taps("recursion").num_taps, d["mix_size"], d["output_size"])
+
+
+def test_native_poly_ext_matches_reference_constraint_program(oracle):
+    """r0hip_poly_ext("recursion") equals the reference verifier's own constraint program on
+    1000 seeded (poly_mix, eval_u, global, mix) inputs: the DEF table of
+    risc0/circuit/recursion/src/poly_ext.rs run by a restatement of PolyExtExecutor
+    (zkp/src/adapter.rs:317-400), whose outputs are the committed fixture
+    tests/golden/poly_ext_recursion.npy (tools/make_poly_ext_golden.py). The Python
+    restatement (tests/verifier.py poly_ext, over the IR the library embeds) agrees too."""
+    import os
+    import risc0_amd as r
+    from risc0_amd.hal import LIB_PATH
+    if not os.path.exists(LIB_PATH):
+        pytest.skip("libr0hip.so not built")
+    want = np.load(os.path.join(os.path.dirname(__file__), "golden", "poly_ext_recursion.npy"))
+    pm, u, g, m = _poly_ext_golden_inputs(oracle, want.shape[0])
+    got = np.stack([r.poly_ext("recursion", m[k], g[k], u[k], pm[k]) for k in range(want.shape[0])])
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} of {want.shape[0]} inputs differ, first {bad[0]}"
+    taps = verifier.Taps("recursion")
+    for k in range(5):
+        ours = verifier.poly_ext("recursion", taps, tuple(verifier.dec(w) for w in pm[k]), verifier.ext_words(u[k]),
+                                 g[k], m[k])
+        assert tuple(verifier.enc(x) for x in ours) == tuple(int(x) for x in want[k])
+
+
+def test_poly_ext_golden_is_the_reference_constraint_program(oracle):
+    """The fixture above re-derived from the reference's poly_ext.rs where it lies (skipped
+    without /root/reference): the first 100 vectors, and the table's shape."""
+    import os
+    import poly_ext_def as D
+    if not D.available():
+        pytest.skip("/root/reference not present")
+    steps, ret = D.parse()
+    assert len(steps) == 12359 and ret == 1228
+    want = np.load(os.path.join(os.path.dirname(__file__), "golden", "poly_ext_recursion.npy"))[:100]
+    pm, u, g, m = _poly_ext_golden_inputs(oracle, 100)
+    assert np.array_equal(D.evaluate(steps, ret, pm, u, g, m), want)
+
+
 @pytest.mark.parametrize("suite", ["poseidon2", "sha-256", "poseidon_254"])
 def test_valid_recursion_seal_passes_validity(oracle, suite):
     """A witness that satisfies the recursion circuit (all-zero code/data/accum; the
