@@ -32,9 +32,11 @@ def _emul(a, b):
     return (r0, r1, r2, r3)
 
 
-def evaluate(prog, args, domain, pm):
+def evaluate(prog, args, domain, pm, inv_rate=4):
     """args: list of plain-integer numpy arrays (per buffer); pm: list of plain FpExt tuples.
-    Returns 4 arrays (plain) of length `domain` = poly_fp(cycle) for every cycle."""
+    Returns 4 arrays (plain) of length `domain` = poly_fp(cycle) for every cycle. Taps read
+    `back * inv_rate` rows back: 4 on the evaluation domain (the generated code's kInvRate),
+    1 to evaluate the constraints on the trace rows themselves."""
     cyc = np.arange(domain, dtype=np.int64)
     mask = domain - 1
     val = {}
@@ -72,7 +74,7 @@ def evaluate(prog, args, domain, pm):
             val[i] = tuple(np.full(domain, x, dtype=np.uint64) for x in ins[2:6])
         elif op == "l":
             buf, col, back = ins[2:5]
-            idx = col * domain + ((cyc - 4 * back) & mask)
+            idx = col * domain + ((cyc - inv_rate * back) & mask)
             val[i] = args[buf][idx].astype(np.uint64)
         elif op == "g":
             val[i] = np.full(domain, int(args[ins[2]][ins[3]]), dtype=np.uint64)

@@ -1,0 +1,519 @@
+"""Recursion-circuit programs, their preflight and their witness (test infrastructure only).
+
+The recursion circuit is a small VM whose program lives in the 23 control columns
+(risc0/circuit/recursion/src/prove/program.rs:33-60; CODE_LAYOUT, layout.rs.inc:224-330).
+The lift/join programs ship in recursion_zkr.zip, which is not in the tree (an LFS pointer),
+so the tests hand-encode programs with `Program` below and run them the way the reference's
+RecursionProverImpl does (prove/mod.rs:160-252):
+
+* `preflight(program, input)`: a restatement of Preflight::step (prove/preflight.rs:181-627)
+  over plain integers mod p: the write-once memory (WOM), per-cycle {iop_idx, is_par_safe}
+  and the IOP reads;
+* `witgen(...)`: the reference's own compiled witness generator,
+  risc0_circuit_recursion_cpu_witgen (recursion-sys/kernels/cxx/ffi.cpp:191-205: step_exec,
+  WOM sort and scan, injectWomBacks, step_verify_mem), from oracle/_ref/libref_recursion.so;
+  then the ZK noise rows and zeroize of WitnessGenerator::new (prove/witgen.rs:44-133);
+* `row_constraints(...)`: poly_fp evaluated on the trace rows themselves (the committed
+  constraint IR, tests/ir_eval.py, at stride 1): zero on every row iff the witness satisfies
+  the circuit.
+"""
+import ctypes as C
+import os
+from collections import deque
+
+import numpy as np
+
+P = 15 * 2**27 + 1
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "_ref", "libref_recursion.so")
+CTRL, DATA, ACCUM, OUT, MIX = 23, 128, 12, 32, 20  # recursion group sizes, globals, mix
+ZK_CYCLES = 1024  # risc0_zkp::ZK_CYCLES (zkp/src/lib.rs:42)
+INVALID = 0xFFFFFFFF
+R = 2**32 % P
+RINV = pow(2**32, P - 2, P)
+TO_MONT, FROM_MONT = 0xFFFFFFE, 0x38400000  # preflight.rs:36-37 (2^32 and 2^-32 mod p)
+
+# control column offsets (CODE_LAYOUT)
+WRITE_ADDR = 0
+SEL = dict(micro=1, macro=2, p2_load=3, p2_full=4, p2_partial=5, p2_store=6, checked_bytes=7)
+MACRO = dict(nop=8, wom_init=9, wom_fini=10, bit_and_elem=11, bit_op_shorts=12, sha_init=13, sha_fini=14,
+             sha_load=15, sha_mix=16, set_global=17)
+MACRO_OPERAND = 18
+# micro opcodes (preflight.rs:41-53)
+CONST, ADD, SUB, MUL, INV, EQ, READ_IOP_HEADER, READ_IOP_BODY, MIX_RNG, SELECT, EXTRACT = range(11)
+
+
+def enc(x):
+    return (int(x) % P) * R % P
+
+
+def dec(w):
+    return int(w) * RINV % P
+
+
+# ---- FpExt over plain integers (baby_bear.rs:375-790) ----
+def eadd(a, b):
+    return tuple((x + y) % P for x, y in zip(a, b))
+
+
+def esub(a, b):
+    return tuple((x - y) % P for x, y in zip(a, b))
+
+
+def emul(a, b):
+    r = [0] * 4
+    for i in range(4):
+        for j in range(4):
+            if i + j < 4:
+                r[i + j] += a[i] * b[j]
+            else:
+                r[i + j - 4] += (P - 11) * a[i] * b[j]
+    return tuple(x % P for x in r)
+
+
+def einv(a):
+    a0, a1, a2, a3 = a
+    b0 = (a0 * a0 + 11 * (a1 * 2 * a3 - a2 * a2)) % P
+    b2 = (a0 * 2 * a2 - a1 * a1 + 11 * a3 * a3) % P
+    c = (b0 * b0 + 11 * b2 * b2) % P
+    ic = pow(c, P - 2, P)
+    b0, b2 = b0 * ic % P, b2 * ic % P
+    return ((a0 * b0 + 11 * a2 * b2) % P, (-a1 * b0 + (P - 11) * a3 * b2) % P, (-a0 * b2 + a2 * b0) % P,
+            (a1 * b2 - a3 * b0) % P)
+
+
+ZERO = (0, 0, 0, 0)
+
+
+class Program:
+    """Rows of the 23 control columns, plain integers (Program::from_encoded maps each word
+    through Elem::from, program.rs:50-58)."""
+
+    def __init__(self):
+        self.rows = []
+
+    def _row(self, sel, write_addr=0):
+        r = [0] * CTRL
+        r[SEL[sel]] = 1
+        r[WRITE_ADDR] = write_addr
+        self.rows.append(r)
+        return r
+
+    def micro(self, write_addr, ops):
+        """up to three micro ops (opcode, a0, a1, a2); op i writes WOM[write_addr + i]"""
+        r = self._row("micro", write_addr)
+        ops = list(ops) + [(CONST, 0, 0, 0)] * (3 - len(ops))
+        for i, (op, a, b, c) in enumerate(ops):
+            r[8 + 4 * i:12 + 4 * i] = [op, a, b, c]
+        return r
+
+    def macro(self, name, write_addr=0, operands=(0, 0, 0)):
+        r = self._row("macro", write_addr)
+        r[MACRO[name]] = 1
+        r[MACRO_OPERAND:MACRO_OPERAND + 3] = list(operands)
+        return r
+
+    def p2_load(self, group, inputs, keep_state=0, keep_upper_state=0, do_mont=0, prep_full=0):
+        r = self._row("p2_load")
+        r[8:12] = [do_mont, keep_state, keep_upper_state, prep_full]
+        r[12 + group] = 1
+        r[15:23] = list(inputs)
+        return r
+
+    def p2_full(self, k):
+        r = self._row("p2_full")
+        r[8 + k] = 1
+        return r
+
+    def p2_partial(self):
+        return self._row("p2_partial")
+
+    def p2_store(self, group, write_addr, do_mont=0):
+        r = self._row("p2_store", write_addr)
+        r[8] = do_mont
+        r[12 + group] = 1
+        return r
+
+    def encoded(self):
+        """the .zkr word stream (row-major, plain integers)"""
+        return np.array([x % P for r in self.rows for x in r], dtype=np.uint32)
+
+
+class Preflight:
+    """Preflight::step (prove/preflight.rs:181-627) over plain integers mod p."""
+
+    def __init__(self, inp=()):
+        self.input = deque(int(x) for x in inp)
+        self.wom = []
+        self.cycles = []  # (iop_idx, is_par_safe)
+        self.iops = []
+        self.p2 = [0] * 24
+        self.cur_iop_body = deque()
+        self.iop_idx = 0
+        self.output = []
+
+    def wom_read(self, addr):
+        return self.wom[addr % P]
+
+    def wom_write(self, addr, val):
+        addr %= P
+        if len(self.wom) <= addr:
+            self.wom += [ZERO] * (addr + 1 - len(self.wom))
+        cur = self.wom[addr]
+        if cur != ZERO and cur != val:
+            raise ValueError(f"WOM {addr} overwritten with {val} from {cur}")
+        self.wom[addr] = val
+
+    def step(self, row):
+        g = lambda i: row[i] % P
+        if g(SEL["macro"]) == 1:
+            safe = self.macro_op(row)
+        elif g(SEL["micro"]) == 1:
+            safe = True
+            for i in range(3):
+                safe &= self.micro_op(row, (g(WRITE_ADDR) + i) % P, 8 + 4 * i)
+        elif g(SEL["checked_bytes"]) == 1:
+            raise NotImplementedError("checked bytes: the reference's C++ witgen cannot run them "
+                                      "(extern_readCoefficients throws, recursion-sys/kernels/cxx/extern.cpp)")
+        elif g(SEL["p2_load"]) == 1:
+            do_mont, keep_state, keep_upper = g(8), g(9), g(10)
+            group = g(13) + 2 * g(14)
+            if keep_state != 1:
+                if keep_upper != 1:
+                    self.p2 = [0] * 24
+                else:
+                    self.p2[:16] = [0] * 16
+            for i in range(8):
+                load = self.wom_read(g(15 + i))[0]
+                if do_mont:
+                    load = load * FROM_MONT % P
+                self.p2[group * 8 + i] = (self.p2[group * 8 + i] + load) % P
+            safe = False
+        elif g(SEL["p2_full"]) == 1:
+            safe = False
+        elif g(SEL["p2_partial"]) == 1:
+            import oracle
+            cells = np.array([enc(x) for x in self.p2], np.uint32)
+            oracle.poseidon2_mix(cells)
+            self.p2 = [dec(x) for x in cells]
+            safe = False
+        elif g(SEL["p2_store"]) == 1:
+            do_mont = g(8)
+            group = g(13) + 2 * g(14)
+            for i in range(8):
+                v = self.p2[group * 8 + i]
+                if do_mont:
+                    v = v * TO_MONT % P
+                self.wom_write(g(WRITE_ADDR) + i, (v, 0, 0, 0))
+            safe = False
+        else:
+            raise ValueError("Illegal recursion op")
+        self.cycles.append((self.iop_idx, int(safe)))
+        self.iop_idx = len(self.iops)
+
+    def macro_op(self, row):
+        g = lambda i: row[i] % P
+        a = [g(MACRO_OPERAND + i) for i in range(3)]
+        wa = g(WRITE_ADDR)
+        if g(MACRO["bit_and_elem"]) == 1:
+            self.wom_write(wa, ((self.wom_read(a[0])[0] & self.wom_read(a[1])[0]) % P, 0, 0, 0))
+        elif g(MACRO["bit_op_shorts"]) == 1:
+            x, y = self.wom_read(a[0]), self.wom_read(a[1])
+            if a[2]:
+                self.wom_write(wa, (((x[0] & y[0]) + ((x[1] & y[1]) << 16)) % P, 0, 0, 0))
+            else:
+                self.wom_write(wa, (x[0] ^ y[0], x[1] ^ y[1], 0, 0))
+        elif any(g(MACRO[k]) == 1 for k in ("sha_init", "sha_load", "sha_mix", "sha_fini")):
+            raise NotImplementedError("SHA macro ops are not restated here")
+        # nop, wom_init, wom_fini, set_global: nothing in the preflight
+        return True
+
+    def micro_op(self, row, wa, base):
+        op = row[base] % P
+        a = [row[base + 1 + i] % P for i in range(3)]
+        if op == CONST:
+            self.wom_write(wa, (a[0], a[1], 0, 0))
+        elif op == ADD:
+            x, y = self.wom_read(a[0]), self.wom_read(a[1])
+            self.wom_write(wa, eadd(x, y))
+            if a[2]:
+                self.output.append(x[0])
+        elif op == SUB:
+            self.wom_write(wa, esub(self.wom_read(a[0]), self.wom_read(a[1])))
+        elif op == MUL:
+            self.wom_write(wa, emul(self.wom_read(a[0]), self.wom_read(a[1])))
+        elif op == INV:
+            x = self.wom_read(a[0])
+            if a[1] == 0:
+                self.wom_write(wa, (1 if x[0] == 0 else 0, 0, 0, 0))
+            else:
+                self.wom_write(wa, einv(x))
+        elif op == EQ:
+            if self.wom_read(a[0]) != self.wom_read(a[1]):
+                raise ValueError("Equality check failed")
+        elif op == READ_IOP_HEADER:
+            count, k_flip = a[0], a[1]
+            k, flip = k_flip // 2, k_flip & 1
+            assert not self.cur_iop_body
+            if k == 2:
+                for _ in range(count):
+                    e = self.input.popleft()
+                    self.cur_iop_body.append([e & 0xFFFF, e >> 16])
+            else:
+                arr = [self.input.popleft() for _ in range(k * count)]
+                for i in range(count):
+                    self.cur_iop_body.append([dec(arr[i * k + j] if flip else arr[j * count + i]) for j in range(k)])
+        elif op == READ_IOP_BODY:
+            front = self.cur_iop_body.popleft()
+            front = list(front) + [0] * (4 - len(front))
+            if a[2]:
+                front = [x * TO_MONT % P for x in front]
+            body = tuple(front[:4])
+            self.wom_write(wa, body)
+            self.iops.append(body)
+        elif op == MIX_RNG:
+            val = a[2]
+            safe = True
+            if a[2]:
+                val = val * self.wom_read(wa - 1)[0] % P
+                safe = False
+            x, y = self.wom_read(a[0]), self.wom_read(a[1])
+            for part in (x[1], x[0], y[1], y[0]):
+                val = (val * (1 << 16) + part) % P
+            self.wom_write(wa, (val, 0, 0, 0))
+            return safe
+        elif op == SELECT:
+            x = self.wom_read(a[0])
+            self.wom_write(wa, self.wom_read((a[1] + a[2] * x[0]) % P))
+        elif op == EXTRACT:
+            x = self.wom_read(a[0])
+            v = (a[1] * a[2] * x[3] + a[1] * (1 - a[2]) * x[2] + (1 - a[1]) * a[2] * x[1]
+                 + (1 - a[1]) * (1 - a[2]) * x[0]) % P
+            self.wom_write(wa, (v, 0, 0, 0))
+        else:
+            raise ValueError("Unknown opcode")
+        return True
+
+
+def preflight(program, inp=()):
+    pf = Preflight(inp)
+    for row in program.rows:
+        pf.step(row)
+    return pf
+
+
+# ---- the reference's compiled witness generator ----
+class _ExecBuffers(C.Structure):
+    _fields_ = [("ctrl", C.c_void_p), ("data", C.c_void_p), ("glob", C.c_void_p)]
+
+
+class _Trace(C.Structure):
+    _fields_ = [("wom", C.c_void_p), ("cycles", C.c_void_p), ("iops", C.c_void_p), ("num_woms", C.c_uint32),
+                ("num_cycles", C.c_uint32), ("num_iops", C.c_uint32)]
+
+
+def available():
+    return os.path.exists(LIB)
+
+
+def ctrl_group(program, po2):
+    """the ctrl group as WitnessGenerator::new lays it out (witgen.rs:56-66), Montgomery words"""
+    n = 1 << po2
+    rows = len(program.rows)
+    assert rows <= n - ZK_CYCLES, "program longer than 2^po2 - ZK_CYCLES rows (program.rs:57)"
+    ctrl = np.zeros((CTRL, n), np.uint32)
+    for i, row in enumerate(program.rows):
+        ctrl[:, i] = [enc(x) for x in row]
+    return ctrl.reshape(-1)
+
+
+def witgen(program, pf, po2, noise_seed=None):
+    """(ctrl, data, global) Montgomery words: the reference's compiled witgen in parallel mode
+    (ffi.cpp:191-205) over the preflight trace, then (witgen.rs:101-123) the last ZK_CYCLES
+    data rows set to one random value (vec![random; n], as the reference does) and INVALID
+    words zeroized."""
+    n = 1 << po2
+    ctrl = ctrl_group(program, po2)
+    data = np.full(DATA * n, INVALID, np.uint32)
+    glob = np.full(OUT, INVALID, np.uint32)
+    wom = np.array([[enc(x) for x in v] for v in pf.wom] or [[0] * 4], np.uint32).reshape(-1)
+    cycles = np.array(pf.cycles or [(0, 0)], np.uint32).reshape(-1)
+    iops = np.array([[enc(x) for x in v] for v in pf.iops] or [[0] * 4], np.uint32).reshape(-1)
+    bufs = _ExecBuffers(ctrl.ctypes.data, data.ctypes.data, glob.ctypes.data)
+    tr = _Trace(wom.ctypes.data, cycles.ctypes.data, iops.ctypes.data, len(pf.wom), len(program.rows), len(pf.iops))
+    lib = C.CDLL(LIB)
+    lib.risc0_circuit_recursion_cpu_witgen.restype = C.c_void_p
+    lib.risc0_circuit_recursion_cpu_witgen.argtypes = [C.c_uint32, C.POINTER(_ExecBuffers), C.POINTER(_Trace),
+                                                        C.c_uint32]
+    err = lib.risc0_circuit_recursion_cpu_witgen(0, C.byref(bufs), C.byref(tr), n)
+    if err:
+        raise RuntimeError(C.cast(err, C.c_char_p).value.decode())
+    rng = np.random.default_rng(noise_seed)
+    d = data.reshape(DATA, n)
+    d[:, n - ZK_CYCLES:] = enc(int(rng.integers(0, P)))
+    data[data == INVALID] = 0
+    glob[glob == INVALID] = 0
+    return ctrl, data, glob
+
+
+def accum_init(po2, noise_seed=None):
+    """the accum group as WitnessGenerator::accum hands it to the accumulation (witgen.rs:
+    134-160): INVALID, last ZK_CYCLES rows one random value"""
+    n = 1 << po2
+    acc = np.full((ACCUM, n), INVALID, np.uint32)
+    acc[:, n - ZK_CYCLES:] = enc(int(np.random.default_rng(noise_seed).integers(0, P)))
+    return acc.reshape(-1)
+
+
+def row_constraints(ctrl, data, accum, glob, mix, po2, poly_mix=(7, 11, 13, 17)):
+    """poly_fp on every trace row (stride 1 instead of the 4x domain's 4): (4, n) plain values,
+    zero on row r iff every constraint holds there (for a random poly_mix)."""
+    import ir_eval
+    n = 1 << po2
+    prog = ir_eval.load_ir("recursion")
+    args = [np.array([dec(x) for x in a], np.uint64) for a in (ctrl, glob, data, mix, accum)]
+    import json
+    with open(os.path.join(ROOT, "risc0_amd", "circuits", "recursion.taps.json")) as f:
+        powers = json.load(f)["poly_mix_powers"]
+    pm = []
+    for k in powers:
+        v, b, e = (1, 0, 0, 0), tuple(poly_mix), k
+        while e:
+            if e & 1:
+                v = emul(v, b)
+            b, e = emul(b, b), e >> 1
+        pm.append(v)
+    return np.stack(ir_eval.evaluate(prog, args, n, pm, inv_rate=1))
+
+
+class Builder:
+    """A Program over a contiguous WOM: every micro-op slot owns its address (ops that write
+    nothing, such as EQ, leave it zero), so the sorted WOM addresses step by 0 or 1 as the
+    memory argument requires (zirgen wom.cpp:72-74, step_verify_mem), from WOM_INIT's (0, 0)
+    header to WOM_FINI at the next free address."""
+
+    def __init__(self, rng):
+        self.p = Program()
+        self.rng = rng
+        self.next = 1
+        self.input = []
+        self.p.macro("wom_init")
+
+    def micro(self, ops):
+        """ops: up to three (opcode, a0, a1, a2); returns the three slot addresses"""
+        wa = self.next
+        self.p.micro(wa, ops)
+        self.next += 3
+        return wa, wa + 1, wa + 2
+
+    def consts(self, vals):
+        """CONST (lo, hi) pairs, three per row; returns their addresses"""
+        out = []
+        for i in range(0, len(vals), 3):
+            chunk = vals[i:i + 3]
+            out += list(self.micro([(CONST, a, b, 0) for a, b in chunk]))[:len(chunk)]
+        return out
+
+    def shorts(self, n):
+        r = self.rng
+        return self.consts([(int(r.integers(0, 1 << 16)), int(r.integers(0, 1 << 16))) for _ in range(n)])
+
+    def elems(self, n):
+        return self.consts([(int(self.rng.integers(1, P)), 0) for _ in range(n)])
+
+    def block_arith(self):
+        a, b, c = self.elems(3)
+        s = self.micro([(ADD, a, b, 0), (SUB, a, c, 0), (MUL, b, c, 0)])
+        t = self.micro([(INV, s[2], 1, 0), (INV, a, 0, 0), (MUL, s[0], s[1], 0)])
+        z = self.consts([(0, 0)])[0]
+        self.micro([(INV, z, 0, 0), (EQ, a, a, 0), (MUL, t[0], s[2], 0)])
+        e = self.consts([tuple(int(x) for x in self.rng.integers(0, P, 2))])[0]
+        ext = self.micro([(MUL, e, e, 0), (ADD, e, a, 0), (INV, e, 1, 0)])
+        self.micro([(EXTRACT, ext[0], 0, 0), (EXTRACT, ext[0], 1, 0), (EXTRACT, ext[0], 1, 1)])
+        idx = self.consts([(int(self.rng.integers(0, 3)), 0)])[0]
+        self.micro([(SELECT, idx, a, 1), (ADD, a, b, 1), (EXTRACT, ext[2], 0, 1)])
+
+    def block_bits(self):
+        x, y = self.shorts(2)
+        self.micro([(CONST, 0, 0, 0)])  # keep rows micro-aligned
+        for name, ops in (("bit_and_elem", (x, y, 0)), ("bit_op_shorts", (x, y, 1)), ("bit_op_shorts", (x, y, 0))):
+            self.p.macro(name, self.next, ops)
+            self.next += 1
+        a, b = self.elems(2)
+        self.p.macro("bit_and_elem", self.next, (a, b, 0))
+        self.next += 1
+
+    def block_mix_rng(self):
+        x, y, z = self.shorts(3)
+        first = self.micro([(MIX_RNG, x, y, 0), (MIX_RNG, y, z, 1), (MIX_RNG, z, x, 1)])
+        self.micro([(MIX_RNG, x, x, 0), (ADD, first[2], first[0], 0), (MIX_RNG, y, y, 5)])
+
+    def block_iop(self):
+        r = self.rng
+        n2 = 3
+        self.input += [int(r.integers(0, 1 << 32)) for _ in range(n2)]
+        self.micro([(READ_IOP_HEADER, n2, 4, 0)])  # k = 2: shorts
+        for _ in range(n2):
+            self.micro([(READ_IOP_BODY, 0, 0, 0)])
+        for k, flip, mont in ((4, 0, 1), (4, 1, 0), (1, 0, 0)):
+            cnt = 2
+            self.input += [enc(int(x)) for x in r.integers(0, P, k * cnt)]
+            self.micro([(READ_IOP_HEADER, cnt, 2 * k + flip, 0)])
+            for _ in range(cnt):
+                self.micro([(READ_IOP_BODY, 0, 0, mont)])
+
+    def block_poseidon2(self):
+        ins = self.elems(24)
+        keep = int(self.rng.integers(0, 2))
+        self.p.p2_load(0, ins[0:8])
+        self.p.p2_load(1, ins[8:16], keep_state=1)
+        self.p.p2_load(2, ins[16:24], keep_state=1, do_mont=keep)
+        for k in range(4):
+            self.p.p2_full(k)
+        self.p.p2_partial()
+        for k in range(4):
+            self.p.p2_full(k)
+        for g in range(3):
+            self.p.p2_store(g, self.next, do_mont=int(g == 2))
+            self.next += 8
+
+    def finish(self):
+        vals = self.shorts(16)
+        for part in range(4):
+            self.p.macro("set_global", 0, (vals[4 * part], part, 0))
+        self.p.macro("wom_fini", self.next)
+        return self.p, self.input
+
+
+def random_program(rng, max_rows, blocks=("arith", "bits", "mix_rng", "iop", "poseidon2")):
+    """a program of random blocks, up to max_rows control rows; returns (program, input)"""
+    b = Builder(rng)
+    while len(b.p.rows) + 40 < max_rows:
+        getattr(b, "block_" + blocks[int(rng.integers(0, len(blocks)))])()
+    return b.finish()
+
+
+def satisfying_witness(seed, po2, max_rows=None, blocks=("arith", "bits", "mix_rng", "iop", "poseidon2")):
+    """A random program filling the segment (all rows but the ZK rows, or max_rows), its
+    preflight, and the witness WitnessGenerator::new makes from it: returns dict with
+    program, input, preflight, ctrl, data, glob (Montgomery words, INVALID zeroized), work
+    (the program's row count, the accumulation's work cycles) and acc0 (the accum group as
+    WitnessGenerator::accum hands it over: INVALID plus the ZK noise rows)."""
+    rng = np.random.default_rng(seed)
+    n = 1 << po2
+    rows = min(max_rows or n, n - ZK_CYCLES - 1)
+    prog, inp = random_program(rng, rows, blocks)
+    pf = preflight(prog, inp)
+    ctrl, data, glob = witgen(prog, pf, po2, noise_seed=seed + 1)
+    return dict(program=prog, input=inp, preflight=pf, ctrl=ctrl, data=data, glob=glob, work=len(prog.rows),
+                acc0=accum_init(po2, noise_seed=seed + 2))
+
+
+def accumulate(w, mix, po2):
+    """the reference's compiled accumulation (risc0_circuit_recursion_cpu_accum) on the
+    witness with the given mix, INVALID words zeroized (witgen.rs:162-175)"""
+    import accum_ir as A
+    acc = w["acc0"].copy()
+    A.ref_accum(w["ctrl"], w["glob"], w["data"], mix, acc, w["work"], 1 << po2)
+    acc[acc == INVALID] = 0
+    return acc

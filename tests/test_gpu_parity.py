@@ -971,3 +971,42 @@ def test_prove_segments_bigint_matches_fused(hal, hal_sha, oracle, suite, po2):
     acc = np.zeros(d["group_sizes"][0] * n, np.uint32)
     with pytest.raises(r.R0HipError, match="without a device accumulation"):
         r.prove_segments(h, "rv32im", po2, [(code, data, acc, glob, recs)], version=2)
+
+
+# ---- a satisfying, non-trivial recursion witness proven on the GPU (tests/recursion_program.py) ----
+
+@pytest.mark.parametrize("suite,po2", [("poseidon2", 16), ("sha-256", 16), ("poseidon2", 18)])
+def test_satisfying_recursion_program_gpu_seal_passes_validity(hal, hal_sha, oracle, suite, po2):
+    """A hand-encoded recursion program filling the segment (every row but the ZK rows),
+    through the restated preflight and the reference's compiled witness generator, proven by
+    r0hip_prove_segment_accum (accumulation on the device). The device accum group equals the
+    reference accumulation with the drawn mix; the seal passes r0hip_verify_seal with the
+    validity equation and the restated verifier; at po2 16 Poseidon2 it equals the oracle
+    prover's seal; flipping one data word makes the native verifier reject the new seal."""
+    import recursion_program as RP
+    import risc0_amd as r
+    import verifier
+    if not RP.available() or oracle.ref_lib() is None:
+        pytest.skip("oracle/_ref not built")
+    h, s = H(suite), S(oracle, suite)
+    w = RP.satisfying_witness(1000 + po2, po2)
+    assert w["work"] > (1 << po2) - RP.ZK_CYCLES - 64
+    dacc = dev(h, w["acc0"])
+    seal, mix = r.prove_segment_accum(h, "recursion", po2, dev(h, w["ctrl"]), dev(h, w["data"]), dacc, w["work"],
+                                      dev(h, w["glob"]))
+    ref_acc = RP.accumulate(w, mix, po2)
+    got = dacc.to_numpy()
+    assert np.array_equal(got, ref_acc), int((got != ref_acc).sum())
+    assert r.verify_seal("recursion", s, seal) == po2
+    assert verifier.verify(oracle, "recursion", seal, s, check_validity=True)["validity"] is True
+    if po2 == 16 and suite == "poseidon2":
+        ref_seal, ref_mix, _ = oracle.prove_segment("recursion", s, po2, w["ctrl"], w["data"], ref_acc, w["glob"])
+        assert np.array_equal(mix, ref_mix)
+        assert np.array_equal(seal, ref_seal)
+    bad = w["data"].copy()
+    bad[9 * (1 << po2) + 100] ^= 1
+    seal_b, _ = r.prove_segment_accum(h, "recursion", po2, dev(h, w["ctrl"]), dev(h, bad), dev(h, w["acc0"]),
+                                      w["work"], dev(h, w["glob"]))
+    with pytest.raises(r.R0HipError):
+        r.verify_seal("recursion", s, seal_b)
+    assert r.verify_seal("recursion", s, seal_b, check_validity=False) == po2

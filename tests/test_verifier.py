@@ -153,6 +153,40 @@ def test_valid_recursion_seal_passes_validity(oracle, suite):
     assert r.verify_seal("recursion", s, seal) == po2
 
 
+@pytest.mark.parametrize("suite", ["poseidon2", "sha-256", "poseidon_254"])
+def test_satisfying_recursion_program_seal_passes_validity(oracle, suite):
+    """A non-trivial satisfying witness: a hand-encoded recursion program (arithmetic, bit
+    ops, MIX_RNG, IOP reads, Poseidon2; tests/recursion_program.py) run through a restatement
+    of the reference preflight (prove/preflight.rs) and the reference's own compiled witness
+    generator and accumulation. Its constraints hold on every row; the oracle's seal of it
+    passes the validity equation in the restated verifier and in r0hip_verify_seal, and one
+    flipped witness word breaks both."""
+    import recursion_program as RP
+    import risc0_amd as r
+    _native_lib_or_skip(oracle)
+    if not RP.available():
+        pytest.skip("oracle/_ref/libref_recursion.so not built")
+    po2, s = 11, SUITES[suite]
+    w = RP.satisfying_witness(77, po2)
+    assert w["work"] > 900 and len(w["preflight"].iops) > 0
+    _, mix, _ = oracle.prove_segment("recursion", s, po2, w["ctrl"], w["data"], w["acc0"] * 0, w["glob"])
+    acc = RP.accumulate(w, mix, po2)
+    rc = RP.row_constraints(w["ctrl"], w["data"], acc, w["glob"], mix, po2)
+    assert not rc.any(), f"constraints fail on rows {np.nonzero(rc.any(axis=0))[0][:8]}"
+    seal, mix2, _ = oracle.prove_segment("recursion", s, po2, w["ctrl"], w["data"], acc, w["glob"])
+    assert np.array_equal(mix, mix2)
+    assert verifier.verify(oracle, "recursion", seal, s, check_validity=True)["validity"] is True
+    assert r.verify_seal("recursion", s, seal) == po2
+    bad = w["data"].copy()
+    bad[7 * (1 << po2) + 5] ^= 1
+    _, mixb, _ = oracle.prove_segment("recursion", s, po2, w["ctrl"], bad, acc, w["glob"])
+    seal_b, _, _ = oracle.prove_segment("recursion", s, po2, w["ctrl"], bad, RP.accumulate(dict(w, data=bad), mixb, po2),
+                                        w["glob"])
+    assert verifier.verify(oracle, "recursion", seal_b, s, check_validity=True)["validity"] is False
+    with pytest.raises(r.R0HipError):
+        r.verify_seal("recursion", s, seal_b)
+
+
 def test_native_verifier_rejects_garbage(oracle):
     """Malformed seals (empty, random words, a valid prefix with a tampered po2 or cut
     anywhere) come back as errors, never as a crash or an out-of-bounds read."""
