@@ -74,13 +74,19 @@ def main():
     import risc0_amd as r
     with open(os.path.join(ROOT, "risc0_amd", "circuits", args.circuit + ".taps.json")) as f:
         circ = json.load(f)
-    device = local_rank
+    device = 0
     if os.environ.get("R0_BENCH_SHARE_GPUS") == "1":
-        # rehearsal of the N-rank path on fewer GPUs (tools/gpu_ranks.sh): ranks share the
-        # visible devices round-robin; never set for a measurement
+        # rehearsal of the N-rank path on fewer GPUs (tools/rehearsal/gpu_ranks.sh): ranks
+        # share the visible devices round-robin; never set for a measurement
         import torch
         device = local_rank % max(1, torch.cuda.device_count())
         print(f"rank {rank}: R0_BENCH_SHARE_GPUS=1, device {device}", file=sys.stderr)
+    elif world > 1:
+        # one GPU per rank process, bound before the first HIP call as r0vm binds its workers
+        # (r0vm/src/actors/mod.rs:449-462); launch_local has already done it for its children
+        from risc0_amd.segments import narrow_visible_devices
+        device = narrow_visible_devices(local_rank, os.environ)
+        print(f"rank {rank}: HIP_VISIBLE_DEVICES={os.environ['HIP_VISIBLE_DEVICES']}", file=sys.stderr)
     hal = r.HipHal(args.hashfn, device=device)
     version = 2 if args.circuit == "rv32im" else None
 

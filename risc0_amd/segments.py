@@ -67,18 +67,42 @@ def free_port():
     return p
 
 
+def narrow_visible_devices(local_rank, env):
+    """Bind a rank to one GPU as r0vm binds each worker (CUDA_VISIBLE_DEVICES=idx,
+    r0vm/src/actors/mod.rs:449-462): HIP_VISIBLE_DEVICES becomes the rank's one device — the
+    local_rank-th entry of an inherited list, else the local_rank-th device the runtime sees
+    (HIP indexes within ROCR_VISIBLE_DEVICES when that is set). The rank then opens ordinal 0.
+    Marks env with R0_RANK_BOUND so a second call (the rank itself, after launch_local bound
+    it) leaves it alone. Returns the HIP ordinal to open (0)."""
+    if env.get("R0_RANK_BOUND") == "1":
+        return 0
+    inherited = env.get("HIP_VISIBLE_DEVICES") or env.get("CUDA_VISIBLE_DEVICES")
+    if inherited:
+        devs = [d for d in inherited.split(",") if d.strip() != ""]
+        if local_rank >= len(devs):
+            raise RuntimeError(f"local rank {local_rank} has no device in HIP_VISIBLE_DEVICES={inherited}")
+        env["HIP_VISIBLE_DEVICES"] = devs[local_rank].strip()
+    else:
+        env["HIP_VISIBLE_DEVICES"] = str(local_rank)
+    env.pop("CUDA_VISIBLE_DEVICES", None)
+    env["R0_RANK_BOUND"] = "1"
+    return 0
+
+
 def rank_env(rank, world, port, base=None):
-    """The environment torch.distributed.run gives rank `rank` of a one-node job."""
+    """The environment torch.distributed.run gives rank `rank` of a one-node job, with the
+    rank bound to its own GPU (narrow_visible_devices) before the child starts."""
     env = dict(os.environ if base is None else base)
     env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    narrow_visible_devices(rank, env)
     return env
 
 
 def launch_local(world, argv, timeout=None):
-    """Start `world` copies of `argv` (one per GPU, rank r on device r), each with the
-    rank environment above, and wait for all of them. Rank 0's stdout passes through;
+    """Start `world` copies of `argv` (one per GPU: rank r sees only device r, as its
+    ordinal 0), each with the rank environment above, and wait for all of them. Rank 0's stdout passes through;
     the other ranks' stdout is dropped (only rank 0 reports), stderr passes through.
     Returns the worst exit code. The caller must not have touched a GPU: the children
     open the devices."""

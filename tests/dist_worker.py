@@ -19,6 +19,8 @@ def main(out_path):
     import test_golden as G
     from risc0_amd.segments import gather_results, segments_for_rank, timed_segments
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    # launch_local bound this rank to one device (r0vm's CUDA_VISIBLE_DEVICES=idx)
+    assert os.environ["HIP_VISIBLE_DEVICES"] == str(rank) and os.environ["R0_RANK_BOUND"] == "1"
     dist.init_process_group("gloo", init_method="env://")
     cases = G.INDEX["seals"]
     suites = {"poseidon2": oracle.POSEIDON2, "sha-256": oracle.SHA256, "poseidon_254": oracle.POSEIDON254}

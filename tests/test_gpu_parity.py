@@ -348,21 +348,31 @@ def test_combos_prepare_and_divide(hal, oracle):
 
 
 def test_poly_divide_exact(hal, oracle):
-    # a polynomial with root z divides exactly: remainder 0 and the quotient matches
+    """A polynomial with root z divides exactly (poly_divide, core/poly.rs:81-89): p = q(x)(x - z)
+    for a random q of degree n - 2 comes back as q with a zero remainder (no bad chunk), and
+    the same p plus one leaves the nonzero remainder reported."""
+    import poly_ext_def as D
     rng = np.random.default_rng(14)
     n = 1 << 20
-    q = oracle.rand_elems(rng, 4 * n)
-    q[-4:] = 0  # degree n-2 quotient
+    q = oracle.rand_elems(rng, 4 * n).reshape(n, 4)
+    q[-1] = 0  # degree n - 2
     z = oracle.rand_elems(rng, 4)
-    # p = q * (x - z) computed with the oracle's ext arithmetic via combos_divide's inverse
-    # check instead: divide random p, then p == q*(x-z) + r elementwise via oracle
-    p = oracle.rand_elems(rng, 4 * n)
+    qd = D.dec(q).T  # (4, n) plain values
+    zd = np.repeat(D.dec(z).reshape(4, 1), n, axis=1)
+    shifted = np.concatenate([np.zeros((4, 1), np.uint64), qd[:, :-1]], axis=1)  # q_{i-1}
+    pd = (shifted + np.uint64(D.P) - D._mul(zd, qd)) % np.uint64(D.P)  # p_i = q_{i-1} - z q_i
+    p = D.enc(pd).T.astype(np.uint32).reshape(-1)
     d = hal.copy_from_extelem("p", p)
     begin = np.array([0, 1], np.uint32)
-    hal.combos_divide(d, z, begin, n)
-    ref = p.copy()
+    assert hal.combos_divide(d, z, begin, n) == -1
+    assert np.array_equal(d.to_numpy(), q.reshape(-1))
+    p1 = p.copy()
+    p1[0] = oracle.encode(np.array([oracle.decode(np.array([p[0]]))[0] + 1]))[0]
+    d1 = hal.copy_from_extelem("p", p1)
+    assert hal.combos_divide(d1, z, begin, n) == 0
+    ref = p1.copy()
     oracle.combos_divide(ref, z, begin, n)
-    assert np.array_equal(d.to_numpy(), ref)
+    assert np.array_equal(d1.to_numpy(), ref)
 
 
 @pytest.mark.parametrize("circuit", ["rv32im", "recursion"])

@@ -26,6 +26,24 @@ def test_rank_env_matches_torchrun():
         ("3", "3", "8", "127.0.0.1", "29500")
 
 
+def test_rank_binds_one_device_like_r0vm():
+    """Each rank sees only its own GPU, as r0vm's workers do (CUDA_VISIBLE_DEVICES=idx,
+    r0vm/src/actors/mod.rs:449-462), and opens it as ordinal 0."""
+    from risc0_amd.segments import narrow_visible_devices
+    assert rank_env(3, 8, 1, base={})["HIP_VISIBLE_DEVICES"] == "3"
+    # an inherited list is indexed by the local rank
+    assert rank_env(1, 2, 1, base={"HIP_VISIBLE_DEVICES": "4,6"})["HIP_VISIBLE_DEVICES"] == "6"
+    e = rank_env(2, 4, 1, base={"CUDA_VISIBLE_DEVICES": "0,1,2,3"})
+    assert e["HIP_VISIBLE_DEVICES"] == "2" and "CUDA_VISIBLE_DEVICES" not in e
+    # the child (bench.py) binds again: already bound, it keeps its one device, ordinal 0
+    assert narrow_visible_devices(2, e) == 0 and e["HIP_VISIBLE_DEVICES"] == "2"
+    # torch.distributed.run ranks (no launch_local) bind themselves
+    env = {"LOCAL_RANK": "5"}
+    assert narrow_visible_devices(5, env) == 0 and env["HIP_VISIBLE_DEVICES"] == "5"
+    with pytest.raises(RuntimeError):
+        narrow_visible_devices(2, {"HIP_VISIBLE_DEVICES": "0,1"})
+
+
 @pytest.mark.timeout(300)
 def test_two_ranks_prove_golden_segments(oracle, tmp_path):
     if oracle.ref_lib() is None:

@@ -241,7 +241,7 @@ ORDER = os.environ.get("EC_ORDER", "dfs")
 PF = int(os.environ.get("EC_PF", "512"))
 # minimum waves per SIMD requested from the register allocator (1 = no limit)
 WAVES = int(os.environ.get("EC_WAVES", "2"))
-# Variants measured on MI355X (per-kernel rocprofv3 sums, rv32im po2=20, tools/ec_variants.sh):
+# Variants measured on MI355X (per-kernel rocprofv3 sums, rv32im po2=20, tools/rehearsal/ec_variants.sh):
 #   canonical results (default)                  28.6-28.8 ms
 #   EC_CANON=0 lazy range analysis               34.3-34.8 ms: 2-11% fewer VALU instructions,
 #                                                but more live registers -> spills in 6 kernels

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Build eval_check variants (generator env knobs) into risc0_amd/lib_variants/libr0hip_tune_<name>.so
-#   bash tools/ec_variants.sh NAME "ENV=VAL ..." [NAME "ENV=..."]...
+#   bash tools/rehearsal/ec_variants.sh NAME "ENV=VAL ..." [NAME "ENV=..."]...
 set -e
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p $ROOT/risc0_amd/lib_variants

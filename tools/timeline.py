@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """What one segment's latency is made of, from a rocprofv3 --kernel-trace
---memory-copy-trace run of tools/micro/one_segment.py (tools/gpu_oneseg.sh):
+--memory-copy-trace run of tools/micro/one_segment.py (tools/rehearsal/gpu_oneseg.sh):
 the last segment's copies (start/end relative to its large data copy) and the GPU's
 kernel-busy time in 8 ms windows.
 
