@@ -38,12 +38,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=6,
                     help="segments of the end-to-end (pinned host witness -> H2D -> seal) leg; 0 = skip")
-    ap.add_argument("--accum-steps", type=int, default=0,
-                    help="segments of an extra leg that runs the rv32im accumulation inside the prover on "
-                         "the resident witness (r0hip_prove_segment_accum); 0 = skip. The default line "
-                         "reports the accumulation through the pipeline (end_to_end.with_device_accumulation); "
-                         "inside a full bench process this 2-thread leg measures 64 or 75-81 ms/segment "
-                         "run to run, 64 in a fresh process (tools/micro/accum_leg_probe.py)")
+    ap.add_argument("--accum-steps", type=int, default=8,
+                    help="segments of the leg that runs the rv32im accumulation inside the prover on the "
+                         "resident witness (r0hip_prove_segment_accum), as the reference's prove_core does; "
+                         "reported beside value as with_accumulation; 0 = skip")
     ap.add_argument("--cpu-po2", type=int, default=None,
                     help="segment size of the CPU baseline proof (default: the bench's own po2, at most 20)")
     ap.add_argument("--inflight", type=int, default=None,

@@ -106,10 +106,10 @@ const char* r0hip_memcpy_d2d(void* d_dst, const void* d_src, size_t bytes) {
   return wrap([&] { HIP_OK(hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, stream())); });
 }
 const char* r0hip_host_alloc(void** h_ptr, size_t bytes) {
-  return wrap([&] { HIP_OK(hipHostMalloc(h_ptr, bytes, hipHostMallocDefault)); });
+  return wrap([&] { *h_ptr = host_alloc(bytes); });
 }
 const char* r0hip_host_free(void* h_ptr) {
-  return wrap([&] { HIP_OK(hipHostFree(h_ptr)); });
+  return wrap([&] { host_free(h_ptr); });
 }
 const char* r0hip_synchronize(void) {
   return wrap([] {});
@@ -396,7 +396,10 @@ const char* r0hip_mem_reset_peak(void) {
 }
 
 const char* r0hip_trim(void) {
-  return wrap([&] { dev_trim(); });
+  return wrap([&] {
+    dev_trim();
+    host_trim();
+  });
 }
 
 }  // extern "C"

@@ -10,6 +10,11 @@ namespace r0 {
 void* dev_alloc(size_t bytes);
 void dev_free(void* p);
 void dev_trim();  // return pooled blocks to the driver
+// page-locked host buffers (r0hip_host_alloc): freed blocks are kept pinned for reuse,
+// host_trim() returns the idle ones to the driver
+void* host_alloc(size_t bytes);
+void host_free(void* p);
+void host_trim();
 void set_device(int ordinal);
 
 // RAII buffer of u32 words.

@@ -360,6 +360,61 @@ void dev_free(void* p) {
   t_ctx.pool.emplace(bytes, p);  // reused only by this thread, i.e. on this stream
 }
 
+// ---- page-locked host memory (r0hip_host_alloc / r0hip_host_free) ----------------
+// Freed blocks stay page-locked in a size-keyed list for the next request instead of going
+// back through hipHostFree. Unpinning host memory is not free for the device: after the
+// bench's end-to-end leg released its 2.2 GB of pinned witness buffers, every later proof
+// in the process ran 10-15 ms slower (a kernel early in each proof ran 20-30x longer while
+// the other stream's kernels could not start), and keeping those buffers
+// pinned removed the slowdown. r0hip_trim releases the list.
+namespace {
+std::mutex g_host_mu;
+std::multimap<size_t, void*> g_host_free;
+std::map<void*, size_t> g_host_size;
+}  // namespace
+
+void* host_alloc(size_t bytes) {
+  if (bytes == 0) bytes = 1;
+  {
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    auto it = g_host_free.lower_bound(bytes);
+    if (it != g_host_free.end() && it->first <= 2 * bytes) {
+      void* p = it->second;
+      g_host_free.erase(it);
+      return p;
+    }
+  }
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+    host_trim();  // pinned memory is a system resource: give back the idle blocks, retry once
+    HIP_OK(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+  }
+  std::lock_guard<std::mutex> lk(g_host_mu);
+  g_host_size[p] = bytes;
+  return p;
+}
+
+void host_free(void* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_host_mu);
+  auto it = g_host_size.find(p);
+  R0_REQUIRE(it != g_host_size.end(), "r0hip_host_free: pointer was not returned by r0hip_host_alloc");
+  g_host_free.emplace(it->second, p);
+}
+
+void host_trim() {
+  std::vector<void*> release;
+  {
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    for (auto& kv : g_host_free) {
+      release.push_back(kv.second);
+      g_host_size.erase(kv.second);
+    }
+    g_host_free.clear();
+  }
+  for (void* p : release) (void)hipHostFree(p);
+}
+
 void dev_trim() {
   if (t_ctx.stream) HIP_OK(hipStreamSynchronize(t_ctx.stream));
   for (auto& kv : t_ctx.pool) counted_free(kv.second, kv.first);

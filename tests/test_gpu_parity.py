@@ -1020,3 +1020,26 @@ def test_satisfying_recursion_program_gpu_seal_passes_validity(hal, hal_sha, ora
     with pytest.raises(r.R0HipError):
         r.verify_seal("recursion", s, seal_b)
     assert r.verify_seal("recursion", s, seal_b, check_validity=False) == po2
+
+
+def test_pinned_host_buffers_are_pooled(hal):
+    """r0hip_host_free keeps the block page-locked for the next r0hip_host_alloc of its size
+    (unpinning stalled later proofs); r0hip_trim returns idle blocks; a pointer
+    the library did not allocate is refused."""
+    import ctypes
+    import risc0_amd as r
+    lib = r.lib()
+    a, b = ctypes.c_void_p(), ctypes.c_void_p()
+    r.check(lib.r0hip_host_alloc(ctypes.byref(a), 3 << 20))
+    arr = np.ctypeslib.as_array(ctypes.cast(a, ctypes.POINTER(ctypes.c_uint32)), shape=(3 << 18,))
+    arr[:] = np.arange(3 << 18, dtype=np.uint32)
+    d = hal.alloc_elem("x", 3 << 18)
+    r.check(lib.r0hip_memcpy_h2d(d.ptr, a, 3 << 20))
+    assert np.array_equal(d.to_numpy(), np.arange(3 << 18, dtype=np.uint32))
+    r.check(lib.r0hip_host_free(a))
+    r.check(lib.r0hip_host_alloc(ctypes.byref(b), 3 << 20))
+    assert b.value == a.value
+    r.check(lib.r0hip_host_free(b))
+    with pytest.raises(r.R0HipError, match="not returned by r0hip_host_alloc"):
+        r.check(lib.r0hip_host_free(ctypes.c_void_p(arr.ctypes.data + 4096)))
+    r.trim()
