@@ -191,6 +191,32 @@ const char* r0hip_recursion_accum(const uint32_t* d_ctrl, const uint32_t* d_glob
                                   const uint32_t* d_mix, uint32_t* d_accum, size_t work_cycles,
                                   size_t total_cycles);
 
+/* ---- recursion witness generation (risc0_circuit_recursion_cuda_witgen / _cpu_witgen,
+ * recursion-sys/kernels/cxx/ffi.cpp:191-205, driven by circuit/recursion/src/prove/witgen.rs:
+ * 91-100 in StepMode::Parallel) ----
+ * From the control group (d_ctrl, 23 columns x total_cycles rows, the program's rows first)
+ * and the preflight trace (RawPreflightTrace, prove/preflight.rs): h_wom the write-once
+ * memory (n_wom FpExt, 4 Montgomery words each), h_cycles {iopIdx, isParSafe} per work
+ * cycle (n_cycles pairs of words), h_iops the IOP values read (n_iops FpExt). Fills d_data
+ * (128 columns x total_cycles, INVALID-filled by the caller as witgen.rs:68-72 allocates it)
+ * and d_global (32 words, INVALID-filled): step_exec per cycle (runs of non-parallel-safe
+ * cycles in order), the WOM argument sorted and scanned, injectWomBacks, step_verify_mem.
+ * Fails with the reference's message on a failed check ("eqz failed at: ..."). ZK noise and
+ * zeroize stay the caller's (witgen.rs:101-123). */
+const char* r0hip_recursion_witgen(const uint32_t* d_ctrl, uint32_t* d_data, uint32_t* d_global, size_t total_cycles,
+                                   const uint32_t* h_wom, size_t n_wom, const uint32_t* h_cycles, size_t n_cycles,
+                                   const uint32_t* h_iops, size_t n_iops);
+/* A whole recursion proof from a program and its preflight (RecursionProverImpl::prove,
+ * circuit/recursion/src/prove/mod.rs:160-230): witness generation as above, ZK noise in the
+ * last 1024 rows of data and accum (per-cell values of r0hip_fill_uniform(noise_seed) and
+ * (noise_seed + 1), laid out as witgen.rs:101-158 copies its noise matrices), zeroize, then
+ * r0hip_prove_segment_accum's sequence with work cycles = n_cycles. po2 >= 11 and n_cycles <=
+ * 2^po2 - 1024 (program.rs:57). Seal and mix out as r0hip_prove_segment. */
+const char* r0hip_prove_recursion(int suite, uint32_t po2, const uint32_t* d_ctrl, const uint32_t* h_wom, size_t n_wom,
+                                  const uint32_t* h_cycles, size_t n_cycles, const uint32_t* h_iops, size_t n_iops,
+                                  uint64_t noise_seed, uint32_t* h_seal, size_t seal_cap, size_t* seal_len,
+                                  uint32_t* h_mix_out);
+
 /* ---- segment pipeline (r0vm's per-GPU worker queue, r0vm/src/actors/worker.rs:75-76, over the
  * zkvm's per-segment prove loop, zkvm/src/host/server/prove/prover_impl.rs:84-94) ----
  * Proves njobs segments of one (circuit, suite, po2) from HOST witness buffers: an uploader

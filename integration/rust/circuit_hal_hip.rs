@@ -7,9 +7,10 @@
 // gfx950 from the circuit, tools/gen_eval_check.py), and so do both circuits' accumulations:
 // rv32im's three phases (r0hip_rv32im_accum: stepAccum generated from the reference's
 // step_TopAccum, the scan and finalizeAccum) and the recursion circuit's
-// (r0hip_recursion_accum). Witness generation (stepExec) of both circuits stays on the host
-// CPU code of the circuit crates (the same C++ the CPU HAL calls), and its result is uploaded
-// once: a GPU stepExec for rv32im is SURVEY.md §8(f) rank 1.
+// (r0hip_recursion_accum), and the recursion circuit's witness generation
+// (r0hip_recursion_witgen). rv32im witness generation (stepExec) stays on the host CPU code of
+// the circuit crate (the same C++ the CPU HAL calls), and its result is uploaded once: a GPU
+// stepExec for rv32im needs the executor's preflight.
 //
 // Selection (one arm each):
 //   circuit/rv32im/src/prove/mod.rs:45-55       if #[cfg(feature = "hip")] { self::hal::hip::segment_prover() }
@@ -241,8 +242,8 @@ mod tests {
 // ===================== risc0/circuit/recursion/src/prove/hal/hip.rs ======================
 // (separate file; its own imports)
 //
-// use risc0_circuit_recursion_sys::{RawAccumBuffers, RawExecBuffers, RawPreflightTrace,
-//     risc0_circuit_recursion_cpu_accum, risc0_circuit_recursion_cpu_witgen};
+// use risc0_circuit_recursion_sys::RawPreflightTrace;
+// use risc0_sys::hip::{r0hip_eval_check, r0hip_recursion_accum, r0hip_recursion_witgen};
 // use risc0_zkp::hal::hip::{HipHal, HipHashPoseidon2, HipHashPoseidon254, HipHashSha256};
 // use super::{CircuitAccumulator, CircuitWitnessGenerator, RecursionProver, RecursionProverImpl};
 // use crate::{REGISTER_GROUP_ACCUM, REGISTER_GROUP_CTRL, REGISTER_GROUP_DATA, GLOBAL_MIX, GLOBAL_OUT};
@@ -250,16 +251,19 @@ mod tests {
 // pub struct HipRecursionCircuitHal<HS: HipHash> { _hal: Rc<HipHal<HS>> }
 //
 // impl<HS: HipHash> CircuitWitnessGenerator<HipHal<HS>> for HipRecursionCircuitHal<HS> {
-//     fn generate_witness(&self, mode: StepMode, total_cycles: u32, preflight: &RawPreflightTrace,
+//     fn generate_witness(&self, _mode: StepMode, total_cycles: u32, preflight: &RawPreflightTrace,
 //                         ctrl: &BufferImpl<BabyBearElem>, data: &BufferImpl<BabyBearElem>,
 //                         global: &BufferImpl<BabyBearElem>) -> Result<()> {
-//         // host images of ctrl/data/global, the CPU witgen (recursion-sys ffi.cpp), then upload
-//         let (mut c, mut d, mut g) = (ctrl.to_vec(), data.to_vec(), global.to_vec());
-//         let buffers = RawExecBuffers { ctrl: c.as_ptr(), data: d.as_mut_ptr(), global: g.as_mut_ptr() };
-//         ffi_wrap(|| unsafe { risc0_circuit_recursion_cpu_witgen(mode, &buffers, preflight, total_cycles) })?;
-//         data.view_mut(|v| v.copy_from_slice(&d));
-//         global.view_mut(|v| v.copy_from_slice(&g));
-//         Ok(())
+//         // on the device (r0hip_recursion_witgen: step_exec, the WOM sort and scan,
+//         // injectWomBacks and step_verify_mem of recursion-sys ffi.cpp:57-205, generated from
+//         // the reference's step code); the RawPreflightTrace arrays are host memory. The
+//         // result is the same for every StepMode, as the reference's modes agree.
+//         ffi_wrap(|| unsafe {
+//             r0hip_recursion_witgen(ctrl.dev(), data.dev(), global.dev(), total_cycles as usize,
+//                 preflight.wom as *const u32, preflight.num_woms as usize,
+//                 preflight.cycles as *const u32, preflight.num_cycles as usize,
+//                 preflight.iops as *const u32, preflight.num_iops as usize)
+//         })
 //     }
 // }
 //

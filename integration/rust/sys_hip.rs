@@ -232,6 +232,36 @@ unsafe extern "C" {
         h_backs: *const R0HipBigIntBack,
         n: usize,
     ) -> *const c_char;
+    /// risc0_circuit_recursion_cuda_witgen's role (recursion-sys ffi.cpp:191-205)
+    pub fn r0hip_recursion_witgen(
+        d_ctrl: *const u32,
+        d_data: *mut u32,
+        d_global: *mut u32,
+        total_cycles: usize,
+        h_wom: *const u32,
+        n_wom: usize,
+        h_cycles: *const u32,
+        n_cycles: usize,
+        h_iops: *const u32,
+        n_iops: usize,
+    ) -> *const c_char;
+    /// RecursionProverImpl::prove from the program and its preflight (recursion prove/mod.rs:160-230)
+    pub fn r0hip_prove_recursion(
+        suite: c_int,
+        po2: u32,
+        d_ctrl: *const u32,
+        h_wom: *const u32,
+        n_wom: usize,
+        h_cycles: *const u32,
+        n_cycles: usize,
+        h_iops: *const u32,
+        n_iops: usize,
+        noise_seed: u64,
+        h_seal: *mut u32,
+        seal_cap: usize,
+        seal_len: *mut usize,
+        h_mix_out: *mut u32,
+    ) -> *const c_char;
     pub fn r0hip_prove_segments(
         circuit: *const c_char,
         suite: c_int,

@@ -6,6 +6,7 @@
 #include "../../include/r0hip.h"
 
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 #include <vector>
@@ -282,6 +283,59 @@ const char* r0hip_recursion_accum(const uint32_t* d_ctrl, const uint32_t* d_glob
     recursion_accum(stream(), d_ctrl, d_global, d_data, d_mix, d_accum, work_cycles, total_cycles);
   });
 }
+const char* r0hip_recursion_witgen(const uint32_t* d_ctrl, uint32_t* d_data, uint32_t* d_global, size_t total_cycles,
+                                   const uint32_t* h_wom, size_t n_wom, const uint32_t* h_cycles, size_t n_cycles,
+                                   const uint32_t* h_iops, size_t n_iops) {
+  return wrap([&] {
+    R0_REQUIRE(d_ctrl && d_data && d_global, "r0hip_recursion_witgen: null argument");
+    stage_reset();
+    recursion_witgen(stream(), d_ctrl, d_data, d_global, total_cycles, h_wom, n_wom, h_cycles, n_cycles, h_iops,
+                     n_iops);
+  });
+}
+
+const char* r0hip_prove_recursion(int suite, uint32_t po2, const uint32_t* d_ctrl, const uint32_t* h_wom, size_t n_wom,
+                                  const uint32_t* h_cycles, size_t n_cycles, const uint32_t* h_iops, size_t n_iops,
+                                  uint64_t noise_seed, uint32_t* h_seal, size_t seal_cap, size_t* seal_len,
+                                  uint32_t* h_mix_out) {
+  return wrap([&] {
+    const CircuitDef* c = find_circuit("recursion");
+    R0_REQUIRE(c && d_ctrl, "r0hip_prove_recursion: null argument");
+    R0_REQUIRE(po2 >= 11 && po2 <= 24, "r0hip_prove_recursion: po2 out of range (ZK rows need po2 >= 11)");
+    constexpr size_t kZk = 1024;  // risc0_zkp::ZK_CYCLES (zkp/src/lib.rs:42)
+    const size_t n = size_t(1) << po2;
+    R0_REQUIRE(n_cycles <= n - kZk, "r0hip_prove_recursion: program longer than 2^po2 - ZK_CYCLES rows");
+    const size_t data_cols = c->group_size(2), accum_cols = c->group_size(0);
+    hipStream_t s = stream();
+    stage_reset();
+    // WitnessGenerator::new (circuit/recursion/src/prove/witgen.rs:44-133)
+    DevBuf data(data_cols * n), global(c->output_size), accum(accum_cols * n), noise(std::max(data_cols, accum_cols) * kZk);
+    HIP_OK(hipMemsetD32Async(data.p, 0xFFFFFFFFu, data.words, s));
+    HIP_OK(hipMemsetD32Async(global.p, 0xFFFFFFFFu, global.words, s));
+    recursion_witgen(s, d_ctrl, data.p, global.p, n, h_wom, n_wom, h_cycles, n_cycles, h_iops, n_iops);
+    // ZK noise in the last ZK_CYCLES data rows (witgen.rs:101-116: eltwise_copy_elem_slice
+    // from a data_size x ZK_CYCLES noise matrix), here per-cell values of r0hip_fill_uniform
+    fill_uniform(s, noise.p, data_cols * kZk, noise_seed);
+    copy_elem_slice(s, data.p, noise.p, data_cols, kZk, 0, kZk, n - kZk, n);
+    eltwise_zeroize(s, data.p, data.words);
+    // WitnessGenerator::accum (witgen.rs:134-177): INVALID plus noise rows, then the
+    // accumulation inside the proof; prove (prove/mod.rs:160-230)
+    HIP_OK(hipMemsetD32Async(accum.p, 0xFFFFFFFFu, accum.words, s));
+    fill_uniform(s, noise.p, accum_cols * kZk, noise_seed + 1);
+    copy_elem_slice(s, accum.p, noise.p, accum_cols, kZk, 0, kZk, n - kZk, n);
+    std::vector<uint32_t> mix;
+    const AccumStep acc{accum.p, n_cycles};
+    std::vector<uint32_t> seal =
+        prove_segment(*c, suite, po2, d_ctrl, data.p, nullptr, global.p, false, 0, &mix, nullptr, &acc);
+    if (seal_len) *seal_len = seal.size();
+    if (h_mix_out) memcpy(h_mix_out, mix.data(), mix.size() * 4);
+    if (h_seal) {
+      R0_REQUIRE(seal.size() <= seal_cap, "seal buffer too small");
+      memcpy(h_seal, seal.data(), seal.size() * 4);
+    }
+  });
+}
+
 const char* r0hip_fill_uniform(uint32_t* d_out, size_t count, uint64_t seed) {
   return wrap([&] { fill_uniform(stream(), d_out, count, seed); });
 }

@@ -91,6 +91,13 @@ enum ScratchSlot : int {
   kSlotAccTileSums = 62,
   kSlotBigIntRows = 63,
   kSlotBigIntStates = 64,
+  // recursion witness generation (recursion_witgen.hip): the uploaded preflight trace, the
+  // exec runs, each cycle's first IOP value, hipcub temporary storage
+  kSlotWitgenWom = 70,
+  kSlotWitgenIops = 71,
+  kSlotWitgenRuns = 72,
+  kSlotWitgenIopIdx = 73,
+  kSlotWitgenTemp = 74,
 };
 
 // Scratch buffer reused across calls (grown on demand; stream-ordered use only).
@@ -221,6 +228,13 @@ void bigint_scatter(hipStream_t s, uint32_t* accum, size_t rows, const uint32_t*
 // recursion circuit accumulation (recursion_accum.hip): compute, prefix product, verify
 void recursion_accum(hipStream_t s, const uint32_t* ctrl, const uint32_t* global, const uint32_t* data,
                      const uint32_t* mix, uint32_t* accum, size_t steps, size_t cycles);
+// recursion circuit witness generation (recursion_witgen.hip; risc0_circuit_recursion_cpu_witgen,
+// recursion-sys/kernels/cxx/ffi.cpp:191-205): data (INVALID-filled) and global written from the
+// control group and the preflight trace (WOM and IOP values 4 words each, cycles {iopIdx,
+// isParSafe}); synchronises, throws on a failed check
+void recursion_witgen(hipStream_t s, const uint32_t* ctrl, uint32_t* data, uint32_t* global, size_t total_cycles,
+                      const uint32_t* h_wom, size_t n_wom, const uint32_t* h_cycles, size_t ncycles,
+                      const uint32_t* h_iops, size_t n_iops);
 void eltwise_sum_extelem(hipStream_t s, uint32_t* out, const uint32_t* in, size_t count, size_t to_add);
 void fri_fold(hipStream_t s, uint32_t* out, const uint32_t* in, FpExt mix, size_t count);
 void gather_sample(hipStream_t s, uint32_t* dst, const uint32_t* src, size_t idx, size_t size, size_t stride);

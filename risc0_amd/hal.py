@@ -88,6 +88,9 @@ def _declare(L):
         "r0hip_prove_segment_accum": [C.c_char_p, C.c_int, C.c_uint32, vp, vp, vp, sz, vp, sz, vp, C.c_int,
                                       C.c_uint32, u32p, sz, C.POINTER(sz), u32p],
         "r0hip_rv32im_bigint_accum_states": [u32p, vp, sz, sz, u32p],
+        "r0hip_recursion_witgen": [vp, vp, vp, sz, u32p, sz, u32p, sz, u32p, sz],
+        "r0hip_prove_recursion": [C.c_int, C.c_uint32, vp, u32p, sz, u32p, sz, u32p, sz, C.c_uint64, u32p, sz,
+                                  C.POINTER(sz), u32p],
         "r0hip_rv32im_bigint_accum_inject": [vp, sz, u32p, vp, sz],
         "r0hip_last_profile": [C.c_char_p, sz],
         "r0hip_set_kernel_timing": [C.c_int],
@@ -409,6 +412,38 @@ def prove_segment_accum(hal, circuit, po2, code, data, accum, work_cycles, glob,
                                           version or 0,
                                           seal.ctypes.data_as(u32p), seal_cap, C.byref(n),
                                           mix.ctypes.data_as(u32p)))
+    return seal[: n.value].copy(), mix
+
+
+def _trace(wom, cycles, iops):
+    w = np.ascontiguousarray(np.asarray(wom, dtype=np.uint32).reshape(-1))
+    c = np.ascontiguousarray(np.asarray(cycles, dtype=np.uint32).reshape(-1))
+    i = np.ascontiguousarray(np.asarray(iops, dtype=np.uint32).reshape(-1))
+    assert w.size % 4 == 0 and c.size % 2 == 0 and i.size % 4 == 0
+    return w, c, i
+
+
+def recursion_witgen(ctrl, data, glob, total_cycles, wom, cycles, iops):
+    """r0hip_recursion_witgen: the recursion circuit's witness generation on the device from
+    the control group and the preflight trace (wom: (k, 4) words, cycles: [(iop_idx,
+    is_par_safe)], iops: (m, 4) words); data and glob must arrive INVALID-filled."""
+    w, c, i = _trace(wom, cycles, iops)
+    check(lib().r0hip_recursion_witgen(ctrl.ptr, data.ptr, glob.ptr, total_cycles, w.ctypes.data_as(u32p), w.size // 4,
+                                       c.ctypes.data_as(u32p), c.size // 2, i.ctypes.data_as(u32p), i.size // 4))
+
+
+def prove_recursion(hal, po2, ctrl, wom, cycles, iops, noise_seed, seal_cap=1 << 24):
+    """r0hip_prove_recursion: a whole recursion proof from the program's control group and its
+    preflight trace (witness generation, ZK noise from noise_seed, accumulation, prove).
+    Returns (seal, mix)."""
+    w, c, i = _trace(wom, cycles, iops)
+    seal = np.zeros(seal_cap, dtype=np.uint32)
+    n = C.c_size_t(0)
+    mix = np.zeros(20, dtype=np.uint32)
+    check(lib().r0hip_prove_recursion(hal.suite, po2, ctrl.ptr, w.ctypes.data_as(u32p), w.size // 4,
+                                      c.ctypes.data_as(u32p), c.size // 2, i.ctypes.data_as(u32p), i.size // 4,
+                                      noise_seed, seal.ctypes.data_as(u32p), seal_cap, C.byref(n),
+                                      mix.ctypes.data_as(u32p)))
     return seal[: n.value].copy(), mix
 
 

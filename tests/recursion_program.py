@@ -327,11 +327,11 @@ def ctrl_group(program, po2):
     return ctrl.reshape(-1)
 
 
-def witgen(program, pf, po2, noise_seed=None):
+def witgen(program, pf, po2, noise_seed=None, raw=False):
     """(ctrl, data, global) Montgomery words: the reference's compiled witgen in parallel mode
     (ffi.cpp:191-205) over the preflight trace, then (witgen.rs:101-123) the last ZK_CYCLES
     data rows set to one random value (vec![random; n], as the reference does) and INVALID
-    words zeroized."""
+    words zeroized; raw=True returns the witness generator's output before those two."""
     n = 1 << po2
     ctrl = ctrl_group(program, po2)
     data = np.full(DATA * n, INVALID, np.uint32)
@@ -348,6 +348,8 @@ def witgen(program, pf, po2, noise_seed=None):
     err = lib.risc0_circuit_recursion_cpu_witgen(0, C.byref(bufs), C.byref(tr), n)
     if err:
         raise RuntimeError(C.cast(err, C.c_char_p).value.decode())
+    if raw:  # the witness generator's own output: no ZK noise, INVALID words kept
+        return ctrl, data, glob
     rng = np.random.default_rng(noise_seed)
     d = data.reshape(DATA, n)
     d[:, n - ZK_CYCLES:] = enc(int(rng.integers(0, P)))
@@ -491,6 +493,14 @@ def random_program(rng, max_rows, blocks=("arith", "bits", "mix_rng", "iop", "po
     while len(b.p.rows) + 40 < max_rows:
         getattr(b, "block_" + blocks[int(rng.integers(0, len(blocks)))])()
     return b.finish()
+
+
+def trace_arrays(pf):
+    """the preflight trace as the witness generator takes it (RawPreflightTrace): WOM and
+    IOP values as (k, 4) Montgomery words, cycles as [(iop_idx, is_par_safe)]"""
+    wom = np.array([[enc(x) for x in v] for v in pf.wom] or np.zeros((0, 4)), np.uint32).reshape(-1, 4)
+    iops = np.array([[enc(x) for x in v] for v in pf.iops] or np.zeros((0, 4)), np.uint32).reshape(-1, 4)
+    return wom, list(pf.cycles), iops
 
 
 def satisfying_witness(seed, po2, max_rows=None, blocks=("arith", "bits", "mix_rng", "iop", "poseidon2")):

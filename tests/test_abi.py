@@ -26,11 +26,13 @@ def test_exports_are_c_linkage():
 
 
 def test_library_is_gfx950_only():
+    """every device code object in the library's offload bundles targets gfx950 (hipcub's
+    host code names other architectures in its tuning tables; those are strings, not code)"""
     lib = os.path.join(ROOT, "risc0_amd", "lib", "libr0hip.so")
     data = open(lib, "rb").read()
-    assert b"gfx950" in data
-    for other in (b"gfx942", b"gfx90a", b"sm_"):
-        assert other not in data or other == b"sm_"
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", data))
+    assert targets == {b"gfx950"}, targets
+    assert b"nvptx" not in data
 
 
 def test_errors_are_reported_not_fatal():

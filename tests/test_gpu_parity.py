@@ -1043,3 +1043,95 @@ def test_pinned_host_buffers_are_pooled(hal):
     with pytest.raises(r.R0HipError, match="not returned by r0hip_host_alloc"):
         r.check(lib.r0hip_host_free(ctypes.c_void_p(arr.ctypes.data + 4096)))
     r.trim()
+
+
+# ---- recursion witness generation on the GPU (r0hip_recursion_witgen, r0hip_prove_recursion) ----
+
+@pytest.mark.parametrize("po2,rows,blocks", [
+    (14, None, ("arith", "bits", "mix_rng", "iop", "poseidon2")),
+    (18, None, ("arith", "bits", "mix_rng", "iop", "poseidon2")),
+    (12, 1500, ("poseidon2",)),
+    (12, 1500, ("iop", "mix_rng", "bits")),
+])
+def test_recursion_witgen_matches_reference(hal, po2, rows, blocks):
+    """r0hip_recursion_witgen (generated step_exec / step_verify_mem kernels, the WOM
+    argument sorted and scanned on the device, injectWomBacks) writes the same data group and
+    globals, INVALID words included, as the reference's compiled
+    risc0_circuit_recursion_cpu_witgen on a program filling the segment (restated preflight,
+    tests/recursion_program.py)."""
+    import recursion_program as RP
+    import risc0_amd as r
+    if not RP.available():
+        pytest.skip("oracle/_ref/libref_recursion.so not built")
+    n = 1 << po2
+    rng = np.random.default_rng(2000 + po2 + (rows or 0))
+    prog, inp = RP.random_program(rng, rows or n - RP.ZK_CYCLES - 1, blocks)
+    pf = RP.preflight(prog, inp)
+    ctrl, data, glob = RP.witgen(prog, pf, po2, raw=True)
+    wom, cyc, iops = RP.trace_arrays(pf)
+    dd = dev(hal, np.full(RP.DATA * n, RP.INVALID, np.uint32))
+    dg = dev(hal, np.full(RP.OUT, RP.INVALID, np.uint32))
+    r.recursion_witgen(dev(hal, ctrl), dd, dg, n, wom, cyc, iops)
+    got = dd.to_numpy()
+    bad = np.nonzero(got != data)[0]
+    assert bad.size == 0, f"{bad.size} words differ; first col {bad[0] // n} row {bad[0] % n}"
+    assert np.array_equal(dg.to_numpy(), glob)
+
+
+def test_recursion_witgen_reports_a_failed_check(hal):
+    """A hole in the write-once memory fails the sorted-memory check as in the reference
+    (eqz at zirgen/circuit/recursion/wom.cpp:74), and the library stays usable."""
+    import recursion_program as RP
+    import risc0_amd as r
+    po2, n = 11, 1 << 11
+    b = RP.Builder(np.random.default_rng(5))
+    b.consts([(3, 0), (4, 0)])
+    b.next += 1
+    b.consts([(5, 0)])
+    prog, inp = b.finish()
+    pf = RP.preflight(prog, inp)
+    wom, cyc, iops = RP.trace_arrays(pf)
+    dd = dev(hal, np.full(RP.DATA * n, RP.INVALID, np.uint32))
+    dg = dev(hal, np.full(RP.OUT, RP.INVALID, np.uint32))
+    with pytest.raises(r.R0HipError, match="wom.cpp:74"):
+        r.recursion_witgen(dev(hal, RP.ctrl_group(prog, po2)), dd, dg, n, wom, cyc, iops)
+    hal.synchronize()
+
+
+@pytest.mark.parametrize("suite,po2", [("poseidon2", 14), ("sha-256", 16), ("poseidon2", 18)])
+def test_prove_recursion_from_program(hal, hal_sha, oracle, suite, po2):
+    """r0hip_prove_recursion: a recursion proof from the program (control group) and its
+    preflight alone — witness generation, ZK noise, accumulation and the proof on the device.
+    The seal passes r0hip_verify_seal with the validity equation; at po2 14 it equals the
+    oracle prover's seal on the witness the reference's compiled witgen and accumulation make
+    with the same noise words (r0hip_fill_uniform's generator, oracle.splitmix_fill)."""
+    import recursion_program as RP
+    import risc0_amd as r
+    import verifier
+    if not RP.available() or oracle.ref_lib() is None:
+        pytest.skip("oracle/_ref not built")
+    h, s = H(suite), S(oracle, suite)
+    n = 1 << po2
+    rng = np.random.default_rng(3000 + po2)
+    prog, inp = RP.random_program(rng, n - RP.ZK_CYCLES - 1)
+    pf = RP.preflight(prog, inp)
+    wom, cyc, iops = RP.trace_arrays(pf)
+    ctrl = RP.ctrl_group(prog, po2)
+    seed = 0x5EED + po2
+    seal, mix = r.prove_recursion(h, po2, dev(h, ctrl), wom, cyc, iops, seed)
+    assert r.verify_seal("recursion", s, seal) == po2
+    if po2 == 14:
+        assert verifier.verify(oracle, "recursion", seal, s, check_validity=True)["validity"] is True
+        _, data, glob = RP.witgen(prog, pf, po2, raw=True)
+        data = data.reshape(RP.DATA, n)
+        data[:, n - RP.ZK_CYCLES:] = oracle.splitmix_fill(seed, RP.DATA * RP.ZK_CYCLES).reshape(RP.DATA, RP.ZK_CYCLES)
+        data = np.where(data == RP.INVALID, 0, data).astype(np.uint32).reshape(-1)
+        glob = np.where(glob == RP.INVALID, 0, glob).astype(np.uint32)
+        acc0 = np.full((RP.ACCUM, n), RP.INVALID, np.uint32)
+        acc0[:, n - RP.ZK_CYCLES:] = oracle.splitmix_fill(seed + 1, RP.ACCUM * RP.ZK_CYCLES).reshape(RP.ACCUM,
+                                                                                                  RP.ZK_CYCLES)
+        w = dict(ctrl=ctrl, data=data, glob=glob, work=len(prog.rows), acc0=acc0.reshape(-1))
+        acc = RP.accumulate(w, mix, po2)
+        ref_seal, ref_mix, _ = oracle.prove_segment("recursion", s, po2, ctrl, data, acc, glob)
+        assert np.array_equal(mix, ref_mix)
+        assert np.array_equal(seal, ref_seal)
