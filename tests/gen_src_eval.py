@@ -1,7 +1,13 @@
 """numpy interpreter of the C subset tools/gen_accum.py emits (one lane per cycle, all cycles
 at once): runs the generated accumulation kernels' *source text* on the CPU, so the
 generator's rewrites (batched inverses, depth-first emission, split guarded stores, load
-look-ahead) are checked against the IR interpreter without a GPU. Test infrastructure."""
+look-ahead, lazily reduced sums of products, arm-sorted kernels) are checked against the IR
+interpreter without a GPU. Test infrastructure.
+
+The 64-bit sums of a fused linear combination run in uint64 with a check that no sum wraps
+and that Montgomery REDC's input stays below p * 2^32, as the generator's bounds promise.
+An arm-sorted kernel's tile sort only permutes which lane takes which cycle, so it runs
+here as the identity."""
 import re
 
 import numpy as np
@@ -28,8 +34,18 @@ _PATTERNS = [
     ("vread", re.compile(r"const uint4 r(\d+) = A\.vals\[cycle\];$")),
     ("vget", re.compile(r"const uint32_t v(\d+) = r(\d+)\.([xyzw]);$")),
     ("vwrite", re.compile(r"A\.vals\[cycle\] = make_uint4\(v(\d+), v(\d+), v(\d+), v(\d+)\);$")),
+    ("umin", re.compile(r"const uint32_t v(\d+) = umin\(v(\d+), v(\d+)\);$")),
+    ("tdef", re.compile(r"uint64_t t(\d+) = uint64_t\(v(\d+)\) \* (v\d+|\d+u|\(kP - v\d+\));$")),
+    ("tadd", re.compile(r"t(\d+) \+= uint64_t\(v(\d+)\) \* (v\d+|\d+u|\(kP - v\d+\));$")),
+    ("tfold", re.compile(r"t(\d+) = fold64\(t(\d+)\);$")),
+    ("redc", re.compile(r"const uint32_t v(\d+) = mont_reduce\(t(\d+)\);$")),
+    ("keyblk", re.compile(r"if \(c0 < A\.steps\) \{$")),
 ]
-_SKIP = re.compile(r"^(const uint32_t (cycle|mask) = .*|if \(cycle >= A\.steps\) return;)$")
+_SKIP = re.compile(r"^(const uint32_t (cycle|mask|c0) = .*|if \(cycle >= A\.steps\) return;|"
+                   r"uint32_t key = \d+u;|key = .*;)$")
+_FOLD_C = 2**32 % P
+_NEG_PINV = (-pow(P, -1, 2**32)) % 2**32
+_M32 = np.uint64(0xFFFFFFFF)
 
 
 def kernel_body(src):
@@ -49,7 +65,15 @@ def run_kernel(src, bufs, rows, steps, vals=None):
     arrays (numpy uint32, updated in place by the stores); vals (recursion) the per-cycle
     FpExt of A.vals, int64 Montgomery words of shape (steps, 4)."""
     cyc = np.arange(steps, dtype=np.int64)
-    v, ib, rr = {}, {}, {}
+    v, ib, rr, t = {}, {}, {}, {}
+
+    def operand(e):
+        if e.startswith("(kP - v"):
+            return np.uint64(P) - v[int(e[7:-1])].astype(np.uint64)
+        if e.startswith("v"):
+            return v[int(e[1:])].astype(np.uint64)
+        return np.full(steps, int(e[:-1]), np.uint64)
+
     mask = [np.ones(steps, bool)]
     for st in kernel_body(src):
         if _SKIP.match(st):
@@ -100,6 +124,25 @@ def run_kernel(src, bufs, rows, steps, vals=None):
             sel = mask[-1]
             for k in range(4):
                 vals[sel, k] = v[int(g[k])][sel]
+        elif kind == "umin":
+            v[int(g[0])] = np.minimum(v[int(g[1])], v[int(g[2])])
+        elif kind == "tdef":
+            t[int(g[0])] = v[int(g[1])].astype(np.uint64) * operand(g[2])
+        elif kind == "tadd":
+            old = t[int(g[0])]
+            t[int(g[0])] = old + v[int(g[1])].astype(np.uint64) * operand(g[2])
+            assert (t[int(g[0])] >= old).all(), "64-bit sum wrapped"
+        elif kind == "tfold":
+            x = t[int(g[1])]
+            t[int(g[0])] = (x >> np.uint64(32)) * np.uint64(_FOLD_C) + (x & _M32)
+        elif kind == "redc":
+            x = t[int(g[1])]
+            assert (x < np.uint64(P) << np.uint64(32)).all(), "REDC input not below p * 2^32"
+            m = ((x & _M32) * np.uint64(_NEG_PINV)) & _M32
+            r = (x + m * np.uint64(P)) >> np.uint64(32)
+            v[int(g[0])] = np.where(r >= P, r - np.uint64(P), r).astype(np.int64)
+        elif kind == "keyblk":
+            mask.append(mask[-1].copy())
         elif kind == "store":
             b, col, i = int(g[0]), int(g[1]), int(g[2])
             sel = mask[-1]

@@ -20,19 +20,25 @@ from test_rv32im_accum_ir import rows_for_arms
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _generate(tmp, limit, inv_batch, ahead):
-    out = os.path.join(tmp, f"rv_{limit}_{inv_batch}_{ahead}")
+def _generate(tmp, limit, inv_batch, ahead, extra=()):
+    out = os.path.join(tmp, f"rv_{limit}_{inv_batch}_{ahead}_{'_'.join(map(str, extra))}")
     subprocess.check_call([sys.executable, os.path.join(ROOT, "tools", "gen_accum.py"), "rv32im", out,
-                           str(limit), str(inv_batch), str(ahead)], stdout=subprocess.DEVNULL)
+                           str(limit), str(inv_batch), str(ahead)] + [str(x) for x in extra],
+                          stdout=subprocess.DEVNULL)
     launcher = open(os.path.join(out, "accum.hip")).read()
     order = re.findall(r"rv_accum::launch_k(\d+)\(s, A\);", launcher)
     return [open(os.path.join(out, f"accum_k{k}.hip")).read() for k in order]
 
 
-@pytest.mark.parametrize("limit,inv_batch,ahead", [(1200, 8, 64), (1200, 1, 0), (600, 16, 0)])
+# (limit, inv batch, look-ahead, [fuse, pack, sort]): the build's settings (fused sums,
+# arm-sorted kernels packed to 20000), the fused contiguous cut, the unfused one, and the
+# unbatched program-order baseline
+@pytest.mark.parametrize("limit,inv_batch,ahead,extra", [(1200, 8, 64, ()), (1200, 8, 64, (1, 0, 0)),
+                                                         (1200, 8, 64, (0, 0, 0)), (1200, 1, 0, (0, 0, 0)),
+                                                         (600, 16, 0, (1, 8000, 256))])
 @pytest.mark.parametrize("rows,last", [(64, 64), (64, 50)])
-def test_generated_source_matches_ir(tmp_path, limit, inv_batch, ahead, rows, last):
-    kernels = _generate(str(tmp_path), limit, inv_batch, ahead)
+def test_generated_source_matches_ir(tmp_path, limit, inv_batch, ahead, extra, rows, last):
+    kernels = _generate(str(tmp_path), limit, inv_batch, ahead, extra)
     rng = np.random.default_rng(rows + last + limit + inv_batch)
     data = rows_for_arms(rng, rows, list(rng.integers(0, 13, rows)))
     glob = rng.integers(0, GS.P, 90, dtype=np.uint64).astype(np.uint32)
