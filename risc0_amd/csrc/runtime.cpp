@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstring>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <tuple>
 #include <mutex>
@@ -84,8 +85,13 @@ void raise_peak(std::atomic<uint64_t>& peak, uint64_t v) {
 void live_add(uint64_t b) { raise_peak(g_peak_live, g_mem_live.fetch_add(b, std::memory_order_relaxed) + b); }
 void live_sub(uint64_t b) { g_mem_live.fetch_sub(b, std::memory_order_relaxed); }
 // every device allocation of the library goes through these two
-hipError_t counted_malloc(void** p, size_t bytes) {
+// R0HIP_TRACE_MALLOC=1: every device allocation to stderr with its scratch slot (-1: the
+// block pool or a table), for finding allocations in a steady state
+const bool g_trace_malloc = std::getenv("R0HIP_TRACE_MALLOC") != nullptr;
+
+hipError_t counted_malloc(void** p, size_t bytes, int slot = -1) {
   const hipError_t e = hipMalloc(p, bytes);
+  if (g_trace_malloc) std::fprintf(stderr, "r0hip malloc %zu bytes slot %d -> %d\n", bytes, slot, int(e));
   if (e == hipSuccess) {
     g_mallocs.fetch_add(1, std::memory_order_relaxed);
     raise_peak(g_peak_reserved, g_reserved.fetch_add(bytes, std::memory_order_relaxed) + bytes);
@@ -197,18 +203,19 @@ void* scratch(size_t bytes, int slot) {
       std::lock_guard<std::mutex> lk(g_mu);
       auto& orph = g_scratch_orphans[slot];
       auto ot = orph.lower_bound(bytes);
-      // at most twice the block this request would allocate: a po2=10 proof must not pin a
-      // po2=24 block (it would stay live and count in mem_stats); the bench's threads ask
-      // for identical sizes, so they still find theirs
-      if (ot != orph.end() && ot->first <= 2 * want) {
+      // at most 8x the block this request would allocate: a po2=10 proof must not pin a
+      // po2=24 block (it would stay live and count in mem_stats), while a slot whose proof
+      // asks small first and then grows (eval_check's, 5.6x between its two requests) still
+      // finds the block another thread grew
+      if (ot != orph.end() && ot->first <= 8 * want) {
         s.p = ot->second;
         want = ot->first;
         orph.erase(ot);
       }
     }
-    if (!s.p && counted_malloc(&s.p, want) != hipSuccess) {
+    if (!s.p && counted_malloc(&s.p, want, slot) != hipSuccess) {
       dev_trim();
-      HIP_OK(counted_malloc(&s.p, want));
+      HIP_OK(counted_malloc(&s.p, want, slot));
     }
     s.bytes = want;
     live_add(want);

@@ -4,6 +4,8 @@ Mirrors the reference's DualHal tests (risc0/zkp/src/hal/mod.rs:319-616, shapes
 noted per test) plus what DualHal does not cover (combos_prepare/combos_divide,
 eval_check, whole-segment seals). The bar is bit-exact equality of u32 words.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -713,14 +715,22 @@ def test_steady_state_proving_makes_no_hipmalloc(oracle):
         for t in ts:
             t.join()
 
-    # two warm batches: per-proof upload sizes differ between the two seals, so the first
-    # steady thread to reach a slot may take the other thread's block; after both threads
-    # have left blocks of both patterns the pool covers either order
-    batch("warm")
-    batch("warm2")
+    # warm until a whole batch allocates nothing: some slots are asked small and then grown
+    # within a proof, and blocks go back to a shared pool at thread exit, so which thread
+    # finds which block depends on the race; once the pool holds blocks of every size both
+    # interleavings need, proving allocates no more (a leak would keep allocating here)
+    for k in range(6):
+        m0 = r.mem_stats()["mallocs"]
+        batch(f"warm{k}")
+        if k and r.mem_stats()["mallocs"] == m0:
+            break
+    else:
+        raise AssertionError("every warm batch allocated device memory")
     r.mem_reset_peak()
     before = r.mem_stats()
+    os.write(2, b"steady batch begins\n")  # brackets R0HIP_TRACE_MALLOC=1 output
     batch("steady")
+    os.write(2, b"steady batch ends\n")
     after = r.mem_stats()
     assert after["mallocs"] == before["mallocs"], (before, after)
     assert after["peak_live"] > after["live"] >= 0
