@@ -279,6 +279,25 @@ SPLIT = int(os.environ.get("EC_SPLIT", "1"))
 # loads cannot be scheduled around; not adopted. Never-taken branches every 100/300
 # statements (basic-block boundaries) made it worse: k13 630-666 SGPR spills, 1 wave/SIMD.
 PIN = os.environ.get("EC_PIN", "0") == "1"
+# EC_PMV=1 (or a kernel's "pmv" in the tuning file): the poly_mix power of each Fp
+# accumulation (ACC + T*pm[k]) is a uint4 vector load with a uniform address, issued EC_PMD
+# program positions before its use. Vector loads complete in order (vmcnt), so unlike the
+# scalar loads (out of order: any use waits for all of them, and the compiler hoists and
+# spills them to VGPR lanes) they can run ahead a fixed distance; the four words sit in
+# VGPRs and feed the v_mad_u64_u32 directly.
+# Measured (rv32im po2=20, tools/tune_ec_pmv.py, gpurun_out r3f): the lane spills go but
+# every kernel gets 1.1-9x slower at distances 16/32/64 — a broadcast vector load still
+# returns 16 B to each of the 64 lanes through the texture data path, ~360 per wave; not
+# adopted.
+PMV = os.environ.get("EC_PMV", "0") == "1"
+PMD = int(os.environ.get("EC_PMD", "64"))
+# EC_PINB=n (or a kernel's "pinb"): the poly_mix terms (acc_fp, acc_ext) go in batches of n;
+# batch b's table pointer is pinned to the running sum after the first term of batch b-1,
+# so batch b's scalar loads are issued once batch b-1's have landed and overlap the rest of
+# batch b-1. Scalar loads return out of order (any use waits for all in flight), so a load
+# per term pinned a few terms back (EC_PIN) made every term wait on the loads of the next
+# ones; batches wait once per batch, on their own loads only, with ~8n SGPRs live.
+PINB = int(os.environ.get("EC_PINB", "0"))
 # ... pinned to the running sum EC_PIND accumulations back, so the load has that long to land
 PIND = int(os.environ.get("EC_PIND", "4"))
 
@@ -491,10 +510,52 @@ def emit(circuit, outdir, budget, host=False):
         "  for (int i = 0; i < 4; i++) a.c[i] += uint64_t(t) * pm[4 * k + i];",
         "  return a;",
         "}",
+        "// poly_mix power k as a vector load (EC_PMV): z is a zero the compiler cannot see",
+        "// through, so the uniform address still takes a global load into VGPRs",
+        "EC_FN uint4 pm_vec(const uint32_t* pm, uint32_t z, int k) {",
+        "  return *reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(pm + 4 * k) + z);",
+        "}",
+        "EC_FN Acc acc_fpv(Acc a, uint32_t t, uint4 q) {",
+        "  a.c[0] += uint64_t(t) * q.x;",
+        "  a.c[1] += uint64_t(t) * q.y;",
+        "  a.c[2] += uint64_t(t) * q.z;",
+        "  a.c[3] += uint64_t(t) * q.w;",
+        "  return a;",
+        "}",
         "// a += t * pm[k]  (t in FpExt; x^4 = NBETA folded into pmn = NBETA * pm)",
         "EC_FN Acc acc_ext(Acc a, FpExt t, const uint32_t* pm, const uint32_t* pmn, int k) {",
         "  const uint32_t* q = pm + 4 * k;",
         "  const uint32_t* n = pmn + 4 * k;",
+        "  a.c[0] += uint64_t(t.c[0]) * q[0] + uint64_t(t.c[1]) * n[3] + uint64_t(t.c[2]) * n[2] + uint64_t(t.c[3]) * n[1];",
+        "  a.c[1] += uint64_t(t.c[0]) * q[1] + uint64_t(t.c[1]) * q[0] + uint64_t(t.c[2]) * n[3] + uint64_t(t.c[3]) * n[2];",
+        "  a.c[2] += uint64_t(t.c[0]) * q[2] + uint64_t(t.c[1]) * q[1] + uint64_t(t.c[2]) * q[0] + uint64_t(t.c[3]) * n[3];",
+        "  a.c[3] += uint64_t(t.c[0]) * q[3] + uint64_t(t.c[1]) * q[2] + uint64_t(t.c[2]) * q[1] + uint64_t(t.c[3]) * q[0];",
+        "  return a;",
+        "}",
+        "// EC_PINB: the table pointer made to depend on `a` (no instruction), then read back",
+        "// uniform (readfirstlane) in the constant address space, so its reads stay scalar loads",
+        "// (an asm result is otherwise taken as divergent: per-lane flat loads)",
+        "#ifdef R0_EC_HOST",
+        "typedef const uint32_t* cptr;",
+        "EC_FN cptr pinc(const uint32_t* p, const Acc&) { return p; }",
+        "#else",
+        "typedef const __attribute__((address_space(4))) uint32_t* cptr;",
+        "EC_FN cptr pinc(const uint32_t* p, const Acc& a) {",
+        "  const uint64_t v = reinterpret_cast<uint64_t>(p);",
+        "  uint32_t lo = uint32_t(v), hi = uint32_t(v >> 32);",
+        "  const uint32_t d = uint32_t(a.c[0]);",
+        "  asm(\"\" : \"+s\"(lo), \"+s\"(hi) : \"v\"(d));",
+        "  lo = __builtin_amdgcn_readfirstlane(lo);",
+        "  hi = __builtin_amdgcn_readfirstlane(hi);",
+        "  return reinterpret_cast<cptr>((uint64_t(hi) << 32) | lo);",
+        "}",
+        "#endif",
+        "EC_FN Acc acc_fpc(Acc a, uint32_t t, cptr pm, int k) {",
+        "#pragma unroll",
+        "  for (int i = 0; i < 4; i++) a.c[i] += uint64_t(t) * pm[4 * k + i];",
+        "  return a;",
+        "}",
+        "EC_FN Acc acc_extc(Acc a, FpExt t, cptr q, cptr n) {",
         "  a.c[0] += uint64_t(t.c[0]) * q[0] + uint64_t(t.c[1]) * n[3] + uint64_t(t.c[2]) * n[2] + uint64_t(t.c[3]) * n[1];",
         "  a.c[1] += uint64_t(t.c[0]) * q[1] + uint64_t(t.c[1]) * q[0] + uint64_t(t.c[2]) * n[3] + uint64_t(t.c[3]) * n[2];",
         "  a.c[2] += uint64_t(t.c[0]) * q[2] + uint64_t(t.c[1]) * q[1] + uint64_t(t.c[2]) * q[0] + uint64_t(t.c[3]) * n[3];",
@@ -546,6 +607,7 @@ def emit(circuit, outdir, budget, host=False):
         red_memo = {}
         offs = set()
         acc_hist = []  # Acc variables in emission order (anchors of pin())
+        pm_idx = []    # acc_hist index of each poly_mix term's result (EC_PINB anchors)
         tmp = {"n": 0}
         L = []
         w = L.append
@@ -695,8 +757,14 @@ def emit(circuit, outdir, budget, host=False):
                 assert bd + add <= U64
             return expr, bd
 
-        def add_prod(expr, bd, t, k):
-            """Acc expression for expr + t * pm[k]; t an operand."""
+        def add_prod(expr, bd, t, k, q=None):
+            """Acc expression for expr + t * pm[k]; t an operand; q: pm[k] already loaded
+            into a uint4 (EC_PMV)."""
+            j = len(pm_idx)
+            pm_idx.append(len(acc_hist))  # the caller appends this term's Acc next
+            pinned = None
+            if kpinb and j >= kpinb:
+                pinned = acc_hist[pm_idx[(j // kpinb - 1) * kpinb]]
             if t[2] == "e":
                 while 4 * t[1] * PM + fold_max(U64) > U64:
                     t = reduce1(t)
@@ -705,11 +773,19 @@ def emit(circuit, outdir, budget, host=False):
                 if PIN and len(acc_hist) >= PIND:
                     a_ = acc_hist[-PIND]
                     return f"acc_ext({expr}, {t[0]}, pin(A.pm, {a_}), pin(A.pmn, {a_}), {k})", bd + add
+                if pinned:
+                    kk = f"4 * ({k})"
+                    return (f"acc_extc({expr}, {t[0]}, pinc(A.pm, {pinned}) + {kk}, pinc(A.pmn, {pinned}) + {kk})",
+                            bd + add)
                 return f"acc_ext({expr}, {t[0]}, A.pm, A.pmn, {k})", bd + add
             add = t[1] * PM
             expr, bd = room(expr, bd, add)
+            if q is not None:
+                return f"acc_fpv({expr}, {t[0]}, {q})", bd + add
             if PIN and len(acc_hist) >= PIND:
                 return f"acc_fp({expr}, {t[0]}, pin(A.pm, {acc_hist[-PIND]}), {k})", bd + add
+            if pinned:
+                return f"acc_fpc({expr}, {t[0]}, pinc(A.pm, {pinned}), {k})", bd + add
             return f"acc_fp({expr}, {t[0]}, A.pm, {k})", bd + add
 
         def acc_to_ext(expr, bd, name):
@@ -733,6 +809,9 @@ def emit(circuit, outdir, budget, host=False):
         acc_state = {"n": 0, "b": 0}
         kwaves = int(os.environ.get("EC_WAVES_OVERRIDE", tune.get(ki, {}).get("waves", WAVES)))
         kpf = tune.get(ki, {}).get("pf", PF)
+        kpmv = PMV or bool(tune.get(ki, {}).get("pmv", 0))
+        kpmd = int(os.environ.get("EC_PMD", tune.get(ki, {}).get("pmd", PMD)))
+        kpinb = int(os.environ.get("EC_PINB", tune.get(ki, {}).get("pinb", PINB)))
         if ORDER == "dfs":
             byid_ = pg.byid
             leaves = set(v for v in need if v in loaded or byid_[v][0] in "clge")
@@ -750,15 +829,26 @@ def emit(circuit, outdir, budget, host=False):
                     continue
                 slots.setdefault(max(0, first_use.get(v, 0) - kpf), []).append(v)
             seq = sorted(consts, key=lambda v: pg.order[v])
-            for n_, v in enumerate(body):
-                seq += sorted(slots.get(n_, []), key=lambda v: pg.order[v])
-                seq.append(v)
+            pmslots = {}
+            if kpmv:
+                for n_, v in enumerate(body):
+                    ins_ = byid_[v]
+                    if ins_[0] == "a" and types[ins_[3]] == "f":
+                        pmslots.setdefault(max(0, n_ - kpmd), []).append(("pmv", f"q{v}", ins_[4], v))
+                    elif ins_[0] == "b" and types[ins_[3]] == "f" and types[ins_[4]] == "f":
+                        pmslots.setdefault(max(0, n_ - kpmd), []).append(("pmv", f"q{v}", ins_[5], v))
             kprog = [byid_[v] for v in seq]
+            for n_, v in enumerate(body):
+                kprog += [byid_[x] for x in sorted(slots.get(n_, []), key=lambda v: pg.order[v])]
+                kprog += pmslots.get(n_, [])
+                kprog.append(byid_[v])
         else:
             kprog = [ins_ for ins_ in prog if ins_[0] != "r"]
         order_pos = {}
         for n_, ins_ in enumerate(kprog):
-            order_pos[ins_[1]] = n_
+            if ins_[0] != "pmv":
+                order_pos[ins_[1]] = n_
+        qv = {}
         term_at = {}
         for ti, (e, f) in enumerate(mine):
             rts = [x for x in term_roots((e, f)) if pg.byid[x][0] not in "ceg"]
@@ -806,8 +896,19 @@ def emit(circuit, outdir, budget, host=False):
 
         if mine or last:
             w("  const Acc s0 = Acc{{0, 0, 0, 0}};")
+        if kpmv:
+            w("  uint32_t pmz;")
+            w("#ifdef R0_EC_HOST")
+            w("  pmz = 0;")
+            w("#else")
+            w('  asm volatile("v_mov_b32 %0, 0" : "=v"(pmz));')
+            w("#endif")
         for ins in kprog:
             op, i = ins[0], ins[1]
+            if op == "pmv":
+                w(f"  const uint4 {i} = pm_vec(A.pm, pmz, {ins[2]});")
+                qv[ins[3]] = i
+                continue
             if i not in need or op == "r":
                 continue
             if i in loaded:
@@ -855,7 +956,7 @@ def emit(circuit, outdir, budget, host=False):
                 idx = pos % SPLIT
                 if idx >= len(ps):
                     ps.append(("Acc{{0, 0, 0, 0}}", 0))
-                expr, bd = add_prod(ps[idx][0], ps[idx][1], t, k)
+                expr, bd = add_prod(ps[idx][0], ps[idx][1], t, k, qv.get(i) if t[2] == "f" else None)
                 w(f"  const Acc a{i} = {expr};")
                 acc_hist.append(f"a{i}")
                 ps[idx] = (f"a{i}", bd)
