@@ -307,14 +307,23 @@ def kernel_config(circuit, budget):
     committed as risc0_amd/circuits/<circuit>.ectune.json; EC_WAVES/EC_PF (if set) or
     the defaults apply to kernels it does not list (or when EC_NOTUNE is set)."""
     path = os.path.join(ROOT, "risc0_amd", "circuits", circuit + ".ectune.json")
-    if os.environ.get("EC_NOTUNE") or "EC_WAVES" in os.environ or "EC_PF" in os.environ or not os.path.exists(path):
+    keep = os.environ.get("EC_KEEPTUNE") == "1"  # EC_WAVES/EC_PF override only those two fields
+    if (os.environ.get("EC_NOTUNE") or (not keep and ("EC_WAVES" in os.environ or "EC_PF" in os.environ))
+            or not os.path.exists(path)):
         return {}
     import json
     with open(path) as f:
         t = json.load(f)
     if t.get("budget") != budget or t.get("order") != ORDER:
         return {}
-    return {int(k): v for k, v in t["kernels"].items()}
+    ks = {int(k): dict(v) for k, v in t["kernels"].items()}
+    if keep:
+        for v in ks.values():
+            if "EC_WAVES" in os.environ:
+                v["waves"] = int(os.environ["EC_WAVES"])
+            if "EC_PF" in os.environ:
+                v["pf"] = int(os.environ["EC_PF"])
+    return ks
 
 
 # ---- value-range analysis --------------------------------------------------------

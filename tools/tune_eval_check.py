@@ -24,7 +24,7 @@ CSRC = os.path.join(ROOT, "risc0_amd", "csrc")
 VAR = os.path.join(ROOT, "risc0_amd", "lib_variants")
 OUT = os.path.join(ROOT, "gpurun_out", "tune")
 CIRCUIT = "rv32im"
-GRID = [(w, pf) for w in (1, 2) for pf in (128, 256, 384, 512, 640, 768, 1024)]
+GRID = [(w, pf) for w in (1, 2) for pf in (128, 256, 512, 768, 1024)]
 BUDGET = 4000
 
 
@@ -34,7 +34,8 @@ def build(circuit):
         os.remove(f)
     for w, pf in GRID:
         shutil.rmtree(os.path.join(CSRC, "gen", circuit), ignore_errors=True)
-        env = dict(os.environ, EC_WAVES=str(w), EC_PF=str(pf))
+        # the committed per-kernel choices other than these two (canon, pinb) stay
+        env = dict(os.environ, EC_WAVES=str(w), EC_PF=str(pf), EC_KEEPTUNE="1")
         subprocess.run(["make", "-j8", f"EC_BUDGET_{circuit}={BUDGET}"], cwd=CSRC, env=env, check=True,
                        stdout=subprocess.DEVNULL)
         shutil.copy(os.path.join(ROOT, "risc0_amd", "lib", "libr0hip.so"),
@@ -71,8 +72,11 @@ def pick(circuit):
     tot = sum(v[0] for v in best.values())
     path = os.path.join(ROOT, "risc0_amd", "circuits", circuit + ".ectune.json")
     prev = json.load(open(path)) if os.path.exists(path) else {}
+    kern = {str(k): dict(prev.get("kernels", {}).get(str(k), {})) for k in best}
+    for k, v in best.items():  # other per-kernel fields (canon, pinb) were fixed in the variants
+        kern[str(k)].update(waves=v[1], pf=v[2], us=round(v[0], 1))
     out = {"budget": BUDGET, "order": "dfs", "measured_total_us": round(tot, 1),
-           "kernels": {str(k): {"waves": v[1], "pf": v[2], "us": round(v[0], 1)} for k, v in sorted(best.items())}}
+           "kernels": {k: kern[k] for k in sorted(kern, key=int)}}
     if prev.get("mat"):
         out["mat"] = prev["mat"]  # the partition these kernels belong to
     with open(path, "w") as f:
