@@ -321,13 +321,17 @@ void* dev_alloc(size_t bytes) {
   if (bytes == 0) bytes = 16;
   bytes = (bytes + 255) & ~size_t(255);
   {
-    auto it = t_ctx.pool.find(bytes);
-    if (it != t_ctx.pool.end()) {
+    // best fit, exact or up to 25% larger, as for the orphans below: a block taken from the
+    // orphans at its own (larger) size comes back here under that size, and an exact-size
+    // lookup would then miss it and allocate again in a steady state
+    auto it = t_ctx.pool.lower_bound(bytes);
+    if (it != t_ctx.pool.end() && it->first <= bytes + bytes / 4) {
       void* p = it->second;
+      const size_t have = it->first;
       t_ctx.pool.erase(it);
-      live_add(bytes);
+      live_add(have);
       std::lock_guard<std::mutex> lk(g_mu);
-      g_live[p] = bytes;
+      g_live[p] = have;
       return p;
     }
     std::lock_guard<std::mutex> lk(g_mu);
