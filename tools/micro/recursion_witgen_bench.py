@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""Recursion witness generation (r0hip_recursion_witgen) against the reference's compiled
-CPU witgen (risc0_circuit_recursion_cpu_witgen in oracle/_ref/libref_recursion.so, parallel
+"""Recursion witness generation (r0hip_recursion_witgen) and accumulation
+(r0hip_recursion_accum) against the reference's compiled CPU witgen and accumulation (risc0_circuit_recursion_cpu_witgen in oracle/_ref/libref_recursion.so, parallel
 mode, every host core) on the same program: a random recursion program filling a segment
 of 2^po2 rows (tests/recursion_program.py, restated preflight).
 
@@ -63,8 +63,35 @@ def main():
         t = r.kernel_times()
         r.set_kernel_timing(False)
         phases.append({k: round(v[0], 3) for k, v in t.items()})
+    # the accumulation (r0hip_recursion_accum) on the same program's witness as the prover
+    # hands it over (ZK noise rows, INVALID zeroized), against the compiled
+    # risc0_circuit_recursion_cpu_accum with the same mix
+    import accum_ir as A
+    w_ctrl, w_data, w_glob = RP.witgen(prog, pf, po2, noise_seed=5)
+    acc0 = RP.accum_init(po2, noise_seed=6)
+    mix = np.random.default_rng(7).integers(0, RP.P, RP.MIX, dtype=np.uint64).astype(np.uint32)
+    want = acc0.copy()
+    t0 = time.perf_counter()
+    A.ref_accum(w_ctrl, w_glob, w_data, mix, want, len(prog.rows), n)
+    acc_cpu_s = time.perf_counter() - t0
+    dc, dgl, dda, dmx = (hal.copy_from_elem(nm, x) for nm, x in
+                         (("c", w_ctrl), ("g", w_glob), ("d", w_data), ("m", mix)))
+    dacc = hal.copy_from_elem("acc", acc0)
+    hal.recursion_accum(dc, dgl, dda, dmx, dacc, len(prog.rows), n)  # warm
+    acc_equal = bool(np.array_equal(dacc.to_numpy(), want))
+    acc_ms = []
+    for _ in range(reps):
+        dacc.copy_from(acc0)
+        hal.synchronize()
+        r.set_kernel_timing(True)
+        hal.recursion_accum(dc, dgl, dda, dmx, dacc, len(prog.rows), n)
+        t = r.kernel_times()
+        r.set_kernel_timing(False)
+        acc_ms.append(sum(v[0] for v in t.values()))
     print(json.dumps({
         "po2": po2, "cycles": len(prog.rows), "equal_to_reference": equal,
+        "accumulation": {"gpu_ms": round(float(np.median(acc_ms)), 3), "reference_cpu_ms": round(acc_cpu_s * 1e3, 1),
+                         "equal_to_reference": acc_equal},
         "gpu_ms_by_phase": phases[-1],
         "gpu_ms_wall_with_upload": round(float(np.median(plain)), 3),
         "gpu_ms_wall_with_upload_and_kernel_timing": round(float(np.median(walls)), 3),
