@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """rv32im accumulation (r0hip_rv32im_accum) at po2=20 on random rows over all instruction
-arms: HIP-event times of the generated per-cycle step and of the scan/finalize."""
+arms: HIP-event times of the generated per-cycle step and of the scan/finalize; with
+--reference also the compiled reference accumulation's time on the same rows and equality."""
 import json
 import os
 import sys
@@ -23,8 +24,10 @@ def main():
     rng = np.random.default_rng(3)
     data = rows_for_arms(rng, rows, list(rng.integers(0, 13, rows)))
     d_data = hal.copy_from_elem("data", data)
-    d_glob = hal.copy_from_elem("g", rng.integers(0, P, 90, dtype=np.uint64).astype(np.uint32))
-    d_mix = hal.copy_from_elem("m", rng.integers(0, P, 36, dtype=np.uint64).astype(np.uint32))
+    glob = rng.integers(0, P, 90, dtype=np.uint64).astype(np.uint32)
+    mix = rng.integers(0, P, 36, dtype=np.uint64).astype(np.uint32)
+    d_glob = hal.copy_from_elem("g", glob)
+    d_mix = hal.copy_from_elem("m", mix)
     inval = np.full(103 * rows, 0xFFFFFFFF, np.uint32)
     acc = hal.copy_from_elem("acc", inval)
     hal.rv32im_accum(d_data, acc, d_glob, d_mix, rows, rows)  # warm
@@ -37,7 +40,18 @@ def main():
         t = r.kernel_times()
         r.set_kernel_timing(False)
         out[rep] = {k: round(v[0], 3) for k, v in t.items()}
-    print(json.dumps({"po2": po2, "ms": out}))
+    res = {"po2": po2, "ms": out}
+    if "--reference" in sys.argv:
+        # the reference's compiled risc0_circuit_rv32im_cpu_accum (all three phases) on the
+        # same rows, on every host thread its pool starts; and word-for-word equality
+        import time
+        import rv32im_accum_ref as R
+        t0 = time.perf_counter()
+        want = R.accum(data, glob, mix, rows, rows)
+        res["reference_cpu_ms"] = round((time.perf_counter() - t0) * 1e3, 1)
+        res["reference_cpu_threads"] = os.cpu_count()
+        res["equal_to_reference"] = bool(np.array_equal(acc.to_numpy(), want))
+    print(json.dumps(res))
 
 
 if __name__ == "__main__":
