@@ -105,6 +105,12 @@ def arm_chunks(prog, limit):
     different kernels never store the same column unless their guards are exclusive
     (checked: each guard is a conjunction of selector literals, and two such conjunctions
     are exclusive when one selector appears with both polarities).
+    The units that store the BigInt state columns (accum 0..11) also read them at back 1;
+    another cycle's lane may write that row in the same kernel, before or after the read,
+    in either order (the unsorted kernels had the same race across waves). Both orders give
+    the same words because the step writes exactly the state the host injected there
+    (tests/test_bigint_accum.py checks the reference's own step rewrites every injected
+    state unchanged).
     Returns None when the program is not of that shape (a guarded block that defines
     values, or nested blocks)."""
     defs = {}
