@@ -57,17 +57,23 @@ constexpr uint32_t lds_words() {
   return COLS ? (1u << (B + C)) : ((1u << B) + (1u << B >> 3)) << C;
 }
 
-// One group of NST (1..3) radix-2 stages [s0, s0+NST) in registers: a lane owns blocks
-// of 2^NST elements t_base + m*h (h = 2^(s0-1)), so a group costs one LDS read and
-// write per element instead of NST. Twiddles come from the LDS copy of the table.
-template <bool INV, bool COLS, int B, int C, int NST, int FROM_EB = 0, int NT = kThreads>
-__device__ __forceinline__ void stage_group(uint32_t* lds, const uint32_t* tw, uint32_t s0,
-                                            const uint32_t* csrc = nullptr) {
+// One group of NST (1..3) radix-2 stages [S0, S0+NST) in registers: a lane owns blocks
+// of 2^NST elements t_base + m*h (h = 2^(S0-1)), so a group costs one LDS read and
+// write per element instead of NST. Twiddles come from the LDS copy of the table. S0 is a
+// template parameter, so h and every shift below are constants.
+template <bool INV, bool COLS, int B, int C, int NST, int FROM_EB, int NT, int S0>
+__device__ __forceinline__ void stage_group(uint32_t* lds, const uint32_t* tw, const uint32_t* csrc) {
   if constexpr (NST > B) return;  // never reached; keeps the shifts below well-formed
   constexpr uint32_t M = 1u << NST;
-  const uint32_t h = 1u << (s0 - 1);
+  constexpr uint32_t h = 1u << (S0 - 1);
   constexpr uint32_t nrb = 1u << (B >= NST ? B - NST : 0);  // blocks per column/row
   constexpr uint32_t nblk = nrb << C;
+  // Row layout t + (t >> 3): the elements t_base + m*h sit at constant offsets from
+  // t_base's word when h is a multiple of 8 (m*h*9/8) or the whole block lies in one
+  // 8-word run (h*M <= 8: t_base is aligned to h*M up to k < h, so t_base mod 8 +
+  // (M-1)*h < 8); column layout (t << C) + j always.
+  constexpr bool LIN = COLS || h % 8 == 0 || h * M <= 8;
+  constexpr uint32_t step = COLS ? (h << C) : (h % 8 == 0 ? h + h / 8 : h);
 #pragma unroll
   for (uint32_t it = 0; it < (nblk + NT - 1) / NT; it++) {
     const uint32_t blk = it * NT + threadIdx.x;
@@ -81,12 +87,13 @@ __device__ __forceinline__ void stage_group(uint32_t* lds, const uint32_t* tw, u
       r = blk & (nrb - 1);
     }
     const uint32_t k = r & (h - 1);
-    const uint32_t tb = ((r >> (s0 - 1)) << (s0 - 1 + NST)) | k;
+    const uint32_t tb = ((r >> (S0 - 1)) << (S0 - 1 + NST)) | k;
+    const uint32_t base = lidx<COLS, B, C>(j, tb);
     uint32_t v[M];
 #pragma unroll
     for (uint32_t m = 0; m < M; m++) {
       if (FROM_EB) v[m] = csrc[(j << (B - FROM_EB)) + ((tb + m * h) >> FROM_EB)];  // replicated input
-      else v[m] = lds[lidx<COLS, B, C>(j, tb + m * h)];
+      else v[m] = lds[LIN ? base + m * step : lidx<COLS, B, C>(j, tb + m * h)];
     }
     if (!INV) {
 #pragma unroll
@@ -116,49 +123,40 @@ __device__ __forceinline__ void stage_group(uint32_t* lds, const uint32_t* tw, u
       }
     }
 #pragma unroll
-    for (uint32_t m = 0; m < M; m++) lds[lidx<COLS, B, C>(j, tb + m * h)] = v[m];
+    for (uint32_t m = 0; m < M; m++) lds[LIN ? base + m * step : lidx<COLS, B, C>(j, tb + m * h)] = v[m];
   }
   __syncthreads();
 }
 
-// stages [first, B] ascending (DIT) or [1, B] descending (DIF), radix-8 groups first
+// DIT stages [S, B] ascending, radix-8 groups first; the first group of an expanding pass
+// (S == EB + 1) reads the compact (unreplicated) input. Compile-time recursion, so each
+// group's first stage is a constant.
+template <bool COLS, int B, int C, int EB, int NT, int S>
+__device__ __forceinline__ void fwd_stages(uint32_t* lds, const uint32_t* tw, const uint32_t* csrc) {
+  if constexpr (S <= B) {
+    constexpr int n = B - S + 1;
+    constexpr int NST = n >= 3 ? 3 : n;
+    constexpr int FROM = (S == EB + 1 && EB > 0) ? EB : 0;
+    stage_group<false, COLS, B, C, NST, FROM, NT, S>(lds, tw, csrc);
+    fwd_stages<COLS, B, C, EB, NT, S + NST>(lds, tw, csrc);
+  }
+}
+
+// DIF stages [1, S] descending, radix-8 groups first
+template <bool COLS, int B, int C, int NT, int S>
+__device__ __forceinline__ void inv_stages(uint32_t* lds, const uint32_t* tw) {
+  if constexpr (S >= 1) {
+    constexpr int NST = S >= 3 ? 3 : S;
+    stage_group<true, COLS, B, C, NST, 0, NT, S - NST + 1>(lds, tw, nullptr);
+    inv_stages<COLS, B, C, NT, S - NST>(lds, tw);
+  }
+}
+
+// stages [EB+1, B] ascending (DIT) or [1, B] descending (DIF)
 template <bool INV, bool COLS, int B, int C, int EB = 0, int NT = kThreads>
 __device__ __forceinline__ void stages(uint32_t* lds, const uint32_t* tw, const uint32_t* csrc = nullptr) {
-  if (!INV) {
-    // DIT stages EB+1 .. B; the first group reads the compact (unreplicated) input
-#pragma unroll
-    for (uint32_t s = EB + 1; s <= uint32_t(B);) {
-      const uint32_t n = uint32_t(B) - s + 1;
-      const bool first = s == EB + 1 && EB > 0;
-      if (n >= 3) {
-        if (first) stage_group<INV, COLS, B, C, 3, EB, NT>(lds, tw, s, csrc);
-        else stage_group<INV, COLS, B, C, 3, 0, NT>(lds, tw, s);
-        s += 3;
-      } else if (n == 2) {
-        if (first) stage_group<INV, COLS, B, C, 2, EB, NT>(lds, tw, s, csrc);
-        else stage_group<INV, COLS, B, C, 2, 0, NT>(lds, tw, s);
-        s += 2;
-      } else {
-        if (first) stage_group<INV, COLS, B, C, 1, EB, NT>(lds, tw, s, csrc);
-        else stage_group<INV, COLS, B, C, 1, 0, NT>(lds, tw, s);
-        s += 1;
-      }
-    }
-  } else {
-#pragma unroll
-    for (int s = B; s >= 1;) {
-      if (s >= 3) {
-        stage_group<INV, COLS, B, C, 3, 0, NT>(lds, tw, uint32_t(s - 2));
-        s -= 3;
-      } else if (s == 2) {
-        stage_group<INV, COLS, B, C, 2, 0, NT>(lds, tw, uint32_t(s - 1));
-        s -= 2;
-      } else {
-        stage_group<INV, COLS, B, C, 1, 0, NT>(lds, tw, uint32_t(s));
-        s -= 1;
-      }
-    }
-  }
+  if constexpr (!INV) fwd_stages<COLS, B, C, EB, NT, EB + 1>(lds, tw, csrc);
+  else inv_stages<COLS, B, C, NT, B>(lds, tw);
 }
 
 
