@@ -458,8 +458,9 @@ void launch_pass_be(hipStream_t s, const PassArgs& p) {
   uint64_t nwg = COLS ? (p.groups >> C) : ((p.groups + (uint64_t(1) << C) - 1) >> C);
   R0_REQUIRE(nwg < (1ull << 31), "ntt grid too large");
   // 13-bit row passes hold ~74 KB of LDS (data + stage twiddles), so only two workgroups
-  // fit a CU: 512 lanes per workgroup double the waves that hide their loads
-  constexpr int NT = (!COLS && B >= 13) ? (INV ? 1024 : 512) : kThreads;
+  // fit a CU: 1024 lanes per workgroup (forward and inverse) multiply the waves that hide
+  // their loads (forward 512 -> 1024 lanes: 2219 -> 2148 us per pass, profiles/r3m_ntt_*)
+  constexpr int NT = (!COLS && B >= 13) ? 1024 : kThreads;
   hipLaunchKernelGGL((ntt_pass_kernel<INV, EXPAND, LAST, COLS, B, C, EB, NT>), dim3(unsigned(nwg)), dim3(NT), lds,
                      s, p);
   HIP_OK(hipGetLastError());
