@@ -166,3 +166,35 @@ def test_arm_sorted_kernels_store_each_column_write_once_under_its_guard():
             if m:
                 got.append((int(m.group(1)), int(m.group(2)), int(m.group(3)), tuple(stack)))
     assert sorted(got) == sorted(want)
+
+
+def test_arm_chunks_merges_non_exclusive_writers_and_readers():
+    """arm_chunks keeps in one kernel, in program order, the units that store one column
+    under guards that are not provably exclusive, and the units whose cones read a column
+    another unit stores; units under exclusive selector literals may split."""
+    # v1, v2: two selector loads; g_a = [v1 == 0], g_b = [v1 != 0] (exclusive), g_c = [v2 == 0]
+    prog = [
+        ("l", 1, 0, 1, 0), ("l", 2, 0, 2, 0), ("l", 3, 0, 3, 0),
+        ("z", 10, 1), ("z", 11, 10), ("z", 12, 2),
+        ("*", 20, 3, 3), ("*", 21, 20, 3),
+        ("if", 10), ("w", 1, 5, 20), ("end",),
+        ("if", 11), ("w", 1, 5, 21), ("end",),   # same column, exclusive with the first
+        ("if", 12), ("w", 1, 6, 20), ("end",),
+        ("if", 12), ("w", 1, 5, 3), ("end",),    # column 5 again, not exclusive with g_a/g_b
+        ("l", 30, 1, 6, 1), ("*", 31, 30, 3),
+        ("if", 10), ("w", 1, 7, 31), ("end",),   # reads column 6, which the third unit stores
+    ]
+    out = G.arm_chunks(prog, 10**9)
+    assert out is not None
+    kern = lambda guard_col: next(k for k, (_, nodes) in enumerate(out)
+                                  for n in nodes if n[0] == "if" and (n[1], n[2][0][1][2]) == guard_col)
+    assert kern((10, 5)) == kern((12, 5)) == kern((11, 5))  # column 5: non-exclusive pairs merge
+    assert kern((12, 6)) == kern((10, 7))                    # column 6: stored by one, read by another
+    # one unit per kernel at a tiny cost cap: the merged groups still cannot split
+    tiny = G.arm_chunks(prog, 1)
+    ks = {}
+    for k, (_, nodes) in enumerate(tiny):
+        for n in nodes:
+            ks.setdefault(k, []).append((n[1], n[2][0][1][2]))
+    together = [k for k, us in ks.items() if (10, 5) in us]
+    assert together and {(12, 5), (11, 5)} <= set(ks[together[0]])
