@@ -150,18 +150,31 @@ __global__ __launch_bounds__(kThreads) void mix_kernel(uint32_t* out, const uint
 // 64-entry table in LDS (4 v_mad_u64_u32 per coefficient, folded every 4), scales by
 // x^(4 l), and the wave adds its lanes with xor shuffles. A last kernel combines the
 // 4096-coefficient pieces by Horner in x^4096.
+// Bit-reversed rows (the inverse NTT's order, L >= 12 bits): stored position
+// j = piece*4096 + 256 q + 4 l + r holds coefficient rev_L(j) = rev_2(r) 2^(L-2) +
+// rev_6(l) 2^(L-8) + rev_4(q) 2^(L-12) + rev_(L-12)(piece), so the same kernel runs with
+// the table x^(rev_2(r) 2^(L-2) + rev_4(q) 2^(L-12)), the lane scale x^(rev_6(l) 2^(L-8)),
+// and the pieces are summed with weights x^rev_(L-12)(piece) instead of by Horner.
 constexpr int kEvLane = 64;                     // coefficients per lane
 constexpr int kEvWave = 64 * kEvLane;           // 4096 per wave
 constexpr int kEvChunk = kThreads * kEvLane;    // 16384 per workgroup
 constexpr int kEvTab = kEvLane + 64 + 1;        // x^(256 q + r), x^(4 l) l < 64, x^4096
 
 __global__ __launch_bounds__(kThreads) void eval_tables_kernel(const uint32_t* __restrict__ xs, uint32_t evals,
-                                                             uint32_t* tab) {
+                                                             uint32_t* tab, uint32_t L, bool bitrev) {
   const uint64_t id = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (id >= uint64_t(evals) * kEvTab) return;
   const uint32_t k = uint32_t(id / kEvTab), e = uint32_t(id % kEvTab);
   const FpExt x = ld_fe(xs + 4 * k);
-  const uint64_t pw = e < kEvLane ? 256 * (e >> 2) + (e & 3) : (e < kEvLane + 64 ? 4 * (e - kEvLane) : kEvWave);
+  uint64_t pw;
+  if (!bitrev)
+    pw = e < kEvLane ? 256 * (e >> 2) + (e & 3) : (e < kEvLane + 64 ? 4 * (e - kEvLane) : kEvWave);
+  else if (e < kEvLane)
+    pw = (uint64_t(bitrev_n(e & 3, 2)) << (L - 2)) + (uint64_t(bitrev_n(e >> 2, 4)) << (L - 12));
+  else if (e < kEvLane + 64)
+    pw = uint64_t(bitrev_n(e - kEvLane, 6)) << (L - 8);
+  else
+    pw = 0;  // no Horner step
   st_fe(tab + (uint64_t(k) * kEvTab + e) * 4, fe_pow(x, pw));
 }
 
@@ -235,16 +248,28 @@ __global__ __launch_bounds__(kThreads) void eval_chunk_kernel(const uint32_t* __
 }
 
 // one wave per evaluation: lane l runs Horner over pieces l, l + 64, ... in y^64 (y = x^4096),
-// then the wave adds S_l * y^l
+// then the wave adds S_l * y^l. Bit-reversed rows: lane l adds piece c times x^rev_P(c)
+// (P = L - 12) for c = l, l + 64, ...
 __global__ __launch_bounds__(kThreads) void eval_any_reduce(const uint32_t* partial, uint32_t npieces,
-                                                          const uint32_t* tab, uint32_t* out, uint32_t evals) {
+                                                          const uint32_t* tab, uint32_t* out, uint32_t evals,
+                                                          const uint32_t* xs, uint32_t L, bool bitrev) {
   const uint32_t k = blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (k >= evals) return;  // whole waves leave together
+  const uint32_t* pk = partial + uint64_t(k) * npieces * 4;
+  if (bitrev) {
+    const FpExt x = ld_fe(xs + 4 * k);
+    FpExt s = fe_zero();
+    for (uint32_t c = lane; c < npieces; c += 64)
+      s = fe_add(s, fe_mul(ld_fe(pk + uint64_t(c) * 4), fe_pow(x, bitrev_n(c, L - 12))));
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) s = fe_add(s, shfl_xor4(s, m));
+    if (lane == 0) st_fe(out + uint64_t(k) * 4, s);
+    return;
+  }
   const FpExt y = ld_fe(tab + (uint64_t(k) * kEvTab + kEvTab - 1) * 4);  // x^4096
   FpExt y64 = y;
 #pragma unroll
   for (int i = 0; i < 6; i++) y64 = fe_mul(y64, y64);
-  const uint32_t* pk = partial + uint64_t(k) * npieces * 4;
   FpExt s = fe_zero();
   if (lane < npieces) {
     uint32_t c = lane + ((npieces - 1 - lane) / 64) * 64;  // the lane's last piece
@@ -533,9 +558,10 @@ void mix_poly_coeffs(hipStream_t s, uint32_t* out, const uint32_t* in, const uin
 }
 
 void batch_evaluate_any_host(hipStream_t s, const uint32_t* coeffs, size_t poly_count, uint32_t log_n,
-                             const std::vector<uint32_t>& which, const uint32_t* xs, uint32_t* out) {
+                             const std::vector<uint32_t>& which, const uint32_t* xs, uint32_t* out, bool bitrev) {
   const size_t eval_count = which.size();
   if (!eval_count) return;
+  R0_REQUIRE(!bitrev || log_n >= kEvalBitrevMinLog, "batch_evaluate_any: bit-reversed rows need log_n >= 12");
   const uint64_t n = uint64_t(1) << log_n;
   const uint32_t nchunks = uint32_t((n + kEvChunk - 1) / kEvChunk);
   const uint32_t npieces = nchunks * (kThreads / 64);  // 4096-coefficient pieces, one per wave
@@ -563,13 +589,13 @@ void batch_evaluate_any_host(hipStream_t s, const uint32_t* coeffs, size_t poly_
   uint32_t* tab = static_cast<uint32_t*>(scratch(eval_count * kEvTab * 16, kSlotEvalTable));
   uint32_t* partial = static_cast<uint32_t*>(scratch(eval_count * npieces * 16, kSlotEvalPartial));
   hipLaunchKernelGGL(eval_tables_kernel, dim3(div_up(eval_count * kEvTab, kThreads)), dim3(kThreads), 0, s, xs,
-                     uint32_t(eval_count), tab);
+                     uint32_t(eval_count), tab, log_n, bitrev);
   HIP_OK(hipGetLastError());
   hipLaunchKernelGGL(eval_chunk_kernel, dim3(nchunks, unsigned(groups.size())), dim3(kThreads), 0, s, coeffs, n,
                      d_gpoly, d_gbegin, d_geval, tab, partial, npieces);
   HIP_OK(hipGetLastError());
   hipLaunchKernelGGL(eval_any_reduce, dim3(div_up(eval_count, kThreads / 64)), dim3(kThreads), 0, s, partial, npieces,
-                     tab, out, uint32_t(eval_count));
+                     tab, out, uint32_t(eval_count), xs, log_n, bitrev);
   HIP_OK(hipGetLastError());
 }
 

@@ -339,9 +339,11 @@ __global__ __launch_bounds__(NT) void ntt_pass_kernel(PassArgs p) {
 // Rows of 2^L: i = (hi:k | mid:m | lo:k) -> rev(i) = (rev_k(lo) | rev_m(mid) | rev_k(hi)).
 // A workgroup swaps the 2^k x 2^k tiles of mid and rev_m(mid) through LDS, so
 // both the reads (lo contiguous) and the writes (rev_k(hi) contiguous) coalesce.
-__global__ __launch_bounds__(kThreads) void bit_reverse_tiles(uint32_t* io, uint32_t L, uint32_t k) {
-  __shared__ uint32_t ta[32 * 33];
-  __shared__ uint32_t tb[32 * 33];
+// T = uint32_t for Fp rows, uint4 for rows of FpExt (AoS, 16-byte elements).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void bit_reverse_tiles(T* io, uint32_t L, uint32_t k) {
+  __shared__ T ta[32 * 33];
+  __shared__ T tb[32 * 33];
   const uint32_t m = L - 2 * k;
   const uint32_t nmid = 1u << m;
   const uint32_t mid = blockIdx.x % nmid;
@@ -349,7 +351,7 @@ __global__ __launch_bounds__(kThreads) void bit_reverse_tiles(uint32_t* io, uint
   const uint32_t rmid = bitrev_n(mid, m);
   if (mid > rmid) return;
   const uint32_t K = 1u << k;
-  uint32_t* base = io + (row << L);
+  T* base = io + (row << L);
   for (uint32_t i = threadIdx.x; i < K * K; i += kThreads) {
     uint32_t hi = i >> k, lo = i & (K - 1);
     ta[hi * 33 + lo] = base[(uint64_t(hi) << (m + k)) + (uint64_t(mid) << k) + lo];
@@ -580,14 +582,24 @@ void ntt_interpolate_from(hipStream_t s, uint32_t* io, const uint32_t* src, size
   }
 }
 
-void bit_reverse(hipStream_t s, uint32_t* io, size_t count, uint32_t L) {
-  if (count == 0 || L < 2) return;
-  KScope ks("bit_reverse", double(count) * 8 * (size_t(1) << L));
+template <typename T>
+static void launch_bit_reverse(hipStream_t s, T* io, size_t count, uint32_t L) {
+  KScope ks("bit_reverse", double(count) * 2 * sizeof(T) * (size_t(1) << L));
   uint32_t k = L / 2 < 5 ? L / 2 : 5;
   uint64_t nwg = uint64_t(count) << (L - 2 * k);
   R0_REQUIRE(nwg < (1ull << 31), "bit_reverse grid too large");
-  hipLaunchKernelGGL(bit_reverse_tiles, dim3(unsigned(nwg)), dim3(kThreads), 0, s, io, L, k);
+  hipLaunchKernelGGL(bit_reverse_tiles<T>, dim3(unsigned(nwg)), dim3(kThreads), 0, s, io, L, k);
   HIP_OK(hipGetLastError());
+}
+
+void bit_reverse(hipStream_t s, uint32_t* io, size_t count, uint32_t L) {
+  if (count == 0 || L < 2) return;
+  launch_bit_reverse(s, io, count, L);
+}
+
+void bit_reverse_ext(hipStream_t s, uint32_t* io, size_t count, uint32_t L) {
+  if (count == 0 || L < 2) return;
+  launch_bit_reverse(s, reinterpret_cast<uint4*>(io), count, L);
 }
 
 void zk_shift(hipStream_t s, uint32_t* io, size_t count, uint32_t L) {

@@ -128,22 +128,31 @@ struct MerkleTree {
   }
 };
 
+// From po2 = 12 the coefficient rows stay in the bit-reversed order the inverse NTT leaves
+// (the order the forward NTT takes): evaluate_any reads them with bit-reversed power tables
+// and mix_poly_coeffs is elementwise, so the only natural-order consumer is combos_divide,
+// which gets the (combo_count + 1) mixed rows reversed instead of every trace column.
+bool coeffs_stay_bitrev(size_t po2) { return po2 >= kEvalBitrevMinLog; }
+
 struct PolyGroup {
   DevBuf coeffs;
   size_t count = 0;
+  bool bitrev = false;  // coeffs rows in bit-reversed order
   DevBuf evaluated;
   MerkleTree tree;
   // poly_group.rs:63-83 (coeffs already interpolated + zk-shifted)
-  PolyGroup(int suite, DevBuf c, size_t cnt, size_t po2) : coeffs(std::move(c)), count(cnt) {
+  PolyGroup(int suite, DevBuf c, size_t cnt, size_t po2)
+      : coeffs(std::move(c)), count(cnt), bitrev(coeffs_stay_bitrev(po2)) {
     size_t size = size_t(1) << po2, domain = size * INV_RATE;
     evaluated = DevBuf(count * domain);
     ntt_evaluate(stream(), evaluated.p, coeffs.p, count, uint32_t(po2 + 2), 2);
-    bit_reverse(stream(), coeffs.p, count, uint32_t(po2));
+    if (!bitrev) bit_reverse(stream(), coeffs.p, count, uint32_t(po2));
     tree.build(suite, evaluated.p, domain, count);
   }
-  // coefficients (natural order), evaluations and leaf digests already made chunk by chunk
+  // coefficients (natural order below po2 12), evaluations and leaf digests already made
+  // chunk by chunk
   PolyGroup(int suite, DevBuf c, DevBuf ev, DevBuf leaf_nodes, size_t cnt, size_t po2)
-      : coeffs(std::move(c)), count(cnt), evaluated(std::move(ev)) {
+      : coeffs(std::move(c)), count(cnt), bitrev(coeffs_stay_bitrev(po2)), evaluated(std::move(ev)) {
     tree.build_from_leaves(suite, std::move(leaf_nodes), evaluated.p, (size_t(1) << po2) * INV_RATE, count);
   }
 };
@@ -297,7 +306,7 @@ struct Prover {
         ntt_interpolate_from(s, coeffs.p + c0 * n, witness + c0 * n, cc, uint32_t(po2), true);
       }
       ntt_evaluate(s, evaluated.p + c0 * domain, coeffs.p + c0 * n, cc, uint32_t(po2 + 2), 2);
-      bit_reverse(s, coeffs.p + c0 * n, cc, uint32_t(po2));
+      if (!coeffs_stay_bitrev(po2)) bit_reverse(s, coeffs.p + c0 * n, cc, uint32_t(po2));
       hash_rows_range(s, suite, nodes.p + domain * 8, state.p, evaluated.p + c0 * domain, domain, cc, c0 == 0,
                       c0 + cc == gs);
     }
@@ -355,7 +364,7 @@ struct Prover {
       for (size_t id = 0; id < 3; id++) {
         uint32_t* dx = upload(xss[id], kSlotTapXs + int(id));
         batch_evaluate_any_host(s, groups[id]->coeffs.p, groups[id]->count, uint32_t(po2), whichs[id], dx,
-                                out.p + off * 4);
+                                out.p + off * 4, groups[id]->bitrev);
         off += whichs[id].size();
       }
       std::vector<uint32_t> h(total * 4);
@@ -377,7 +386,8 @@ struct Prover {
       for (size_t i = 0; i < CHECK_SIZE; i++) which[i] = uint32_t(i);
       std::vector<FpExt> xs(CHECK_SIZE, z_pow);
       DevBuf out(CHECK_SIZE * 4);
-      batch_evaluate_any_host(s, check_group.coeffs.p, CHECK_SIZE, uint32_t(po2), which, upload(xs, kSlotCheckXs), out.p);
+      batch_evaluate_any_host(s, check_group.coeffs.p, CHECK_SIZE, uint32_t(po2), which, upload(xs, kSlotCheckXs), out.p,
+                              check_group.bitrev);
       std::vector<uint32_t> h(CHECK_SIZE * 4);
       d2h(h.data(), out.p, h.size() * 4);
       for (size_t i = 0; i < CHECK_SIZE; i++) coeff_u.push_back(fe_from_words(&h[4 * i]));
@@ -404,6 +414,10 @@ struct Prover {
       std::vector<uint32_t> which(CHECK_SIZE, uint32_t(combo_count));
       mix_poly_coeffs(s, combos.p, check_group.coeffs.p, upload(which, kSlotMixWhichCheck), which, cur_mix, mix_fri, CHECK_SIZE,
                       cycles);
+      R0_REQUIRE(check_group.bitrev == groups[0]->bitrev && groups[1]->bitrev == groups[0]->bitrev &&
+                     groups[2]->bitrev == groups[0]->bitrev,
+                 "coefficient groups in mixed orders");
+      if (check_group.bitrev) bit_reverse_ext(s, combos.p, combo_count + 1, uint32_t(po2));
     }
     if (prof) prof->mark("mix");
     {

@@ -179,6 +179,8 @@ void ntt_interpolate(hipStream_t s, uint32_t* io, size_t count, uint32_t log_n, 
 void ntt_interpolate_from(hipStream_t s, uint32_t* io, const uint32_t* src, size_t count, uint32_t log_n,
                           bool zk_shift);
 void bit_reverse(hipStream_t s, uint32_t* io, size_t count, uint32_t log_n);
+// the same permutation on rows of 2^log_n FpExt elements (AoS, 4 words each)
+void bit_reverse_ext(hipStream_t s, uint32_t* io, size_t count, uint32_t log_n);
 void zk_shift(hipStream_t s, uint32_t* io, size_t count, uint32_t log_n);
 
 // Hashes (hash.hip). suite: 0 = poseidon2, 1 = sha-256, 2 = poseidon254.
@@ -244,8 +246,12 @@ void mix_poly_coeffs(hipStream_t s, uint32_t* out, const uint32_t* in, const uin
 void batch_evaluate_any(hipStream_t s, const uint32_t* coeffs, size_t poly_count, uint32_t log_n,
                         const uint32_t* which, const uint32_t* xs, uint32_t* out, size_t eval_count);
 // the same with `which` on the host (groups evaluations by polynomial without a D2H)
+// bitrev: the coefficient rows are stored in bit-reversed order (row[j] = coefficient
+// rev_{log_n}(j), as the inverse NTT leaves them); needs log_n >= kEvalBitrevMinLog
 void batch_evaluate_any_host(hipStream_t s, const uint32_t* coeffs, size_t poly_count, uint32_t log_n,
-                             const std::vector<uint32_t>& which, const uint32_t* xs, uint32_t* out);
+                             const std::vector<uint32_t>& which, const uint32_t* xs, uint32_t* out,
+                             bool bitrev = false);
+constexpr uint32_t kEvalBitrevMinLog = 12;
 void scatter(hipStream_t s, uint32_t* into, const uint32_t* index, const uint32_t* offsets,
              const uint32_t* values, size_t cycles);
 void copy_elem_slice(hipStream_t s, uint32_t* into, const uint32_t* from, size_t rows, size_t cols,

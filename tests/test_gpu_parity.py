@@ -401,9 +401,13 @@ def test_eval_check(hal, oracle, circuit, po2):
 
 @pytest.mark.parametrize("circuit,suite,po2", [("rv32im", "poseidon2", 8), ("rv32im", "poseidon2", 11),
                                                ("rv32im", "sha-256", 9), ("recursion", "poseidon2", 9),
-                                               ("recursion", "sha-256", 8), ("recursion", "poseidon_254", 8)])
+                                               ("recursion", "sha-256", 8), ("recursion", "poseidon_254", 8),
+                                               ("rv32im", "poseidon2", 12), ("recursion", "sha-256", 13),
+                                               ("rv32im", "poseidon2", 14)])
 def test_prove_segment_seal_identical(hal, hal_sha, oracle, circuit, suite, po2):
-    """Whole-segment seals (Vec<u32>) are bit-identical to the CPU oracle's."""
+    """Whole-segment seals (Vec<u32>) are bit-identical to the CPU oracle's. From po2 12 the
+    prover keeps coefficient rows bit-reversed (prover.cpp: coeffs_stay_bitrev), so the
+    po2 >= 12 cases pin that order through evaluate_any, mix and the combos reversal."""
     if oracle.ref_lib() is None:
         pytest.skip("oracle/_ref not built")
     import risc0_amd as r
