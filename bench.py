@@ -149,6 +149,9 @@ def main():
     from risc0_amd.segments import gather_results
     import hashlib
     digests = gather_results({rank: hashlib.sha256(seal.tobytes()).hexdigest()[:16]}, dist)
+    # ranks that had to share a device (segments.narrow_visible_devices, or the rehearsal switch)
+    shared = gather_results({rank: os.environ.get("R0_RANKS_SHARE_DEVICES") == "1"
+                             or os.environ.get("R0_BENCH_SHARE_GPUS") == "1"}, dist)
     cycles_total = world * args.steps * (1 << args.po2)
     value = cycles_total / t
     ms_per_step = 1000.0 * t / args.steps
@@ -190,7 +193,8 @@ def main():
                        "circuit": args.circuit, "po2": args.po2, "hashfn": args.hashfn,
                        "segments_per_gpu": args.steps, "segments_in_flight_per_gpu": k,
                        "parallelism": f"segment-per-gpu x{world}",
-                       "seal_sha256_by_rank": [digests[i] for i in range(world)]},
+                       "seal_sha256_by_rank": [digests[i] for i in range(world)],
+                       "ranks_share_devices": any(shared[i] for i in range(world))},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

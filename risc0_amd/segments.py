@@ -73,15 +73,22 @@ def narrow_visible_devices(local_rank, env):
     local_rank-th entry of an inherited list, else the local_rank-th device the runtime sees
     (HIP indexes within ROCR_VISIBLE_DEVICES when that is set). The rank then opens ordinal 0.
     Marks env with R0_RANK_BOUND so a second call (the rank itself, after launch_local bound
-    it) leaves it alone. Returns the HIP ordinal to open (0)."""
+    it) leaves it alone. Returns the HIP ordinal to open (0).
+    An inherited list shorter than the ranks is a misconfigured launch: the ranks then share
+    its devices round-robin, with a warning and R0_RANKS_SHARE_DEVICES=1 (bench.py reports
+    it in its config line), rather than ending the job."""
     if env.get("R0_RANK_BOUND") == "1":
         return 0
     inherited = env.get("HIP_VISIBLE_DEVICES") or env.get("CUDA_VISIBLE_DEVICES")
     if inherited:
         devs = [d for d in inherited.split(",") if d.strip() != ""]
+        if not devs:
+            raise RuntimeError(f"no device in HIP_VISIBLE_DEVICES={inherited}")
         if local_rank >= len(devs):
-            raise RuntimeError(f"local rank {local_rank} has no device in HIP_VISIBLE_DEVICES={inherited}")
-        env["HIP_VISIBLE_DEVICES"] = devs[local_rank].strip()
+            print(f"warning: local rank {local_rank} has no device of its own in HIP_VISIBLE_DEVICES={inherited}; "
+                  f"sharing device {devs[local_rank % len(devs)].strip()}", file=sys.stderr)
+            env["R0_RANKS_SHARE_DEVICES"] = "1"
+        env["HIP_VISIBLE_DEVICES"] = devs[local_rank % len(devs)].strip()
     else:
         env["HIP_VISIBLE_DEVICES"] = str(local_rank)
     env.pop("CUDA_VISIBLE_DEVICES", None)
@@ -96,7 +103,8 @@ def rank_env(rank, world, port, base=None):
     env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    narrow_visible_devices(rank, env)
+    if env.get("R0_BENCH_SHARE_GPUS") != "1":  # rehearsal: the ranks share the visible devices
+        narrow_visible_devices(rank, env)
     return env
 
 

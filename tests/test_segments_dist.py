@@ -40,8 +40,14 @@ def test_rank_binds_one_device_like_r0vm():
     # torch.distributed.run ranks (no launch_local) bind themselves
     env = {"LOCAL_RANK": "5"}
     assert narrow_visible_devices(5, env) == 0 and env["HIP_VISIBLE_DEVICES"] == "5"
+    # more ranks than inherited devices: shared round-robin, flagged for the bench line
+    short = {"HIP_VISIBLE_DEVICES": "0,1"}
+    assert narrow_visible_devices(2, short) == 0 and short["HIP_VISIBLE_DEVICES"] == "0"
+    assert short["R0_RANKS_SHARE_DEVICES"] == "1"
     with pytest.raises(RuntimeError):
-        narrow_visible_devices(2, {"HIP_VISIBLE_DEVICES": "0,1"})
+        narrow_visible_devices(0, {"HIP_VISIBLE_DEVICES": ","})
+    # the rehearsal switch leaves the devices to bench.py's round-robin
+    assert "R0_RANK_BOUND" not in rank_env(1, 2, 1, base={"HIP_VISIBLE_DEVICES": "0", "R0_BENCH_SHARE_GPUS": "1"})
 
 
 @pytest.mark.timeout(300)
