@@ -40,6 +40,20 @@ def main():
         for k, v in sorted(r.kernel_times().items()):
             print(f"{os.environ.get('R0HIP_LIB', 'default')}: {k} {v[0] / v[1]:.3f} ms/launch")
         return
+    if "fold" in which:
+        # the Merkle layers of one po2=20 tree (2^22 leaves) down to 1024 nodes
+        D = 4 << 20
+        nodes = hal.copy_from_elem("nodes", rng.integers(0, P, 2 * D * 8, dtype=np.uint64).astype(np.uint32))
+        r.set_kernel_timing(True)
+        for _ in range(5):
+            size = D
+            while size > 1024:
+                hal.hash_fold(nodes, size, size // 2)
+                size //= 2
+        hal.synchronize()
+        for k, (ms, calls, b, _mm) in sorted(r.kernel_times().items()):
+            print(f"{k:28s} {ms / calls:9.3f} ms/launch")
+        return
     cols, po2 = 211, 20
     n = 1 << po2
     inp = hal.copy_from_elem("in", rng.integers(0, P, cols * n, dtype=np.uint64).astype(np.uint32))
