@@ -340,6 +340,7 @@ def kernel_config(circuit, budget):
 U32 = 2**32 - 1
 U64 = 2**64 - 1
 FOLDC = 2**32 % P
+NBW = (P - 11) * 2**32 % P  # kNBeta, Montgomery word of NBETA = -11 (x^4 = NBETA)
 
 
 def redc_max(t):
@@ -465,6 +466,8 @@ def emit(circuit, outdir, budget, host=False):
         "  return FpExt{{lsub(a, b.c[0], kp), kp - b.c[1], kp - b.c[2], kp - b.c[3]}};",
         "}",
         "EC_FN FpExt xmulf(FpExt a, uint32_t b) { return FpExt{{lmul(a.c[0], b), lmul(a.c[1], b), lmul(a.c[2], b), lmul(a.c[3], b)}}; }",
+        "// a * x (the extension generator, FpExt(0, 1, 0, 0)): a limb shift, x^4 = NBETA",
+        "EC_FN FpExt xmulx(FpExt a) { return FpExt{{lmul(a.c[3], kNBeta), a.c[0], a.c[1], a.c[2]}}; }",
         "// extension product; b's upper limbs times NBETA are canonical; four 4-term sums,",
         "// folded and REDC'd without the final min",
         "EC_FN FpExt xmul(FpExt a, FpExt b) {",
@@ -613,6 +616,7 @@ def emit(circuit, outdir, budget, host=False):
         chainpos = {}
         Mv = {}      # word bounds of v<i>
         cval = {}    # Fp constants: Montgomery word
+        ecval = {}   # FpExt constants: Montgomery words of the four limbs
         red_memo = {}
         offs = set()
         acc_hist = []  # Acc variables in emission order (anchors of pin())
@@ -713,6 +717,22 @@ def emit(circuit, outdir, budget, host=False):
                         kp = max(1, -(-y[1] // P)) * P
                         return out("f", f"{kp}u - {y[0]}", kp, name)
             if ta == "e" and tb == "e":
+                # a constant operand (the program's `e` values: x, and Fp constants embedded
+                # as FpExt) needs no full extension product
+                for x, y in ((a, b), (b, a)):
+                    c = ecval.get(x[3]) if x[3] is not None else None
+                    if c is None:
+                        continue
+                    if c[1:] == [0, 0, 0]:
+                        if c[0] == one:
+                            return out("e", y[0], y[1], name)
+                        while not mul_ok(y[1], c[0]):
+                            y = reduce1(y)
+                        return out("e", f"xmulf({y[0]}, {c[0]}u)", redc_max(y[1] * c[0]), name)
+                    if c == [0, one, 0, 0]:
+                        while not mul_ok(y[1], NBW):
+                            y = reduce1(y)
+                        return out("e", f"xmulx({y[0]})", max(y[1], redc_max(y[1] * NBW)), name)
                 while not emul_ok(a[1], b[1]):
                     if a[1] >= b[1]:
                         a = reduce1(a)
@@ -951,6 +971,7 @@ def emit(circuit, outdir, budget, host=False):
                 Mv[i] = cval[i]
             elif op == "e":
                 ev = [enc(x) for x in ins[2:6]]
+                ecval[i] = ev
                 w(f"  const FpExt v{i} = FpExt{{{{{', '.join(str(x) + 'u' for x in ev)}}}}};")
                 Mv[i] = max(ev)
             elif op == "g":
