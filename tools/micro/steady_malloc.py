@@ -12,7 +12,7 @@ import sys
 import threading
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+sys.path[:0] = [os.path.join(ROOT, "oracle"), ROOT, os.path.join(ROOT, "tests")]
 import oracle as o  # noqa: E402  (the CPU checker, for the golden case's witness only)
 import risc0_amd as r  # noqa: E402
 import test_golden as G  # noqa: E402
