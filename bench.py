@@ -30,7 +30,7 @@ P = 15 * 2**27 + 1
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=6)  # a multiple of the segments in flight
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--po2", type=int, default=20)
     ap.add_argument("--circuit", default="rv32im")
@@ -46,7 +46,7 @@ def parse():
                     help="segment size of the CPU baseline proof (default: the bench's own po2, at most 20)")
     ap.add_argument("--inflight", type=int, default=None,
                     help="segments in flight per GPU (host threads, each with its own HIP stream); "
-                         "default 6 up to po2=18, 2 up to po2=22, 1 above (one po2=24 segment needs ~150 GB)")
+                         "default 6 up to po2=18, 3 up to po2=20, 2 up to po2=22, 1 above (one po2=24 segment needs ~150 GB)")
     return ap.parse_args()
 
 
@@ -115,7 +115,7 @@ def main():
     import threading
     # segments in flight per GPU: small segments are latency-bound (6 at po2<=18 measured
     # 5.32 -> 4.67 ms for recursion po2=18), po2=20 gains nothing past 2, po2>22 fits one
-    inflight = args.inflight if args.inflight is not None else (6 if args.po2 <= 18 else 2 if args.po2 <= 22 else 1)
+    inflight = args.inflight if args.inflight is not None else (6 if args.po2 <= 18 else 3 if args.po2 <= 20 else 2 if args.po2 <= 22 else 1)
     k = max(1, min(inflight, len(segs) or 1))
     # per-thread globals buffer: prove_segment zeroizes it in place; the witness
     # groups are only read and are shared
@@ -166,10 +166,13 @@ def main():
         roofline = kt
         phases = {key: round(v / args.steps, 3) for key, v in phase_tot.items()}
         print(json.dumps({"phases_ms": phases, "seal_words": int(seal.size)}), file=sys.stderr)
+        # the side legs keep 2 in flight below po2 21 unless --inflight says otherwise: the
+        # pipeline's uploader and a third prover measured slower there (63.1 against 57.6 ms)
+        kl = k if args.inflight is not None else min(k, 2)
         if args.e2e_steps > 0 and host_witness is not None:
-            e2e = end_to_end(r, hal, args, host_witness, k, version)
+            e2e = end_to_end(r, hal, args, host_witness, kl, version)
         if args.accum_steps > 0 and args.circuit == "rv32im" and host_witness is not None:
-            acc_leg = with_accumulation(r, hal, args, host_witness, k, version)
+            acc_leg = with_accumulation(r, hal, args, host_witness, kl, version)
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(args, circ)
     del host_witness
@@ -407,7 +410,7 @@ def end_to_end(r, hal, args, witness, k, version):
         for hp in hosts:
             r.check(lib.r0hip_host_free(hp))
     return {"value": round(args.e2e_steps * (1 << args.po2) / t, 1), "unit": "cycles/s",
-            "ms_per_step": round(1000.0 * t / args.e2e_steps, 3), "steps": args.e2e_steps,
+            "ms_per_step": round(1000.0 * t / args.e2e_steps, 3), "steps": args.e2e_steps, "segments_in_flight_per_gpu": k,
             "h2d_bytes_per_segment": int(h2d_bytes), "ms_one_segment_unpipelined": round(1000.0 * t_one, 1),
             "note": f"witness in pinned host memory; native pipeline (r0hip_prove_segments): an uploader fills "
                     f"{k + 1} device buffer sets ahead of {k} prover threads, so H2D overlaps proving; a prover "
