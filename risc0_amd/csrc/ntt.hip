@@ -102,8 +102,11 @@ __device__ __forceinline__ void stage_group(uint32_t* lds, const uint32_t* tw, c
 #pragma unroll
         for (uint32_t m = 0; m < M; m++) {
           if (m & half) continue;
-          uint32_t w = tw[hs + k + (m & (half - 1)) * h];
-          uint32_t x = v[m], y = fp_mul(v[m + half], w);
+          // a group that starts at stage 1 has k = 0, so its twiddle w_{2^s}^0 = 1 wherever
+          // m & (half - 1) == 0 (all of stage 1, half of stage 2, a quarter of stage 3):
+          // no multiply, the staged words being canonical already
+          uint32_t x = v[m], y = v[m + half];
+          if (!(S0 == 1 && (m & (half - 1)) == 0)) y = fp_mul(y, tw[hs + k + (m & (half - 1)) * h]);
           v[m] = fp_add(x, y);
           v[m + half] = fp_sub(x, y);
         }
@@ -115,10 +118,10 @@ __device__ __forceinline__ void stage_group(uint32_t* lds, const uint32_t* tw, c
 #pragma unroll
         for (uint32_t m = 0; m < M; m++) {
           if (m & half) continue;
-          uint32_t w = tw[hs + k + (m & (half - 1)) * h];
           uint32_t x = v[m], y = v[m + half];
           v[m] = fp_add(x, y);
-          v[m + half] = fp_mul(fp_sub(x, y), w);
+          v[m + half] = fp_sub(x, y);
+          if (!(S0 == 1 && (m & (half - 1)) == 0)) v[m + half] = fp_mul(v[m + half], tw[hs + k + (m & (half - 1)) * h]);
         }
       }
     }
