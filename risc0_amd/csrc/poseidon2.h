@@ -140,6 +140,65 @@ R0_HD void p2_m_ext64(const uint32_t* x, uint64_t* y) {
   }
 }
 
+// ---- signed Montgomery for the full rounds -----------------------------------------
+// Values are int32 in (-p, p). sredc(t) = (t - m p) / 2^32 with m = t * p^-1 mod 2^32 taken
+// signed, so |result| < |t| / 2^32 + p/2: a product of two values below p in magnitude
+// comes back below 0.969p, closed under multiplication with no correction step (the
+// unsigned REDC needs a canonical square before x^4). Overflow bound: |t| + 2^31 p < 2^63,
+// i.e. |t| < 1.2 p^2, which every product below keeps (bounds at each use). Same R^-1 per
+// reduction as mont_lazy, so the scaled round constants of P2Scaled apply unchanged.
+constexpr uint32_t kPinv = 0u - kNegPinv;  // p^-1 mod 2^32
+R0_HD int64_t smad64(int32_t a, int32_t b, int64_t acc) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(P2_NO_ASM)
+  int64_t r;
+  uint64_t carry;
+  asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(carry) : "v"(a), "v"(b), "v"(acc));
+  return r;
+#else
+  return int64_t(a) * b + acc;
+#endif
+}
+R0_HD int32_t sredc(int64_t t) {
+  const int32_t m = int32_t(uint32_t(uint64_t(t)) * kPinv);
+  return int32_t(uint64_t(t - int64_t(m) * int64_t(kP)) >> 32);  // low word is 0: exact
+}
+R0_HD int32_t smul(int32_t a, int32_t b) { return sredc(int64_t(a) * b); }
+// |x| < 0.5p + 60 (after sredc of an M_EXT output) or x canonical: x^7 with every
+// intermediate below 0.969p in magnitude (products at most 0.94 p^2)
+R0_HD int32_t p2_sbox_s(int32_t x) {
+  const int32_t x2 = smul(x, x);
+  const int32_t x4 = smul(x2, x2);
+  const int32_t x6 = smul(x4, x2);
+  return smul(x6, x);
+}
+R0_HD uint32_t s_canon(int32_t r) {  // (-p, p) -> [0, p)
+  const uint32_t u = uint32_t(r);
+  return umin(u, u + kP);
+}
+// y = M_EXT x over the integers, signed (|x| < 0.969p: |y| < 112 * 0.969p < 2^37)
+R0_HD void p2_m_ext64s(const int32_t* x, int64_t* y) {
+#pragma unroll
+  for (int b = 0; b < 6; b++) {
+    const int32_t* v = x + 4 * b;
+    int64_t t0 = smad64(v[0], 1, smad64(v[1], 1, 0));
+    int64_t t1 = smad64(v[2], 1, smad64(v[3], 1, 0));
+    int64_t t2 = smad64(v[1], 2, t1);
+    int64_t t3 = smad64(v[3], 2, t0);
+    int64_t t4 = int64_t(uint64_t(t1) << 2) + t3;
+    int64_t t5 = int64_t(uint64_t(t0) << 2) + t2;
+    y[4 * b] = t3 + t5;
+    y[4 * b + 1] = t5;
+    y[4 * b + 2] = t2 + t4;
+    y[4 * b + 3] = t4;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    int64_t s = ((y[j] + y[4 + j]) + (y[8 + j] + y[12 + j])) + (y[16 + j] + y[20 + j]);
+#pragma unroll
+    for (int b = 0; b < 6; b++) y[4 * b + j] += s;
+  }
+}
+
 // Full rounds without Barrett steps. A full round's M_EXT output y (< 224p + p with the
 // next round constant) goes straight into a lazy REDC, which returns y * 2^-32 mod p in
 // [0, p + 106) in two instructions instead of p2_red39's seven; that is small enough for
@@ -190,19 +249,23 @@ static constexpr P2Scaled kP2S = p2_make_scaled();
 #endif
 
 R0_HD void poseidon2_mix(uint32_t* c) {
-  uint64_t y[24];
-  uint32_t x[24];
-  p2_m_ext64(c, y);
-  // rolled: each round's 24 constants are loaded at the top of its iteration instead of
-  // all 168 living in SGPRs (which spill to VGPR lanes in hash_rows)
+  int64_t y[24];
+  int32_t x[24];
+#pragma unroll
+  for (int i = 0; i < 24; i++) x[i] = int32_t(c[i]);  // canonical: below p < 2^31
+  p2_m_ext64s(x, y);
+  // Full rounds in signed Montgomery (above): |y + rc| < 113p, so sredc returns below
+  // 0.5p + 54, the S-box's input. Rolled: each round's 24 constants are loaded at the top
+  // of its iteration instead of all 168 living in SGPRs (which spill to VGPR lanes in
+  // hash_rows).
 #pragma unroll 1
   for (int r = 0; r < 4; r++) {
 #pragma unroll
-    for (int i = 0; i < 24; i++) x[i] = p2_sbox_lazy(mont_lazy(y[i] + kP2S.rc[r * 24 + i]));
-    p2_m_ext64(x, y);
+    for (int i = 0; i < 24; i++) x[i] = p2_sbox_s(sredc(y[i] + int64_t(kP2S.rc[r * 24 + i])));
+    p2_m_ext64s(x, y);
   }
 #pragma unroll
-  for (int i = 0; i < 24; i++) c[i] = fp_mul(mont_lazy(y[i]), kP2S.k_mid);
+  for (int i = 0; i < 24; i++) c[i] = s_canon(smul(sredc(y[i]), int32_t(kP2S.k_mid)));
 #pragma unroll
   // Partial rounds keep every cell lazy in [0, 2p): with cells c < X the M_INT output
   // REDC(c*d + sf) < 0.469 X + sf/2^32 + p, whose fixed point (sf < 2^57 + 2^32 after
@@ -223,16 +286,16 @@ R0_HD void poseidon2_mix(uint32_t* c) {
 #pragma unroll
   for (int i = 0; i < 24; i++) c[i] = umin(c[i], c[i] - kP);
 #pragma unroll
-  for (int i = 0; i < 24; i++) x[i] = p2_sbox_lazy(fp_add(c[i], kP2Full[4 * 24 + i]));
-  p2_m_ext64(x, y);
+  for (int i = 0; i < 24; i++) x[i] = p2_sbox_s(int32_t(fp_add(c[i], kP2Full[4 * 24 + i])));
+  p2_m_ext64s(x, y);
 #pragma unroll 1
   for (int r = 5; r < 8; r++) {
 #pragma unroll
-    for (int i = 0; i < 24; i++) x[i] = p2_sbox_lazy(mont_lazy(y[i] + kP2S.rc[r * 24 + i]));
-    p2_m_ext64(x, y);
+    for (int i = 0; i < 24; i++) x[i] = p2_sbox_s(sredc(y[i] + int64_t(kP2S.rc[r * 24 + i])));
+    p2_m_ext64s(x, y);
   }
 #pragma unroll
-  for (int i = 0; i < 24; i++) c[i] = fp_mul(mont_lazy(y[i]), kP2S.k_end);
+  for (int i = 0; i < 24; i++) c[i] = s_canon(smul(sredc(y[i]), int32_t(kP2S.k_end)));
 }
 
 #if defined(__HIP__)
