@@ -13,7 +13,7 @@ run() {  # name, timeout, bench args...
 }
 run po2_24 500 --po2 24 --steps 2 --warmup 1
 run sha256_recursion 300 --circuit recursion --hashfn sha-256 --po2 18 --steps 12 --warmup 6
-run sha256_rv32im 300 --hashfn sha-256 --steps 5 --warmup 2
+run sha256_rv32im 300 --hashfn sha-256 --steps 6 --warmup 3
 run recursion_p2 300 --circuit recursion --po2 18 --steps 12 --warmup 6
 run recursion_p254 300 --circuit recursion --hashfn poseidon_254 --po2 18 --steps 12 --warmup 6
 echo configs done
