@@ -124,10 +124,10 @@ def main():
 
     def prove_on(slot, n):
         for _ in range(n):
-            seal, _mix = r.prove_segment(hal, args.circuit, args.po2, dc, dd, da, globs[slot], version=version)
+            seal, mix = r.prove_segment(hal, args.circuit, args.po2, dc, dd, da, globs[slot], version=version)
             prof = r.last_profile()
             with lock:
-                last["seal"] = seal
+                last["seal"], last["mix"] = seal, mix
                 for key, v in prof.items():
                     phase_tot[key] = phase_tot.get(key, 0.0) + v
 
@@ -174,7 +174,7 @@ def main():
         if args.accum_steps > 0 and args.circuit == "rv32im" and host_witness is not None:
             acc_leg = with_accumulation(r, hal, args, host_witness, kl, version)
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(args, circ)
+            cpu = cpu_baseline(args, circ, seal, last["mix"])
     del host_witness
 
     if rank == 0:
@@ -208,6 +208,10 @@ def main():
         print(json.dumps(line))
     if dist:
         dist.destroy_process_group()
+    if rank == 0 and cpu and (cpu.get("seal_equal") is False or cpu.get("mix_equal") is False):
+        # full-size oracle parity failed: the line above carries both digests
+        print("bench: GPU seal differs from the CPU oracle's on the same witness", file=sys.stderr)
+        sys.exit(1)
 
 
 HBM_PEAK_GBS = 8000.0
@@ -458,10 +462,17 @@ def host_cores():
     return n
 
 
-def cpu_baseline(args, circ):
+def cpu_baseline(args, circ, gpu_seal=None, gpu_mix=None):
     """The CPU oracle (C++ restatement of CpuHal + Prover, eval_check through the
     reference's compiled poly_fp) proving one segment of the bench's own config, with the
-    per-Hal-op breakdown, on every host core the process may use."""
+    per-Hal-op breakdown, on every host core the process may use.
+
+    Its witness is rank 0's (same seed, same draw), so when the sizes agree the oracle
+    seal and mix are compared with the last timed GPU seal and mix: every bench line then
+    carries full-size oracle parity (`seal_equal`, both SHA-256 digests), as the reference
+    prover verifies its own receipt before returning it
+    (zkvm/src/host/server/prove/prover_impl.rs:277-280). main() exits nonzero on a
+    mismatch."""
     try:
         cores = host_cores()
         os.environ["ORACLE_THREADS"] = str(cores)  # read once, at the oracle's first parallel op
@@ -475,16 +486,25 @@ def cpu_baseline(args, circ):
         suite = {"poseidon2": oracle.POSEIDON2, "sha-256": oracle.SHA256, "poseidon_254": oracle.POSEIDON254}[args.hashfn]
         oracle.op_times(reset=True)
         t0 = time.perf_counter()
-        oracle.prove_segment(args.circuit, suite, po2, code, data, accum, glob,
-                             version=2 if args.circuit == "rv32im" else None)
+        cseal, cmix, _ = oracle.prove_segment(args.circuit, suite, po2, code, data, accum, glob,
+                                              version=2 if args.circuit == "rv32im" else None)
         t = time.perf_counter() - t0
         ops = {k: round(v[0], 3) for k, v in sorted(oracle.op_times().items(), key=lambda kv: -kv[1][0])}
         ops["other (transcript, openings, host polys)"] = round(t - sum(ops.values()), 3)
+        import hashlib
+        dig = lambda a: hashlib.sha256(np.ascontiguousarray(a, dtype=np.uint32).tobytes()).hexdigest()
+        parity = {"seal_equal": None, "oracle_seal_sha256": dig(cseal), "oracle_mix_sha256": dig(cmix)}
+        if gpu_seal is not None and po2 == args.po2 and args.po2 <= 22:
+            parity.update({"seal_equal": bool(np.array_equal(cseal, gpu_seal)),
+                           "mix_equal": bool(np.array_equal(cmix, gpu_mix)),
+                           "gpu_seal_sha256": dig(gpu_seal), "gpu_mix_sha256": dig(gpu_mix),
+                           "parity_note": "oracle prover on rank 0's own witness (same seed and draw) against "
+                                          "the last timed GPU seal of that witness"})
         return {"value": round((1 << po2) / t, 1), "unit": "cycles/s", "cores": int(oracle.num_threads()),
                 "kind": "port",
                 "sample": f"one {args.circuit} segment at po2={po2} ({args.hashfn}), {t:.1f} s wall; "
                           "eval_check uses the reference's compiled C++ poly_fp",
-                "seconds_by_hal_op": ops}
+                "seconds_by_hal_op": ops, **parity}
     except Exception as e:  # the baseline is reported, never required
         print(f"cpu baseline failed: {e}", file=sys.stderr)
         return None

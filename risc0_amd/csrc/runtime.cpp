@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <map>
+#include <set>
 #include <tuple>
 #include <mutex>
 #include <thread>
@@ -382,6 +383,7 @@ namespace {
 std::mutex g_host_mu;
 std::multimap<size_t, void*> g_host_free;
 std::map<void*, size_t> g_host_size;
+std::set<void*> g_host_idle;  // the blocks now on g_host_free (a second free must not list one twice)
 }  // namespace
 
 void* host_alloc(size_t bytes) {
@@ -392,6 +394,7 @@ void* host_alloc(size_t bytes) {
     if (it != g_host_free.end() && it->first <= 2 * bytes) {
       void* p = it->second;
       g_host_free.erase(it);
+      g_host_idle.erase(p);
       return p;
     }
   }
@@ -410,6 +413,7 @@ void host_free(void* p) {
   std::lock_guard<std::mutex> lk(g_host_mu);
   auto it = g_host_size.find(p);
   R0_REQUIRE(it != g_host_size.end(), "r0hip_host_free: pointer was not returned by r0hip_host_alloc");
+  R0_REQUIRE(g_host_idle.insert(p).second, "r0hip_host_free: block is already free (double free)");
   g_host_free.emplace(it->second, p);
 }
 
@@ -422,6 +426,7 @@ void host_trim() {
       g_host_size.erase(kv.second);
     }
     g_host_free.clear();
+    g_host_idle.clear();
   }
   for (void* p : release) (void)hipHostFree(p);
 }

@@ -1043,7 +1043,7 @@ def test_satisfying_recursion_program_gpu_seal_passes_validity(hal, hal_sha, ora
 def test_pinned_host_buffers_are_pooled(hal):
     """r0hip_host_free keeps the block page-locked for the next r0hip_host_alloc of its size
     (unpinning stalled later proofs); r0hip_trim returns idle blocks; a pointer
-    the library did not allocate is refused."""
+    the library did not allocate and a second free of one block are refused."""
     import ctypes
     import risc0_amd as r
     lib = r.lib()
@@ -1058,6 +1058,15 @@ def test_pinned_host_buffers_are_pooled(hal):
     r.check(lib.r0hip_host_alloc(ctypes.byref(b), 3 << 20))
     assert b.value == a.value
     r.check(lib.r0hip_host_free(b))
+    # a second free of the same block is refused (it would hand one buffer to two callers)
+    with pytest.raises(r.R0HipError, match="double free"):
+        r.check(lib.r0hip_host_free(b))
+    c, e = ctypes.c_void_p(), ctypes.c_void_p()
+    r.check(lib.r0hip_host_alloc(ctypes.byref(c), 3 << 20))
+    r.check(lib.r0hip_host_alloc(ctypes.byref(e), 3 << 20))
+    assert c.value != e.value
+    r.check(lib.r0hip_host_free(c))
+    r.check(lib.r0hip_host_free(e))
     with pytest.raises(r.R0HipError, match="not returned by r0hip_host_alloc"):
         r.check(lib.r0hip_host_free(ctypes.c_void_p(arr.ctypes.data + 4096)))
     r.trim()
