@@ -1,0 +1,862 @@
+"""Test infrastructure: a restated rv32im preflight for small user-mode programs, producing
+the PreflightTrace the reference's witness generator consumes (rv32im-sys/kernels/cxx/
+preflight.h:21-50), the injector (witgen/mod.rs:226-378) and the global vector
+(witgen/mod.rs:272-327). It follows the executor and preflight of the reference crate:
+
+  * Preflight::preflight (prove/witgen/preflight.rs:91-107): povw nonce, root load, paging
+    in, body, paging out, tables, the memory-transaction wrap and the Poseidon2 z-checks;
+  * the machine (execute/r0vm.rs): resume/suspend through SUSPEND_PC/MODE, registers in
+    memory (USER_REGS_ADDR, x0 writes shunted to base + 64);
+  * the instruction semantics and memory-access order of execute/rv32im.rs:
+    step/step_compute/step_load/step_store/step_system (ecall, mret and traps excepted);
+  * load_u32/store_u32/add_cycle (preflight.rs:373-400, 571-634), fini (265-326) and
+    wrap_memory_txns (212-232).
+
+Paging is reduced to what the rows check locally: the code pages are paged in (their
+Poseidon2 sponges, 32 blocks each, against their digests in the image) and the root node is
+paged out; the witness generator checks each cycle against its own columns, not the whole
+Merkle image, so these traces exercise every row kind it computes for user programs
+(decode, ALU, mul/div, loads, stores, branches, jumps, resume/suspend, the Poseidon2 paging
+rows and rounds, store root, the lookup tables and the done rows). Whether the reference's own generator
+accepts a trace (it throws on any EQZ, on txn/address mismatch, on unset reads) is the
+first thing the tests check, so the restatement is pinned by the reference itself.
+"""
+import re
+
+import numpy as np
+
+P = 15 * 2**27 + 1
+U32_MAX = 0xFFFFFFFF
+
+# execute/platform.rs
+MEMORY_PAGES = 1 << 22
+MACHINE_REGS_WADDR = 0xFFFF0000 // 4
+USER_REGS_WADDR = 0xFFFF0080 // 4
+SUSPEND_PC_WADDR = 0xFFFF0210 // 4
+SUSPEND_MODE_WADDR = 0xFFFF0214 // 4
+GLOBAL_OUTPUT_WADDR = 0xFFFF0240 // 4
+GLOBAL_INPUT_WADDR = 0xFFFF0260 // 4
+MEMORY_END_WADDR = 0x40000000
+MERKLE_TREE_START_WADDR = 0x40000000
+MERKLE_TREE_END_WADDR = 0x44000000
+POVW_NONCE_START_WADDR = 0x44000000
+ZERO_PAGE_END = 0x10000
+KERNEL_START = 0xC0000000
+LOOKUP_TABLE_CYCLES = ((1 << 8) + (1 << 16)) // 16
+RESERVED_CYCLES = LOOKUP_TABLE_CYCLES + 1
+REG_MAX = 32
+
+# CycleState (platform.rs:101-131)
+LOAD_ROOT_AND_NONCE, RESUME, SUSPEND, STORE_ROOT, CONTROL_TABLE, CONTROL_DONE = 0, 1, 4, 5, 6, 7
+POSEIDON_ENTRY, POSEIDON_PAGING = 16, 22
+DECODE = 48
+
+CYCLE_DTYPE = np.dtype([("state", "<u4"), ("pc", "<u4"), ("major", "u1"), ("minor", "u1"), ("machineMode", "u1"),
+                        ("padding", "u1"), ("userCycle", "<u4"), ("txnIdx", "<u4"), ("pagingIdx", "<u4"),
+                        ("bigintIdx", "<u4"), ("diffCount", "<u4", (2,))])
+TXN_DTYPE = np.dtype([("addr", "<u4"), ("cycle", "<u4"), ("word", "<u4"), ("prevCycle", "<u4"), ("prevWord", "<u4")])
+assert CYCLE_DTYPE.itemsize == 36 and TXN_DTYPE.itemsize == 20
+
+# InsnKind (rv32im.rs) -> (major, minor) = (kind / 8, kind % 8)
+KINDS = {"add": 0, "sub": 1, "xor": 2, "or": 3, "and": 4, "slt": 5, "sltu": 6, "addi": 7, "xori": 8, "ori": 9,
+         "andi": 10, "slti": 11, "sltiu": 12, "beq": 13, "bne": 14, "blt": 15, "bge": 16, "bltu": 17, "bgeu": 18,
+         "jal": 19, "jalr": 20, "lui": 21, "auipc": 22, "sll": 24, "slli": 25, "mul": 26, "mulh": 27, "mulhsu": 28,
+         "mulhu": 29, "srl": 32, "sra": 33, "srli": 34, "srai": 35, "div": 36, "divu": 37, "rem": 38, "remu": 39,
+         "lb": 40, "lh": 41, "lw": 42, "lbu": 43, "lhu": 44, "sb": 48, "sh": 49, "sw": 50, "fence": 58}
+
+
+def node_idx_to_waddr(idx):
+    return MERKLE_TREE_END_WADDR - idx * 8
+
+
+def node_waddr_to_idx(waddr):
+    return (MERKLE_TREE_END_WADDR - waddr) // 8
+
+
+def digest_waddr(idx):  # preflight.rs:110-112
+    return MERKLE_TREE_START_WADDR + 8 * (2 * MEMORY_PAGES - idx)
+
+
+def s32(x):
+    return x - (1 << 32) if x & 0x80000000 else x
+
+
+# ------------------------------------------------------------------ a tiny assembler
+R_OPS = {"add": (0, 0), "sub": (0, 0x20), "sll": (1, 0), "slt": (2, 0), "sltu": (3, 0), "xor": (4, 0), "srl": (5, 0),
+         "sra": (5, 0x20), "or": (6, 0), "and": (7, 0), "mul": (0, 1), "mulh": (1, 1), "mulhsu": (2, 1),
+         "mulhu": (3, 1), "div": (4, 1), "divu": (5, 1), "rem": (6, 1), "remu": (7, 1)}
+I_OPS = {"addi": 0, "slti": 2, "sltiu": 3, "xori": 4, "ori": 6, "andi": 7}
+SH_OPS = {"slli": (1, 0), "srli": (5, 0), "srai": (5, 0x20)}
+L_OPS = {"lb": 0, "lh": 1, "lw": 2, "lbu": 4, "lhu": 5}
+S_OPS = {"sb": 0, "sh": 1, "sw": 2}
+B_OPS = {"beq": 0, "bne": 1, "blt": 4, "bge": 5, "bltu": 6, "bgeu": 7}
+
+
+def asm(op, *a):
+    """encode one RV32IM instruction: R (rd, rs1, rs2), I/loads (rd, rs1, imm),
+    stores (rs2, rs1, imm), branches (rs1, rs2, offset), lui/auipc (rd, imm20), jal (rd, off),
+    jalr (rd, rs1, imm), fence ()"""
+    if op in R_OPS:
+        f3, f7 = R_OPS[op]
+        rd, rs1, rs2 = a
+        return f7 << 25 | rs2 << 20 | rs1 << 15 | f3 << 12 | rd << 7 | 0b0110011
+    if op in I_OPS or op in L_OPS or op == "jalr":
+        rd, rs1, imm = a
+        f3, opc = (I_OPS[op], 0b0010011) if op in I_OPS else (L_OPS[op], 0b0000011) if op in L_OPS else (0, 0b1100111)
+        return (imm & 0xFFF) << 20 | rs1 << 15 | f3 << 12 | rd << 7 | opc
+    if op in SH_OPS:
+        f3, f7 = SH_OPS[op]
+        rd, rs1, sh = a
+        return f7 << 25 | (sh & 31) << 20 | rs1 << 15 | f3 << 12 | rd << 7 | 0b0010011
+    if op in S_OPS:
+        rs2, rs1, imm = a
+        return ((imm >> 5) & 0x7F) << 25 | rs2 << 20 | rs1 << 15 | S_OPS[op] << 12 | (imm & 31) << 7 | 0b0100011
+    if op in B_OPS:
+        rs1, rs2, off = a
+        return (((off >> 12) & 1) << 31 | ((off >> 5) & 0x3F) << 25 | rs2 << 20 | rs1 << 15 | B_OPS[op] << 12
+                | ((off >> 1) & 0xF) << 8 | ((off >> 11) & 1) << 7 | 0b1100011)
+    if op in ("lui", "auipc"):
+        rd, imm20 = a
+        return (imm20 & 0xFFFFF) << 12 | rd << 7 | (0b0110111 if op == "lui" else 0b0010111)
+    if op == "jal":
+        rd, off = a
+        return (((off >> 20) & 1) << 31 | ((off >> 1) & 0x3FF) << 21 | ((off >> 11) & 1) << 20
+                | ((off >> 12) & 0xFF) << 12 | rd << 7 | 0b1101111)
+    if op == "fence":
+        return 0b0001111
+    raise ValueError(op)
+
+
+# ------------------------------------------------------------------ Poseidon2 (execute/poseidon2.rs)
+def _p2_consts():
+    """ROUND_CONSTANTS and M_INT_DIAG_HZN (risc0_zkp poseidon2/consts.rs, plain integers) from
+    the oracle's extracted table"""
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "poseidon2_consts.inc")
+    text = open(path).read()
+    tabs = {}
+    for m in re.finditer(r"static const uint32_t (\w+)\[[^\]]*\] = \{(.*?)\};", text, re.S):
+        tabs[m.group(1)] = [int(x, 16) for x in re.findall(r"0x[0-9a-fA-F]+", m.group(2))]
+    return tabs["ROUND_CONSTANTS_INT"], tabs["M_INT_DIAG_HZN_INT"]
+
+
+RC, M_INT_DIAG = _p2_consts()
+ROUNDS_HALF_FULL, ROUNDS_PARTIAL = 4, 21
+POSEIDON_LOAD_STATE, POSEIDON_LOAD_IN, POSEIDON_DO_OUT, POSEIDON_STORE_STATE = 17, 18, 21, 23
+POSEIDON_EXT_ROUND, POSEIDON_INT_ROUND = 24, 25
+TX_READ, TX_PAGE_IN, TX_PAGE_OUT = 0, 1, 2
+
+
+def _circ4(x):  # multiply_by_4x4_circulant (poseidon2.rs:245-258)
+    t0 = (x[0] + x[1]) % P
+    t1 = (x[2] + x[3]) % P
+    t2 = (2 * x[1] + t1) % P
+    t3 = (2 * x[3] + t0) % P
+    t4 = (4 * t1 + t3) % P
+    t5 = (4 * t0 + t2) % P
+    return [(t3 + t5) % P, t5, (t2 + t4) % P, t4]
+
+
+def _m_ext(s):
+    out = [0] * 24
+    sums = [0] * 4
+    for i in range(6):
+        ch = _circ4(s[4 * i:4 * i + 4])
+        for j in range(4):
+            sums[j] = (sums[j] + ch[j]) % P
+            out[4 * i + j] = ch[j]
+    return [(out[i] + sums[i % 4]) % P for i in range(24)]
+
+
+def _sbox(x):
+    return pow(x, 7, P)
+
+
+def _ext_round(s, idx):
+    if idx >= ROUNDS_HALF_FULL:
+        idx += ROUNDS_PARTIAL
+    s = [_sbox((s[i] + RC[idx * 24 + i]) % P) for i in range(24)]
+    return _m_ext(s)
+
+
+def _int_rounds(s):
+    s = list(s)
+    for i in range(ROUNDS_PARTIAL):
+        s[0] = _sbox((s[0] + RC[(ROUNDS_HALF_FULL + i) * 24]) % P)
+        tot = sum(s) % P
+        s = [(tot + M_INT_DIAG[j] * s[j]) % P for j in range(24)]
+    return s
+
+
+class Poseidon2State:
+    """the injected Poseidon2 columns (witgen/poseidon2.rs:39-160): 11 words, inner[24],
+    zcheck (4 words), and the sponge driver Poseidon2State::rest (execute/poseidon2.rs:86-176)"""
+
+    def __init__(self, **kw):
+        self.f = dict(has_state=0, state_addr=0, buf_out_addr=0, is_elem=0, check_out=0, load_tx_type=0,
+                      next_state=0, sub_state=0, buf_in_addr=0, count=0, mode=0)
+        self.f.update(kw)
+        self.inner = [0] * 24
+        self.zcheck = [0, 0, 0, 0]
+
+    def copy(self):
+        c = Poseidon2State(**self.f)
+        c.inner = list(self.inner)
+        c.zcheck = list(self.zcheck)
+        return c
+
+    def as_array(self):
+        f = self.f
+        return [f["has_state"], f["state_addr"], f["buf_out_addr"], f["is_elem"], f["check_out"], f["load_tx_type"],
+                f["next_state"], f["sub_state"], f["buf_in_addr"], f["count"], f["mode"]] + self.inner + self.zcheck
+
+    def step(self, tr, cur, nxt, sub):
+        self.f["next_state"] = nxt
+        self.f["sub_state"] = sub
+        tr.p2_cycle(cur[0], self)
+        cur[0] = nxt
+
+    def rest(self, tr, final_state):
+        f = self.f
+        cur = [f["next_state"]]
+        assert f["has_state"] == 0, "state-carrying sponges are not modelled"
+        addr = f["buf_in_addr"]
+        while f["count"] > 0:
+            self.step(tr, cur, POSEIDON_LOAD_IN, 0)
+            if f["is_elem"]:
+                for i in range(8):
+                    self.inner[i] = tr.load_u32(addr)
+                    addr += 1
+                f["buf_in_addr"] = addr
+                self.step(tr, cur, POSEIDON_LOAD_IN, 1)
+                for i in range(8):
+                    self.inner[8 + i] = tr.load_u32(addr)
+                    addr += 1
+                f["buf_in_addr"] = addr
+            else:
+                for i in range(8):
+                    w = tr.load_u32(addr)
+                    addr += 1
+                    self.inner[2 * i] = w & 0xFFFF
+                    self.inner[2 * i + 1] = w >> 16
+                f["buf_in_addr"] = addr
+            self.inner = _m_ext(self.inner)
+            for i in range(ROUNDS_HALF_FULL):
+                self.step(tr, cur, POSEIDON_EXT_ROUND, i)
+                self.inner = _ext_round(self.inner, i)
+            self.step(tr, cur, POSEIDON_INT_ROUND, 0)
+            self.inner = _int_rounds(self.inner)
+            for i in range(ROUNDS_HALF_FULL, 2 * ROUNDS_HALF_FULL):
+                self.step(tr, cur, POSEIDON_EXT_ROUND, i)
+                self.inner = _ext_round(self.inner, i)
+            f["count"] -= 1
+        self.step(tr, cur, POSEIDON_DO_OUT, 0)
+        out = f["buf_out_addr"]
+        if f["check_out"]:
+            for i in range(8):
+                w = tr.load_u32(out + i)
+                assert w == self.inner[i], "poseidon2 check failed"
+        else:
+            for i in range(8):
+                tr.store_u32(out + i, self.inner[i])
+        f["buf_in_addr"] = 0
+        self.step(tr, cur, final_state, 0)
+
+
+def p2_new_node(node_idx, is_read):  # witgen/poseidon2.rs:60-73
+    return Poseidon2State(buf_out_addr=node_idx_to_waddr(node_idx), is_elem=1, check_out=int(is_read),
+                          load_tx_type=TX_PAGE_IN if is_read else TX_PAGE_OUT, next_state=POSEIDON_PAGING,
+                          buf_in_addr=node_idx_to_waddr(2 * node_idx + 1), count=1, mode=0 if is_read else 4)
+
+
+def p2_new_page(page_idx, is_read):  # witgen/poseidon2.rs:75-87
+    return Poseidon2State(buf_out_addr=node_idx_to_waddr(MEMORY_PAGES + page_idx), check_out=int(is_read),
+                          load_tx_type=TX_PAGE_IN if is_read else TX_PAGE_OUT, next_state=POSEIDON_PAGING,
+                          buf_in_addr=page_idx * 256, count=32, mode=1 if is_read else 3)
+
+
+def ancestors(node):
+    out = []
+    while node != 1:
+        node //= 2
+        out.append(node)
+    return out
+
+
+def node_hash(d_hi, d_lo):
+    """a node's digest from its children (rest() with is_elem = 1, count = 1: children
+    2n+1 then 2n)"""
+    s = _m_ext(list(d_hi) + list(d_lo) + [0] * 8)
+    for i in range(ROUNDS_HALF_FULL):
+        s = _ext_round(s, i)
+    s = _int_rounds(s)
+    for i in range(ROUNDS_HALF_FULL, 2 * ROUNDS_HALF_FULL):
+        s = _ext_round(s, i)
+    return s[:8]
+
+
+def page_digest(words):
+    """the page hash paging checks (the sponge of rest() with is_elem = 0, 32 blocks)"""
+    s = [0] * 24
+    for b in range(32):
+        for i in range(8):
+            w = words[8 * b + i]
+            s[2 * i], s[2 * i + 1] = w & 0xFFFF, w >> 16
+        s = _m_ext(s)
+        for i in range(ROUNDS_HALF_FULL):
+            s = _ext_round(s, i)
+        s = _int_rounds(s)
+        for i in range(ROUNDS_HALF_FULL, 2 * ROUNDS_HALF_FULL):
+            s = _ext_round(s, i)
+    return s[:8]
+
+
+# BabyBear degree-4 extension (x^4 = -11), plain integers, for the Poseidon2 z-checks
+def ext_mul(a, b):
+    r = [0] * 7
+    for i in range(4):
+        for j in range(4):
+            r[i + j] += a[i] * b[j]
+    return [(r[0] - 11 * r[4]) % P, (r[1] - 11 * r[5]) % P, (r[2] - 11 * r[6]) % P, r[3] % P]
+
+
+def ext_add(a, b):
+    return [(x + y) % P for x, y in zip(a, b)]
+
+
+class Trace:
+    """the restated preflight of one segment"""
+
+    def __init__(self, po2, program, *, base_pc=0x10000, data=None, regs=None, seed=1, max_user_cycles=None,
+                 read_nodes=True):
+        self.po2 = po2
+        self.rng = np.random.default_rng(seed)
+        # image: code, data, registers, suspend state, input/output digests
+        mem = {}
+        for i, w in enumerate(program):
+            mem[base_pc // 4 + i] = w
+        for a, w in (data or {}).items():
+            mem[a // 4] = w
+        regs = regs or {}
+        for r in range(REG_MAX):
+            mem[USER_REGS_WADDR + r] = regs.get(r, 0) if r else 0
+        mem[SUSPEND_PC_WADDR] = base_pc
+        mem[SUSPEND_MODE_WADDR] = 0
+        self.input_words = [int(x) for x in self.rng.integers(0, 1 << 32, 8, dtype=np.uint64)]
+        for i in range(8):
+            mem[GLOBAL_OUTPUT_WADDR + i] = int(self.rng.integers(0, 1 << 32))
+        self.nonce = [int(x) for x in self.rng.integers(0, 1 << 32, 8, dtype=np.uint64)]
+        self.rand_z = [int(x) for x in self.rng.integers(0, P, 4)]
+        self.program_end = base_pc + 4 * len(program)
+        self.max_user_cycles = max_user_cycles
+        # pass 1 (the executor's run that fixes the segment's partial image): the pages the
+        # body touches and dirties
+        self.reset(mem, {})
+        self.discover = True
+        self.touched, self.dirty = set(), set()
+        self.body()
+        touched, dirty = sorted(self.touched), sorted(self.dirty)
+        # the sparse Merkle image: page digests, their ancestors hashed from the children,
+        # arbitrary digests for the siblings off the paths (PagingActivity::new, preflight.rs:720-736)
+        anc = lambda pages: sorted({n for p in pages for n in ancestors(MEMORY_PAGES + p)})
+        page_memory = {}
+        digest = {}
+        for p in touched:
+            digest[MEMORY_PAGES + p] = page_digest([mem.get(p * 256 + i, 0) for i in range(256)])
+        nodes_in = anc(touched)
+        for n in sorted(nodes_in, reverse=True):
+            for c in (2 * n, 2 * n + 1):
+                if c not in digest:
+                    digest[c] = [int(x) for x in self.rng.integers(0, P, 8)]
+            digest[n] = node_hash(digest[2 * n + 1], digest[2 * n])
+        for n, d in digest.items():
+            for i, w in enumerate(d):
+                page_memory[node_idx_to_waddr(n) + i] = w
+        self.root = digest[1]
+        self.read_nodes = nodes_in if read_nodes else []
+        self.read_pages = touched
+        self.write_pages = dirty
+        self.write_nodes = anc(dirty)
+        assert self.write_nodes, "a segment pages out at least the registers' page"
+        # pass 2: the preflight proper
+        self.reset(mem, page_memory)
+        self.discover = False
+        self.build()
+
+    def reset(self, mem, page_memory):
+        self.cycles = []
+        self.backs = []
+        self.txns = []
+        self.pc = 0
+        self.machine_mode = 0
+        self.user_cycle = 0
+        self.txn_idx = 0
+        self.mem = dict(mem)              # user/machine memory (word address -> word)
+        self.page_memory = dict(page_memory)  # Merkle node digests (word address -> word)
+        self.orig_words = {}
+        self.prev_cycle = {}
+
+    # ---- memory (preflight.rs:571-634)
+    def load_u32(self, addr):
+        cycle = 2 * len(self.cycles)
+        if addr >= MERKLE_TREE_START_WADDR:
+            if addr < MERKLE_TREE_END_WADDR:
+                word = self.page_memory[addr]
+            else:
+                word = self.nonce[addr - POVW_NONCE_START_WADDR]
+        else:
+            word = self.mem.get(addr, 0)
+            if self.discover:
+                self.touched.add(addr // 256)
+        self.orig_words.setdefault(addr, word)
+        prev = self.prev_cycle.get(addr, U32_MAX)
+        self.prev_cycle[addr] = cycle
+        self.txns.append((addr, cycle, word, prev, word))
+        return word
+
+    def store_u32(self, addr, word):
+        cycle = 2 * len(self.cycles) + 1
+        if addr >= MEMORY_END_WADDR:
+            prev_word = self.page_memory[addr]
+            self.page_memory[addr] = word
+        else:
+            prev_word = self.mem.get(addr, 0)
+            self.mem[addr] = word
+            if self.discover:
+                self.touched.add(addr // 256)
+                self.dirty.add(addr // 256)
+        prev = self.prev_cycle.get(addr, U32_MAX)
+        self.prev_cycle[addr] = cycle
+        self.txns.append((addr, cycle, word, prev, prev_word))
+
+    # ---- cycles (preflight.rs:373-469)
+    def add_cycle(self, state, pc, major, minor, paging_idx=0, back=None):
+        self.cycles.append([state, pc, major, minor, self.machine_mode, self.user_cycle, self.txn_idx, paging_idx,
+                            0, 0, 0])
+        self.backs.append(back)
+        self.txn_idx = len(self.txns)
+
+    def add_cycle_special(self, cur, nxt, pc, paging_idx=0, back=None):
+        self.add_cycle(nxt, pc, 7 + cur // 8, cur % 8, paging_idx, back)
+
+    def p2_cycle(self, cur, p2):  # on_poseidon2_cycle (preflight.rs:688-697): the state as of now
+        self.add_cycle_special(cur, p2.f["next_state"], self.pc, node_waddr_to_idx(p2.f["buf_out_addr"]),
+                               ("p2", p2.copy()))
+
+    # ---- registers (r0vm.rs:674-695), user mode only
+    def load_reg(self, idx):
+        return self.load_u32(USER_REGS_WADDR + idx)
+
+    def store_reg(self, idx, word):
+        self.store_u32(USER_REGS_WADDR + (REG_MAX * 2 if idx == 0 else idx), word & U32_MAX)
+
+    # ---- one instruction (rv32im.rs: step, step_compute, step_load, step_store, step_system)
+    def step(self):
+        pc = self.pc
+        assert pc >= ZERO_PAGE_END and pc < KERNEL_START and pc % 4 == 0, hex(pc)
+        insn = self.load_u32(pc // 4)
+        assert insn & 3 == 3
+        opc, f3, f7 = insn & 0x7F, (insn >> 12) & 7, insn >> 25
+        rd, rs1i, rs2i = (insn >> 7) & 31, (insn >> 15) & 31, (insn >> 20) & 31
+        top = insn >> 31
+        imm_i = (top * 0xFFFFF000) | (f7 << 5) | rs2i
+        imm_s = (top * 0xFFFFF000) | (f7 << 5) | rd
+        imm_b = (top * 0xFFFFF000) | ((rd & 1) << 11) | ((f7 & 0x3F) << 5) | (rd & 0x1E)
+        imm_j = (top * 0xFFF00000) | (rs1i << 15) | (f3 << 12) | ((rs2i & 1) << 11) | ((f7 & 0x3F) << 5) | (rs2i & 0x1E)
+        imm_u = insn & 0xFFFFF000
+        M = U32_MAX
+        if opc == 0b0001111:  # fence
+            kind = "fence"
+            self.pc = pc + 4
+            self.end_insn(kind)
+            return
+        if opc == 0b0000011:  # loads
+            kind = {0: "lb", 1: "lh", 2: "lw", 4: "lbu", 5: "lhu"}[f3]
+            rs1 = self.load_reg(rs1i)
+            addr = (rs1 + imm_i) & M
+            assert addr >= ZERO_PAGE_END and addr < KERNEL_START, hex(addr)
+            data = self.load_u32(addr // 4)
+            sh = 8 * (addr & 3)
+            if kind == "lb":
+                out = (data >> sh) & 0xFF
+                out |= 0xFFFFFF00 if out & 0x80 else 0
+            elif kind == "lh":
+                assert addr & 1 == 0
+                out = (data >> sh) & 0xFFFF
+                out |= 0xFFFF0000 if out & 0x8000 else 0
+            elif kind == "lw":
+                assert addr & 3 == 0
+                out = data
+            elif kind == "lbu":
+                out = (data >> sh) & 0xFF
+            else:
+                assert addr & 1 == 0
+                out = (data >> sh) & 0xFFFF
+            self.store_reg(rd, out)
+            self.pc = pc + 4
+            self.end_insn(kind)
+            return
+        if opc == 0b0100011:  # stores
+            kind = {0: "sb", 1: "sh", 2: "sw"}[f3]
+            rs1 = self.load_reg(rs1i)
+            rs2 = rs1 if rs1i == rs2i else self.load_reg(rs2i)
+            addr = (rs1 + imm_s) & M
+            sh = 8 * (addr & 3)
+            assert addr >= ZERO_PAGE_END and addr < KERNEL_START, hex(addr)
+            data = self.load_u32(addr // 4)
+            if kind == "sb":
+                data = (data & ~(0xFF << sh) & M) | ((rs2 & 0xFF) << sh)
+            elif kind == "sh":
+                assert addr & 1 == 0
+                data = (data & ~(0xFFFF << sh) & M) | ((rs2 & 0xFFFF) << sh)
+            else:
+                assert addr & 3 == 0
+                data = rs2
+            self.store_u32(addr // 4, data)
+            self.pc = pc + 4
+            self.end_insn(kind)
+            return
+        # step_compute
+        if opc == 0b0110011:
+            kind = {(0, 0): "add", (0, 0x20): "sub", (1, 0): "sll", (2, 0): "slt", (3, 0): "sltu", (5, 0): "srl",
+                    (4, 0): "xor", (5, 0x20): "sra", (6, 0): "or", (7, 0): "and", (0, 1): "mul", (1, 1): "mulh",
+                    (2, 1): "mulhsu", (3, 1): "mulhu", (4, 1): "div", (5, 1): "divu", (6, 1): "rem",
+                    (7, 1): "remu"}[(f3, f7)]
+        elif opc == 0b0010011:
+            kind = {0: "addi", 2: "slti", 3: "sltiu", 4: "xori", 6: "ori", 7: "andi"}.get(f3)
+            if kind is None:
+                kind = {(1, 0): "slli", (5, 0): "srli", (5, 0x20): "srai"}[(f3, f7)]
+        elif opc == 0b0110111:
+            kind = "lui"
+        elif opc == 0b0010111:
+            kind = "auipc"
+        elif opc == 0b1100011:
+            kind = {0: "beq", 1: "bne", 4: "blt", 5: "bge", 6: "bltu", 7: "bgeu"}[f3]
+        elif opc == 0b1101111:
+            kind = "jal"
+        elif opc == 0b1100111:
+            kind = "jalr"
+        else:
+            raise ValueError(f"unsupported instruction {insn:#010x}")
+        new_pc = (pc + 4) & M
+        rs1 = self.load_reg(rs1i)
+        rs2 = rs1 if rs1i == rs2i else self.load_reg(rs2i)
+        br = None
+        if kind in B_OPS:
+            cond = {"beq": rs1 == rs2, "bne": rs1 != rs2, "blt": s32(rs1) < s32(rs2), "bge": s32(rs1) >= s32(rs2),
+                    "bltu": rs1 < rs2, "bgeu": rs1 >= rs2}[kind]
+            rd = 0
+            if cond:
+                new_pc = (pc + imm_b) & M
+            out = 0
+        elif kind == "jal":
+            new_pc = (pc + imm_j) & M
+            out = pc + 4
+        elif kind == "jalr":
+            new_pc = (rs1 + imm_i) & M & 0xFFFFFFFE
+            out = pc + 4
+        else:
+            out = alu(kind, rs1, rs2, imm_i, imm_u, pc)
+        assert new_pc % 4 == 0, "misaligned jump (trap) is not modelled"
+        self.store_reg(rd, out)
+        self.pc = new_pc
+        self.end_insn(kind)
+
+    def end_insn(self, kind):  # on_insn_end (preflight.rs:559-564)
+        k = KINDS[kind]
+        if kind == "fence":
+            self.add_cycle(DECODE, self.pc, 7, 2)  # CONTROL0 / FENCE (preflight.rs:440-449)
+        else:
+            self.add_cycle(DECODE, self.pc, k // 8, k % 8)
+        self.user_cycle += 1
+
+    # ---- the segment (preflight.rs:91-107)
+    def build(self):
+        # read_povw_nonce
+        for i in range(8):
+            self.load_u32(POVW_NONCE_START_WADDR + i)
+        self.add_cycle_special(LOAD_ROOT_AND_NONCE, LOAD_ROOT_AND_NONCE, 0)
+        # read_pages: root, Poseidon2 entry, nodes, pages, done
+        for i in range(8):
+            self.load_u32(digest_waddr(1) + i)
+        self.add_cycle_special(LOAD_ROOT_AND_NONCE, POSEIDON_ENTRY, 0)
+        self.p2_cycle(POSEIDON_ENTRY, Poseidon2State(buf_out_addr=MERKLE_TREE_END_WADDR, is_elem=1, check_out=1,
+                                                     load_tx_type=1, next_state=POSEIDON_PAGING, mode=0))
+        for node in self.read_nodes:  # ascending (BTreeSet), Poseidon2::read_node
+            p2_new_node(node, True).rest(self, POSEIDON_PAGING)
+        self.machine_mode = 1
+        for page in self.read_pages:  # Poseidon2::read_page
+            p2_new_page(page, True).rest(self, POSEIDON_PAGING)
+        self.machine_mode = 2
+        self.p2_cycle(POSEIDON_PAGING, Poseidon2State(buf_out_addr=MERKLE_TREE_START_WADDR, next_state=RESUME, mode=2))
+        self.body()
+        # write_pages: entry, pages, nodes, done; write_root
+        self.p2_cycle(POSEIDON_ENTRY, Poseidon2State(buf_out_addr=MERKLE_TREE_START_WADDR, is_elem=1, check_out=1,
+                                                     load_tx_type=1, next_state=POSEIDON_PAGING, mode=3))
+        for page in reversed(self.write_pages):  # Poseidon2::write_page
+            p2_new_page(page, False).rest(self, POSEIDON_PAGING)
+        self.machine_mode = 4
+        for node in reversed(self.write_nodes):  # Poseidon2::write_node
+            p2_new_node(node, False).rest(self, POSEIDON_PAGING)
+        self.machine_mode = 5
+        self.p2_cycle(POSEIDON_PAGING, Poseidon2State(buf_out_addr=MERKLE_TREE_END_WADDR, next_state=STORE_ROOT, mode=5))
+        self.machine_mode = 0
+        for i in range(8):
+            self.load_u32(digest_waddr(1) + i)
+        self.add_cycle_special(STORE_ROOT, CONTROL_TABLE, 0)
+        # generate_tables / fini (preflight.rs:205-326)
+        self.table_split_cycle = len(self.cycles)
+        start = len(self.cycles)
+        for i in range(16, 256, 16):
+            self.add_cycle_special(CONTROL_TABLE, CONTROL_TABLE, i)
+        self.machine_mode = 1
+        for i in range(0, 64 * 1024, 16):
+            self.add_cycle_special(CONTROL_TABLE, CONTROL_TABLE, i)
+        self.machine_mode = 0
+        self.add_cycle_special(CONTROL_TABLE, CONTROL_DONE, 0)
+        # not a terminating segment: the shutdown threshold is this cycle count
+        self.segment_threshold = len(self.cycles)
+        diff = len(self.cycles) - self.segment_threshold
+        self.cycles[diff // 2][9 + diff % 2] += 1
+        self.machine_mode = 1
+        self.add_cycle_special(CONTROL_DONE, CONTROL_DONE, 0)
+        assert len(self.cycles) - start == RESERVED_CYCLES
+        total = 1 << self.po2
+        assert len(self.cycles) <= total, "program too long for the segment"
+        while len(self.cycles) < total:
+            self.add_cycle_special(CONTROL_DONE, CONTROL_DONE, 0)
+        # wrap_memory_txns (preflight.rs:212-232)
+        txns = []
+        for (addr, cycle, word, prev, prev_word) in self.txns:
+            if prev == U32_MAX:
+                prev = self.prev_cycle[addr]
+            else:
+                assert cycle != prev
+                diff = cycle - 1 - prev
+                self.cycles[diff // 2][9 + diff % 2] += 1
+            if cycle == self.prev_cycle[addr]:
+                word = self.orig_words.get(addr, 0)
+            txns.append((addr, cycle, word, prev, prev_word))
+        self.txns = txns
+        # update_p2_zcheck (preflight.rs:234-263)
+        powers = [[1, 0, 0, 0]]
+        for _ in range(16):
+            powers.append(ext_mul(powers[-1], self.rand_z))
+        z = [0, 0, 0, 0]
+        for row, back in enumerate(self.backs):
+            if back is None or back[0] != "p2":
+                continue
+            p2 = back[1]
+            cyc, nxt = self.cycles[row], self.cycles[row + 1]
+            state = (cyc[2] - 7) * 8 + cyc[3]
+            if state == POSEIDON_LOAD_IN:
+                z = ext_mul(z, powers[16])
+                for i, t in enumerate(range(cyc[6], nxt[6])):
+                    addr, cycle, word, prev, prev_word = self.txns[t]
+                    kind = p2.f["load_tx_type"]
+                    if kind == TX_READ:
+                        c0, c1 = 0, 1
+                    elif kind == TX_PAGE_IN:
+                        c0, c1 = 0, (cycle - prev) % P
+                    else:
+                        c0, c1 = ((word & 0xFFFF) - (prev_word & 0xFFFF)) % P, ((word >> 16) - (prev_word >> 16)) % P
+                    z = ext_add(z, [(c0 * x) % P for x in powers[2 * i]])
+                    z = ext_add(z, [(c1 * x) % P for x in powers[2 * i + 1]])
+            if state in (POSEIDON_LOAD_IN, POSEIDON_EXT_ROUND, POSEIDON_INT_ROUND):
+                p2.zcheck = list(z)
+            else:
+                z = [0, 0, 0, 0]
+
+    def body(self):
+        """resume, the program, suspend (preflight.rs:170-185, r0vm.rs:316-331, 506-543)"""
+        self.pc = self.load_u32(SUSPEND_PC_WADDR)
+        self.machine_mode = self.load_u32(SUSPEND_MODE_WADDR)
+        self.add_cycle_special(RESUME, RESUME, self.pc)
+        for i, w in enumerate(self.input_words):
+            self.store_u32(GLOBAL_INPUT_WADDR + i, w)
+        self.add_cycle_special(RESUME, DECODE, self.pc)
+        n = 0
+        while self.pc < self.program_end:
+            if self.max_user_cycles is not None and n >= self.max_user_cycles:
+                break
+            self.step()
+            n += 1
+        # suspend (r0vm.rs:316-321, preflight.rs:528-543)
+        self.store_u32(SUSPEND_PC_WADDR, self.pc)
+        self.store_u32(SUSPEND_MODE_WADDR, self.machine_mode)
+        self.pc = 0
+        self.add_cycle_special(SUSPEND, SUSPEND, 0)
+        for i in range(8):
+            self.load_u32(GLOBAL_OUTPUT_WADDR + i)
+        self.machine_mode = 3
+        self.add_cycle_special(SUSPEND, POSEIDON_ENTRY, 0)
+
+    # ---- outputs
+    def arrays(self):
+        """(cycles, txns) as the reference's RawPreflightCycle / RawMemoryTransaction arrays"""
+        cyc = np.zeros(len(self.cycles), CYCLE_DTYPE)
+        c = np.array(self.cycles, dtype=np.uint64)
+        for j, f in enumerate(("state", "pc", "major", "minor", "machineMode", "userCycle", "txnIdx", "pagingIdx",
+                               "bigintIdx")):
+            cyc[f] = c[:, j]
+        cyc["diffCount"] = c[:, 9:11]
+        tx = np.zeros(len(self.txns), TXN_DTYPE)
+        if self.txns:
+            t = np.array(self.txns, dtype=np.uint64)
+            for j, f in enumerate(TXN_DTYPE.names):
+                tx[f] = t[:, j]
+        return cyc, tx
+
+    def injector(self, lay):
+        """(rows, cols, plain values) of build_injector (witgen/mod.rs:226-270), in push order"""
+        rows, cols, vals = [], [], []
+
+        def put(r, c, v):
+            rows.append(r)
+            cols.append(c)
+            vals.append(v)
+        for row, back in enumerate(self.backs):
+            cyc = self.cycles[row]
+            if back is not None and back[0] == "p2":
+                for col, v in zip(lay["poseidon2_state"], back[1].as_array()):
+                    put(row, col, v)
+            put(row, lay["cycle"], row)
+            put(row, lay["next_pc_low"], cyc[1] & 0xFFFF)
+            put(row, lay["next_pc_high"], cyc[1] >> 16)
+            put(row, lay["next_state_0"], cyc[0])
+            put(row, lay["next_machine_mode"], cyc[4])
+        return np.array(rows, np.uint32), np.array(cols, np.uint32), np.array(vals, np.uint64)
+
+    def global_values(self, lay):
+        """build_global_vec (witgen/mod.rs:272-327): plain values, None = Val::INVALID"""
+        g = [None] * 90
+        gl = lay["global"]
+        for i, w in enumerate(self.root):  # pre_state digest: the root the segment loads
+            g[gl["state_in"][i][0]], g[gl["state_in"][i][1]] = w & 0xFFFF, w >> 16
+        for i, w in enumerate(self.input_words):
+            g[gl["input"][i][0]], g[gl["input"][i][1]] = w & 0xFFFF, w >> 16
+        for i, e in enumerate(self.rand_z):
+            g[gl["rng"] + i] = e
+        g[gl["is_terminate"]] = 0
+        g[gl["shutdown_cycle"]] = self.segment_threshold
+        for i, w in enumerate(self.nonce):
+            g[gl["povw_nonce"][i][0]], g[gl["povw_nonce"][i][1]] = w & 0xFFFF, w >> 16
+        return g
+
+
+def alu(kind, rs1, rs2, imm_i, imm_u, pc):
+    M = U32_MAX
+    if kind == "add":
+        return (rs1 + rs2) & M
+    if kind == "sub":
+        return (rs1 - rs2) & M
+    if kind == "xor":
+        return rs1 ^ rs2
+    if kind == "or":
+        return rs1 | rs2
+    if kind == "and":
+        return rs1 & rs2
+    if kind == "sll":
+        return (rs1 << (rs2 & 31)) & M
+    if kind == "srl":
+        return rs1 >> (rs2 & 31)
+    if kind == "sra":
+        return (s32(rs1) >> (rs2 & 31)) & M
+    if kind == "slt":
+        return int(s32(rs1) < s32(rs2))
+    if kind == "sltu":
+        return int(rs1 < rs2)
+    if kind == "addi":
+        return (rs1 + imm_i) & M
+    if kind == "xori":
+        return rs1 ^ imm_i
+    if kind == "ori":
+        return rs1 | imm_i
+    if kind == "andi":
+        return rs1 & imm_i
+    if kind == "slli":
+        return (rs1 << (imm_i & 31)) & M
+    if kind == "srli":
+        return rs1 >> (imm_i & 31)
+    if kind == "srai":
+        return (s32(rs1) >> (imm_i & 31)) & M
+    if kind == "slti":
+        return int(s32(rs1) < s32(imm_i))
+    if kind == "sltiu":
+        return int(rs1 < imm_i)
+    if kind == "lui":
+        return imm_u
+    if kind == "auipc":
+        return (pc + imm_u) & M
+    if kind == "mul":
+        return (rs1 * rs2) & M
+    if kind == "mulh":
+        return ((s32(rs1) * s32(rs2)) >> 32) & M
+    if kind == "mulhsu":
+        return ((s32(rs1) * rs2) >> 32) & M
+    if kind == "mulhu":
+        return (rs1 * rs2) >> 32
+    if kind == "div":
+        if rs2 == 0:
+            return M
+        q = abs(s32(rs1)) // abs(s32(rs2))
+        return (-q if (s32(rs1) < 0) != (s32(rs2) < 0) else q) & M
+    if kind == "divu":
+        return M if rs2 == 0 else rs1 // rs2
+    if kind == "rem":
+        if rs2 == 0:
+            return rs1
+        r = abs(s32(rs1)) % abs(s32(rs2))
+        return (-r if s32(rs1) < 0 else r) & M
+    if kind == "remu":
+        return rs1 if rs2 == 0 else rs1 % rs2
+    raise ValueError(kind)
+
+
+def random_program(rng, n, data_base=0x00100000, data_words=256):
+    """n instructions of straight-line RV32IM user code with forward branches and jumps:
+    every R/I ALU op, mul/div (divisors sometimes zero), byte/half/word loads and stores
+    into a data area whose base stays in x31, lui/auipc, fence."""
+    prog = [asm("lui", 31, data_base >> 12)]
+    ops_r = list(R_OPS)
+    ops_i = list(I_OPS)
+    kinds = ["r"] * 8 + ["i"] * 5 + ["sh"] * 2 + ["load"] * 3 + ["store"] * 3 + ["branch"] * 2 + ["u"] + ["jal"]
+    rnd = lambda: int(rng.integers(1, 31))  # x1..x30 (x31 holds the data base)
+    while len(prog) < n:
+        k = kinds[int(rng.integers(len(kinds)))]
+        left = n - len(prog)
+        if k == "r":
+            prog.append(asm(ops_r[int(rng.integers(len(ops_r)))], rnd() if rng.random() < .95 else 0, rnd(), rnd()))
+        elif k == "i":
+            prog.append(asm(ops_i[int(rng.integers(len(ops_i)))], rnd(), rnd(), int(rng.integers(-2048, 2048))))
+        elif k == "sh":
+            prog.append(asm(list(SH_OPS)[int(rng.integers(3))], rnd(), rnd(), int(rng.integers(32))))
+        elif k == "load":
+            op = list(L_OPS)[int(rng.integers(5))]
+            align = {"lb": 1, "lbu": 1, "lh": 2, "lhu": 2, "lw": 4}[op]
+            off = int(rng.integers(0, 4 * data_words // align)) * align
+            prog.append(asm(op, rnd(), 31, off))
+        elif k == "store":
+            op = list(S_OPS)[int(rng.integers(3))]
+            align = {"sb": 1, "sh": 2, "sw": 4}[op]
+            off = int(rng.integers(0, 4 * data_words // align)) * align
+            prog.append(asm(op, rnd(), 31, off))
+        elif k == "branch" and left > 3:
+            skip = int(rng.integers(1, min(4, left - 1)))
+            prog.append(asm(list(B_OPS)[int(rng.integers(6))], rnd(), rnd(), 4 * (skip + 1)))
+        elif k == "u":
+            prog.append(asm("lui" if rng.random() < .5 else "auipc", rnd(), int(rng.integers(0, 1 << 20))))
+        elif k == "jal" and left > 3:
+            skip = int(rng.integers(0, min(3, left - 1)))
+            prog.append(asm("jal", rnd(), 4 * (skip + 1)))
+        elif rng.random() < 0.1:
+            prog.append(asm("fence"))
+    return prog[:n]
+
+
+def random_trace(po2, n_insns, seed=1):
+    rng = np.random.default_rng(seed)
+    prog = random_program(rng, n_insns)
+    data = {0x00100000 + 4 * i: int(rng.integers(0, 1 << 32)) for i in range(256)}
+    regs = {r: int(rng.integers(0, 1 << 32)) for r in range(1, 31)}
+    return Trace(po2, prog, data=data, regs=regs, seed=seed)

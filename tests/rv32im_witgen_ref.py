@@ -1,0 +1,74 @@
+"""The reference's rv32im witness generator, compiled from /root/reference by oracle/Makefile
+into oracle/_ref/libref_rv32im_accum.so (test infrastructure only):
+risc0_circuit_rv32im_cpu_witgen (rv32im-sys/kernels/cxx/ffi.cpp:267-308) over the buffers
+WitnessGenerator::hal_generate_witness hands it (witgen/mod.rs:135-176): the global vector
+and the data group filled with Val::INVALID, the injector scattered into data."""
+import ctypes as C
+import json
+import os
+
+import numpy as np
+
+import rv32im_accum_ref as RA
+import rv32im_trace as T
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+P = T.P
+INVALID = RA.INVALID
+DATA_COLS, GLOBAL_WORDS = RA.DATA_COLS, RA.GLOBAL_WORDS
+MODE_PARALLEL, MODE_SEQ_FORWARD, MODE_SEQ_REVERSE = 0, 1, 2
+
+
+class ExecBuffers(C.Structure):
+    """witgen.h:36-39"""
+    _fields_ = [("glob", RA.Buffer), ("data", RA.Buffer)]
+
+
+def layout():
+    with open(os.path.join(ROOT, "risc0_amd", "circuits", "rv32im.witgen.json")) as f:
+        return json.load(f)
+
+
+def encode(v):
+    """Val::new (plain integer -> Montgomery word)"""
+    v = np.asarray(v, dtype=np.uint64) % P
+    return ((v << np.uint64(32)) % np.uint64(P)).astype(np.uint32)
+
+
+def inputs(trace, lay=None):
+    """(data, global, cycles, txns) as hal_generate_witness prepares them: data all INVALID
+    with the injector scattered in, globals INVALID except build_global_vec's words"""
+    lay = lay or layout()
+    rows = 1 << trace.po2
+    data = np.full(DATA_COLS * rows, INVALID, np.uint32)
+    r, c, v = trace.injector(lay)
+    data[c.astype(np.int64) * rows + r] = encode(v)
+    g = trace.global_values(lay)
+    glob = np.array([INVALID if x is None else int(encode(x)) for x in g], np.uint32)
+    cyc, tx = trace.arrays()
+    return data, glob, cyc, tx
+
+
+def witgen(trace, mode=MODE_SEQ_FORWARD, lay=None):
+    """(data, global) after the reference's witness generation; raises RuntimeError with the
+    reference's message when it throws"""
+    data, glob, cyc, tx = inputs(trace, lay)
+    return run(data, glob, cyc, tx, trace.table_split_cycle, 1 << trace.po2, mode)
+
+
+def run(data, glob, cyc, tx, split, rows, mode=MODE_SEQ_FORWARD):
+    data = np.array(data, np.uint32)
+    glob = np.array(glob, np.uint32)
+    cyc = np.array(cyc)  # the reference advances txnIdx in place
+    tx = np.ascontiguousarray(tx)
+    bigint = np.zeros(16, np.uint8)
+    lib = C.CDLL(RA.LIB)
+    f = lib.risc0_circuit_rv32im_cpu_witgen
+    f.restype = C.c_void_p
+    f.argtypes = [C.c_uint32, C.POINTER(ExecBuffers), C.POINTER(RA.PreflightTrace), C.c_uint32]
+    bufs = ExecBuffers(RA.Buffer(glob.ctypes.data, 1, GLOBAL_WORDS, True), RA.Buffer(data.ctypes.data, rows, DATA_COLS, True))
+    pf = RA.PreflightTrace(cyc.ctypes.data, tx.ctypes.data, bigint.ctypes.data, len(tx), 0, split)
+    err = f(mode, C.byref(bufs), C.byref(pf), rows)
+    if err:
+        raise RuntimeError(C.cast(err, C.c_char_p).value.decode())
+    return data, glob

@@ -1,0 +1,84 @@
+"""rv32im witness generation on the CPU: the restated preflight (tests/rv32im_trace.py) is
+accepted by the reference's compiled witness generator (risc0_circuit_rv32im_cpu_witgen,
+rv32im-sys/kernels/cxx/ffi.cpp:267-308), and the committed block IR the GPU kernels are
+generated from (risc0_amd/circuits/rv32im.witgen.ir) reproduces its data and global groups
+word for word, INVALID words included. Failing traces fail in both."""
+import os
+
+import numpy as np
+import pytest
+
+import rv32im_trace as T
+import rv32im_witgen_ir as I
+import rv32im_witgen_ref as W
+
+needs_ref = pytest.mark.skipif(not os.path.exists(W.RA.LIB), reason="oracle/_ref/libref_rv32im_accum.so not built")
+
+
+def test_trace_shapes():
+    """fini's reserved rows and the split (preflight.rs:205-326), the injected cycle columns"""
+    t = T.random_trace(13, 300, seed=7)
+    cyc, tx = t.arrays()
+    n = 1 << 13
+    assert len(cyc) == n and t.table_split_cycle + T.RESERVED_CYCLES <= n
+    assert list(cyc["state"][t.table_split_cycle:t.table_split_cycle + 3]) == [T.CONTROL_TABLE] * 3
+    assert cyc["state"][-1] == T.CONTROL_DONE and cyc["major"][-1] == 7 and cyc["minor"][-1] == 7
+    # every transaction belongs to its cycle (txn.cycle / 2) and each address's first
+    # transaction wraps to that address's last cycle
+    owner = np.searchsorted(cyc["txnIdx"].astype(np.int64), np.arange(len(tx)), side="right") - 1
+    assert np.array_equal(tx["cycle"] // 2, owner)
+    lay = W.layout()
+    r, c, v = t.injector(lay)
+    assert (c == lay["cycle"]).sum() == n
+
+
+@needs_ref
+@pytest.mark.parametrize("po2,n,seed", [(13, 1, 3), (13, 600, 1), (14, 2500, 2), (14, 2500, 5)])
+def test_ir_matches_reference(po2, n, seed):
+    t = T.random_trace(po2, n, seed=seed) if n > 1 else T.Trace(po2, [T.asm("addi", 1, 0, 5)])
+    data, glob, cyc, tx = W.inputs(t)
+    ref_d, ref_g = W.run(data, glob, cyc, tx, t.table_split_cycle, 1 << po2)
+    assert (ref_d == W.INVALID).any() and (ref_d != data).any()
+    d, g = I.witgen(data.copy(), glob.copy(), cyc.copy(), tx, 1 << po2)
+    assert np.array_equal(d, ref_d), np.flatnonzero(d != ref_d)[:10]
+    assert np.array_equal(g, ref_g)
+
+
+@needs_ref
+def test_reference_modes_agree():
+    """the reference's parallel schedule (phase 1 before tableSplitCycle, phase 2 after)
+    gives the forward mode's words: the lookup-table reads of phase 2 see every count"""
+    t = T.random_trace(14, 2000, seed=11)
+    data, glob, cyc, tx = W.inputs(t)
+    a = W.run(data, glob, cyc, tx, t.table_split_cycle, 1 << 14, W.MODE_SEQ_FORWARD)
+    b = W.run(data, glob, cyc, tx, t.table_split_cycle, 1 << 14, W.MODE_PARALLEL)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def _fails_both(data, glob, cyc, tx, split, rows, match):
+    with pytest.raises(RuntimeError, match=match):
+        W.run(data, glob, cyc, tx, split, rows)
+    with pytest.raises(I.WitgenError, match=match):
+        I.witgen(data.copy(), glob.copy(), cyc.copy(), tx, rows)
+
+
+@needs_ref
+def test_failures_match_reference():
+    t = T.random_trace(13, 400, seed=4)
+    data, glob, cyc, tx = W.inputs(t)
+    rows = 1 << 13
+    # a transaction at another address than the step reads (ffi.cpp:101-104)
+    bad = tx.copy()
+    k = int(cyc["txnIdx"][400])
+    bad["addr"][k] ^= 4
+    _fails_both(data, glob, cyc, bad, t.table_split_cycle, rows, "memory peek not in preflight")
+    # a decode row whose major/minor disagree with the instruction word: an EQZ fails
+    c2 = cyc.copy()
+    row = next(r for r in range(rows) if c2["state"][r] == T.DECODE and c2["major"][r] == 0 and c2["minor"][r] == 0)
+    c2["minor"][row] = 1
+    _fails_both(data, glob, c2, tx, t.table_split_cycle, rows, "eqz failure")
+    # an injected next-pc that disagrees with the step: the checked re-store refuses it
+    d2 = data.copy()
+    lay = W.layout()
+    d2[lay["next_pc_low"] * rows + 500] = W.encode(12345)
+    _fails_both(d2, glob, cyc, tx, t.table_split_cycle, rows, "Inconsistent set")
