@@ -19,6 +19,7 @@
 #ifndef R0HIP_H
 #define R0HIP_H
 #include <stddef.h>
+#include <stdbool.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -178,6 +179,42 @@ const char* r0hip_rv32im_accum_finalize(uint32_t* d_accum, size_t rows, size_t c
  * AccumBuffers (witgen.h). Columns are `rows` long. */
 const char* r0hip_rv32im_accum(const uint32_t* d_data, uint32_t* d_accum, const uint32_t* d_global,
                                const uint32_t* d_mix, size_t rows, size_t cols, size_t last_cycle);
+
+/* ---- rv32im witness generation (risc0_circuit_rv32im_cuda_witgen / _cpu_witgen,
+ * rv32im-sys/kernels/cuda/ffi.cu:431-472, kernels/cxx/ffi.cpp:267-308; bound in
+ * rv32im-sys/src/lib.rs:55-86 and called from circuit/rv32im/src/prove/hal/cuda.rs:60-101) ----
+ * The same three structs the reference passes (RawBuffer, RawExecBuffers, RawPreflightTrace,
+ * rv32im-sys/src/lib.rs:20-76), field for field. buffers->global (rows 1, cols 90) and
+ * buffers->data (cols 211, rows a power of two) are DEVICE pointers: the global vector as
+ * build_global_vec makes it and the data group all INVALID with the injector scattered in
+ * (witgen/mod.rs:146-162; r0hip_scatter). preflight's arrays are HOST pointers, as in the
+ * reference: `cycles` RawPreflightCycle records (36 bytes), txns RawMemoryTransaction (20
+ * bytes), bigint_bytes. step_Top runs for cycles [0, cycles) in the reference's two phases
+ * (before and after table_split_cycle). mode (0 parallel, 1 forward, 2 reverse) is checked and
+ * every mode runs the parallel schedule, which gives the same words on any trace the
+ * reference accepts. Fails as the reference throws: EQZ ("eqz failure at: ..."), a
+ * transaction at another cycle or address, reads of unset words, inconsistent re-stores, bad
+ * lookups. Zeroize stays the caller's (witgen/mod.rs:166-170). */
+typedef struct r0hip_raw_buffer {
+  uint32_t* buf;
+  size_t rows;
+  size_t cols;
+  bool checked;
+} r0hip_raw_buffer;
+typedef struct r0hip_raw_exec_buffers {
+  r0hip_raw_buffer global;
+  r0hip_raw_buffer data;
+} r0hip_raw_exec_buffers;
+typedef struct r0hip_raw_preflight_trace {
+  const void* cycles;
+  const void* txns;
+  const uint8_t* bigint_bytes;
+  uint32_t txns_len;
+  uint32_t bigint_bytes_len;
+  uint32_t table_split_cycle;
+} r0hip_raw_preflight_trace;
+const char* r0hip_rv32im_witgen(uint32_t mode, const r0hip_raw_exec_buffers* buffers,
+                                const r0hip_raw_preflight_trace* preflight, uint32_t cycles);
 
 /* ---- recursion witness side: the accumulation step (risc0_circuit_recursion_cuda_accum,
  * recursion-sys/kernels/cuda/ffi.cu; CPU driver recursion-sys/kernels/cxx/ffi.cpp:160-217,

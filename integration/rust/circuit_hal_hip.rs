@@ -7,10 +7,10 @@
 // gfx950 from the circuit, tools/gen_eval_check.py), and so do both circuits' accumulations:
 // rv32im's three phases (r0hip_rv32im_accum: stepAccum generated from the reference's
 // step_TopAccum, the scan and finalizeAccum) and the recursion circuit's
-// (r0hip_recursion_accum), and the recursion circuit's witness generation
-// (r0hip_recursion_witgen). rv32im witness generation (stepExec) stays on the host CPU code of
-// the circuit crate (the same C++ the CPU HAL calls), and its result is uploaded once: a GPU
-// stepExec for rv32im needs the executor's preflight.
+// (r0hip_recursion_accum), and both circuits' witness generation: rv32im's stepExec
+// (r0hip_rv32im_witgen: step_Top generated from the reference's steps.cpp, two phases split
+// at tableSplitCycle, the same RawExecBuffers / RawPreflightTrace the CUDA HAL passes) and the
+// recursion circuit's (r0hip_recursion_witgen).
 //
 // Selection (one arm each):
 //   circuit/rv32im/src/prove/mod.rs:45-55       if #[cfg(feature = "hip")] { self::hal::hip::segment_prover() }
@@ -22,11 +22,11 @@
 use std::{ffi::CString, rc::Rc};
 
 use anyhow::Result;
-use risc0_circuit_rv32im_sys::{RawBuffer, RawExecBuffers, RawPreflightTrace, risc0_circuit_rv32im_cpu_witgen};
+use risc0_circuit_rv32im_sys::{RawBuffer, RawExecBuffers, RawPreflightTrace};
 use risc0_core::{field::ExtElem as _, scope};
 use risc0_sys::{
     ffi_wrap,
-    hip::{r0hip_eval_check, r0hip_rv32im_accum},
+    hip::{r0hip_eval_check, r0hip_rv32im_accum, r0hip_rv32im_witgen},
 };
 use risc0_zkp::hal::{
     AccumPreflight, Buffer, CircuitHal,
@@ -51,27 +51,8 @@ impl<HS: HipHash> HipCircuitHal<HS> {
     }
 }
 
-/// Host image of a MetaBuffer: the C++ step code works on host memory, then the result goes
-/// back to the device buffer in one copy.
-struct HostRows {
-    vals: Vec<Val>,
-    rows: usize,
-    cols: usize,
-    checked: bool,
-}
-
-impl HostRows {
-    fn of<HS: HipHash>(m: &MetaBuffer<HipHal<HS>>) -> Self {
-        Self { vals: m.buf.to_vec(), rows: m.rows, cols: m.cols, checked: m.checked }
-    }
-
-    fn raw(&self) -> RawBuffer {
-        RawBuffer { buf: self.vals.as_ptr(), rows: self.rows, cols: self.cols, checked: self.checked }
-    }
-
-    fn store<HS: HipHash>(&self, m: &MetaBuffer<HipHal<HS>>) {
-        m.buf.view_mut(|dst| dst.copy_from_slice(&self.vals));
-    }
+fn raw_device<HS: HipHash>(m: &MetaBuffer<HipHal<HS>>) -> RawBuffer {
+    RawBuffer { buf: m.buf.dev() as *const Val, rows: m.rows, cols: m.cols, checked: m.checked }
 }
 
 fn raw_preflight(p: &PreflightTrace) -> RawPreflightTrace {
@@ -94,15 +75,14 @@ impl<HS: HipHash> CircuitWitnessGenerator<HipHal<HS>> for HipCircuitHal<HS> {
         data: &MetaBuffer<HipHal<HS>>,
     ) -> Result<()> {
         scope!("witgen");
+        // prove/hal/cuda.rs:60-101 with the HIP kernels: device buffers, host preflight arrays
         let cycles = preflight.cycles.len();
         assert_eq!(cycles, data.rows);
-        let (g, d) = (HostRows::of(global), HostRows::of(data));
-        let buffers = RawExecBuffers { global: g.raw(), data: d.raw() };
+        let buffers = RawExecBuffers { global: raw_device(global), data: raw_device(data) };
         let pf = raw_preflight(preflight);
-        ffi_wrap(|| unsafe { risc0_circuit_rv32im_cpu_witgen(mode as u32, &buffers, &pf, cycles as u32) })?;
-        g.store(global);
-        d.store(data);
-        Ok(())
+        ffi_wrap(|| unsafe {
+            r0hip_rv32im_witgen(mode as u32, &buffers as *const _ as *const _, &pf as *const _ as *const _, cycles as u32)
+        })
     }
 }
 

@@ -232,6 +232,15 @@ unsafe extern "C" {
         h_backs: *const R0HipBigIntBack,
         n: usize,
     ) -> *const c_char;
+    /// risc0_circuit_rv32im_cuda_witgen's role (rv32im-sys ffi.cu:431-472): `buffers` and
+    /// `preflight` point at risc0_circuit_rv32im_sys::{RawExecBuffers, RawPreflightTrace}
+    /// (identical repr(C) layouts: struct r0hip_raw_exec_buffers / r0hip_raw_preflight_trace)
+    pub fn r0hip_rv32im_witgen(
+        mode: u32,
+        buffers: *const c_void,
+        preflight: *const c_void,
+        cycles: u32,
+    ) -> *const c_char;
     /// risc0_circuit_recursion_cuda_witgen's role (recursion-sys ffi.cpp:191-205)
     pub fn r0hip_recursion_witgen(
         d_ctrl: *const u32,

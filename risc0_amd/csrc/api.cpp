@@ -14,6 +14,7 @@
 #include "circuit.h"
 #include "devmem.h"
 #include "runtime.h"
+#include "rv32im_witgen.h"
 
 namespace r0 {
 void combos_sub(hipStream_t s, uint32_t* combos, const uint32_t* deltas, size_t rows, size_t width,
@@ -283,6 +284,23 @@ const char* r0hip_recursion_accum(const uint32_t* d_ctrl, const uint32_t* d_glob
     recursion_accum(stream(), d_ctrl, d_global, d_data, d_mix, d_accum, work_cycles, total_cycles);
   });
 }
+const char* r0hip_rv32im_witgen(uint32_t mode, const r0hip_raw_exec_buffers* buffers,
+                                const r0hip_raw_preflight_trace* preflight, uint32_t cycles) {
+  return wrap([&] {
+    R0_REQUIRE(buffers && preflight && buffers->global.buf && buffers->data.buf, "r0hip_rv32im_witgen: null argument");
+    const CircuitDef* c = find_circuit("rv32im");
+    R0_REQUIRE(buffers->data.cols == c->group_size(2) && buffers->global.cols == c->output_size &&
+                   buffers->global.rows == 1,
+               "r0hip_rv32im_witgen: buffers are not the rv32im data group and global vector");
+    R0_REQUIRE(cycles == buffers->data.rows, "r0hip_rv32im_witgen: cycles must equal the data group's rows");
+    stage_reset();
+    rv32im_witgen(stream(), mode, buffers->data.buf, buffers->global.buf, buffers->data.rows,
+                  static_cast<const rvwg::PreflightCycle*>(preflight->cycles),
+                  static_cast<const rvwg::MemoryTxn*>(preflight->txns), preflight->txns_len, preflight->bigint_bytes,
+                  preflight->bigint_bytes_len, preflight->table_split_cycle, cycles);
+  });
+}
+
 const char* r0hip_recursion_witgen(const uint32_t* d_ctrl, uint32_t* d_data, uint32_t* d_global, size_t total_cycles,
                                    const uint32_t* h_wom, size_t n_wom, const uint32_t* h_cycles, size_t n_cycles,
                                    const uint32_t* h_iops, size_t n_iops) {

@@ -98,6 +98,13 @@ enum ScratchSlot : int {
   kSlotWitgenRuns = 72,
   kSlotWitgenIopIdx = 73,
   kSlotWitgenTemp = 74,
+  // rv32im witness generation (rv32im_witgen.hip): the uploaded preflight trace, the cycle
+  // lists per instruction arm, the lookup tables and the error record
+  kSlotRvwgCycles = 75,
+  kSlotRvwgTxns = 76,
+  kSlotRvwgBigint = 77,
+  kSlotRvwgLists = 78,
+  kSlotRvwgTables = 79,
 };
 
 // Scratch buffer reused across calls (grown on demand; stream-ordered use only).

@@ -1,0 +1,220 @@
+// Shared by the generated rv32im witness-generation kernels (tools/gen_rv32im_witgen.py ->
+// gen/rvwitgen/*.hip) and their driver (rv32im_witgen.hip): the preflight records, the
+// argument block, the reference's checked buffers and its externs on the device
+// (rv32im-sys/kernels/cxx/ffi.cpp:84-228, buffers.h, tables.h).
+#pragma once
+#include "bb31.h"
+#include "runtime.h"
+
+namespace r0 {
+namespace rvwg {
+
+constexpr uint32_t kThreads = 128;
+constexpr uint32_t kInvalid = 0xFFFFFFFFu;  // Fp::invalid()
+constexpr uint32_t kMajors = 13;            // Top's instruction mux (majorOnehot)
+
+// rv32im-sys/kernels/cxx/preflight.h:21-41 (RawPreflightCycle / RawMemoryTransaction)
+struct PreflightCycle {
+  uint32_t state;
+  uint32_t pc;
+  uint8_t major;
+  uint8_t minor;
+  uint8_t machine_mode;
+  uint8_t padding;
+  uint32_t user_cycle;
+  uint32_t txn_idx;
+  uint32_t paging_idx;
+  uint32_t bigint_idx;
+  uint32_t diff_count[2];
+};
+static_assert(sizeof(PreflightCycle) == 36, "RawPreflightCycle layout");
+
+struct MemoryTxn {
+  uint32_t addr;
+  uint32_t cycle;
+  uint32_t word;
+  uint32_t prev_cycle;
+  uint32_t prev_word;
+};
+static_assert(sizeof(MemoryTxn) == 20, "RawMemoryTransaction layout");
+
+// error codes (err[0]); err[1] is the cycle, err[2] a detail (column, index)
+constexpr uint32_t kErrEqz = 0x10000u;  // + the EQZ message index (gen/rvwitgen messages)
+constexpr uint32_t kErrUnset = 0x20001u;         // checked read of Fp::invalid() (buffers.h:45-52)
+constexpr uint32_t kErrInconsistent = 0x20002u;  // checked set of another value (buffers.h:30-43)
+constexpr uint32_t kErrUnreachable = 0x20003u;   // "Reached unreachable mux arm"
+constexpr uint32_t kErrTxnCycle = 0x20004u;      // ffi.cpp:96-99
+constexpr uint32_t kErrTxnAddr = 0x20005u;       // ffi.cpp:101-104
+constexpr uint32_t kErrTxnRange = 0x20006u;      // a transaction past the trace's
+constexpr uint32_t kErrLookupTable = 0x20007u;   // tables.h:40-42, 57-59
+constexpr uint32_t kErrLookupIndex = 0x20008u;   // tables.h:43-46
+constexpr uint32_t kErrBigint = 0x20009u;        // bigIntExtern past the trace's bytes
+constexpr uint32_t kErrDiffCount = 0x2000Au;     // getDiffCount past the trace's cycles
+constexpr uint32_t kErrMajor = 0x2000Bu;         // a cycle's major outside the 13 instruction arms
+
+struct Args {
+  uint32_t* data;    // DATA x rows, column-major (MutableBufObj over Buffer<checked>)
+  uint32_t* global;  // the global vector (GlobalBufObj over Buffer<checked>)
+  uint32_t rows;     // a power of two
+  uint32_t ncycles;  // preflight cycles (lastCycle)
+  const PreflightCycle* cycles;
+  const MemoryTxn* txns;
+  uint32_t n_txns;
+  const uint8_t* bigint;
+  uint32_t n_bigint;
+  uint32_t* u8;   // LookupTables::tableU8 (256 counters)
+  uint32_t* u16;  // LookupTables::tableU16 (65536 counters)
+  uint32_t* err;  // [code, cycle, detail]
+};
+
+// Fp::asUInt32 / Fp(uint32_t)
+__device__ __forceinline__ uint32_t to_u32(uint32_t x) { return mont_reduce(x); }
+__device__ __forceinline__ uint32_t from_u32(uint32_t v) { return fp_mul(v % kP, kR2); }
+
+__device__ __forceinline__ void fail(const Args& A, uint32_t code, uint32_t cycle, uint32_t detail = 0) {
+  if (atomicCAS(A.err, 0u, code) == 0u) {
+    A.err[1] = cycle;
+    A.err[2] = detail;
+  }
+}
+
+// Buffer::get / Buffer::set with checked = true
+__device__ __forceinline__ uint32_t ld(const Args& A, uint32_t col, uint32_t row, uint32_t cycle) {
+  const uint32_t v = A.data[uint64_t(col) * A.rows + row];
+  if (v == kInvalid) fail(A, kErrUnset, cycle, col);
+  return v;
+}
+
+__device__ __forceinline__ void st(const Args& A, uint32_t col, uint32_t cycle, uint32_t v) {
+  uint32_t* p = A.data + uint64_t(col) * A.rows + cycle;
+  const uint32_t old = *p;
+  if (old != kInvalid && old != v) fail(A, kErrInconsistent, cycle, col);
+  *p = v;
+}
+
+__device__ __forceinline__ uint32_t gld(const Args& A, uint32_t idx, uint32_t cycle) {
+  const uint32_t v = A.global[idx];
+  if (v == kInvalid) fail(A, kErrUnset, cycle, 0x10000u + idx);
+  return v;
+}
+
+__device__ __forceinline__ void gst(const Args& A, uint32_t idx, uint32_t cycle, uint32_t v) {
+  const uint32_t old = A.global[idx];
+  if (old != kInvalid && old != v) fail(A, kErrInconsistent, cycle, 0x10000u + idx);
+  A.global[idx] = v;
+}
+
+// extern_getMemoryTxn (ffi.cpp:84-113): the cycle's next transaction
+__device__ __forceinline__ void txn(const Args& A, uint32_t cycle, uint32_t& cur, uint32_t addr_w, uint32_t& prev_cycle,
+                                    uint32_t& prev_lo, uint32_t& prev_hi, uint32_t& lo, uint32_t& hi) {
+  if (cur >= A.n_txns) {
+    fail(A, kErrTxnRange, cycle, cur);
+    prev_cycle = prev_lo = prev_hi = lo = hi = 0u;
+    return;
+  }
+  const MemoryTxn t = A.txns[cur++];
+  if (t.cycle / 2 != cycle) fail(A, kErrTxnCycle, cycle, t.cycle);
+  if (t.addr != to_u32(addr_w)) fail(A, kErrTxnAddr, cycle, t.addr);
+  prev_cycle = from_u32(t.prev_cycle);
+  prev_lo = from_u32(t.prev_word & 0xFFFFu);
+  prev_hi = from_u32(t.prev_word >> 16);
+  lo = from_u32(t.word & 0xFFFFu);
+  hi = from_u32(t.word >> 16);
+}
+
+// extern_hostReadPrepare / extern_hostWrite (ffi.cpp:201-212): the word of the cycle's next
+// transaction, without advancing
+__device__ __forceinline__ uint32_t host_word(const Args& A, uint32_t cycle, uint32_t cur) {
+  if (cur >= A.n_txns) {
+    fail(A, kErrTxnRange, cycle, cur);
+    return 0u;
+  }
+  return from_u32(A.txns[cur].word);
+}
+
+// LookupTables::lookupDelta (tables.h:33-53; the count argument is not used there either)
+__device__ __forceinline__ void lookup_delta(const Args& A, uint32_t cycle, uint32_t table_w, uint32_t index_w) {
+  const uint32_t table = to_u32(table_w), index = to_u32(index_w);
+  if (table == 0u) return;
+  if (table != 8u && table != 16u) {
+    fail(A, kErrLookupTable, cycle, table);
+    return;
+  }
+  if (index >= (1u << table)) {
+    fail(A, kErrLookupIndex, cycle, index);
+    return;
+  }
+  atomicAdd((table == 8u ? A.u8 : A.u16) + index, 1u);
+}
+
+// LookupTables::lookupCurrent (tables.h:55-66)
+__device__ __forceinline__ uint32_t lookup_current(const Args& A, uint32_t cycle, uint32_t table_w, uint32_t index_w) {
+  const uint32_t table = to_u32(table_w), index = to_u32(index_w);
+  if ((table != 8u && table != 16u) || index >= (1u << table)) {
+    fail(A, table != 8u && table != 16u ? kErrLookupTable : kErrLookupIndex, cycle, index);
+    return 0u;
+  }
+  return from_u32(__hip_atomic_load((table == 8u ? A.u8 : A.u16) + index, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// extern_getDiffCount (ffi.cpp:141-145)
+__device__ __forceinline__ uint32_t diff_count(const Args& A, uint32_t cycle, uint32_t c_w) {
+  const uint32_t c = to_u32(c_w);
+  if (c / 2 >= A.ncycles) {
+    fail(A, kErrDiffCount, cycle, c);
+    return 0u;
+  }
+  return from_u32(A.cycles[c / 2].diff_count[c % 2]);
+}
+
+// divide_rv32im + extern_divide (ffi.cpp:54-82, 177-188)
+__device__ __forceinline__ void divide(uint32_t nl, uint32_t nh, uint32_t dl, uint32_t dh, uint32_t sign_w, uint32_t& q0,
+                                       uint32_t& q1, uint32_t& r0, uint32_t& r1) {
+  uint32_t numer = to_u32(nl) | (to_u32(nh) << 16);
+  uint32_t denom = to_u32(dl) | (to_u32(dh) << 16);
+  const uint32_t sign = to_u32(sign_w);
+  const uint32_t ones = sign == 2u;
+  const bool neg_n = sign && int32_t(numer) < 0;
+  const bool neg_d = sign == 1u && int32_t(denom) < 0;
+  if (neg_n) numer = -numer - ones;
+  if (neg_d) denom = -denom - ones;
+  uint32_t quot, rem;
+  if (denom == 0u) {
+    quot = 0xFFFFFFFFu;
+    rem = numer;
+  } else {
+    quot = numer / denom;
+    rem = numer % denom;
+  }
+  const uint32_t qneg = uint32_t(neg_n ^ neg_d) - uint32_t(denom == 0u) * uint32_t(neg_n);
+  if (qneg) quot = -quot - ones;
+  if (neg_n) rem = -rem - ones;
+  q0 = from_u32(quot & 0xFFFFu);
+  q1 = from_u32(quot >> 16);
+  r0 = from_u32(rem & 0xFFFFu);
+  r1 = from_u32(rem >> 16);
+}
+
+// extern_bigIntExtern (ffi.cpp:221-228)
+__device__ __forceinline__ uint32_t bigint_byte(const Args& A, uint32_t cycle, uint32_t i) {
+  const uint32_t k = A.cycles[cycle].bigint_idx + i;
+  if (k >= A.n_bigint) {
+    fail(A, kErrBigint, cycle, k);
+    return 0u;
+  }
+  return from_u32(A.bigint[k]);
+}
+
+}  // namespace rvwg
+
+// the generated kernels: step_Top specialised to instruction arm `major` over a list of cycles
+void rv32im_witgen_major(uint32_t major, hipStream_t s, const rvwg::Args& A, const uint32_t* cycles, uint32_t n);
+// EQZ messages of the generated code (steps.cpp locations), by index
+const char* rv32im_witgen_message(uint32_t k);
+// the driver (rv32im_witgen.hip): both phases over cycles [0, last_cycle); synchronises,
+// throws on a failed check
+void rv32im_witgen(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
+                   const rvwg::PreflightCycle* h_cycles, const rvwg::MemoryTxn* h_txns, size_t n_txns,
+                   const uint8_t* h_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle);
+
+}  // namespace r0

@@ -89,6 +89,7 @@ def _declare(L):
                                       C.c_uint32, u32p, sz, C.POINTER(sz), u32p],
         "r0hip_rv32im_bigint_accum_states": [u32p, vp, sz, sz, u32p],
         "r0hip_recursion_witgen": [vp, vp, vp, sz, u32p, sz, u32p, sz, u32p, sz],
+        "r0hip_rv32im_witgen": [C.c_uint32, vp, vp, C.c_uint32],
         "r0hip_prove_recursion": [C.c_int, C.c_uint32, vp, u32p, sz, u32p, sz, u32p, sz, C.c_uint64, u32p, sz,
                                   C.POINTER(sz), u32p],
         "r0hip_rv32im_bigint_accum_inject": [vp, sz, u32p, vp, sz],
@@ -445,6 +446,39 @@ def prove_recursion(hal, po2, ctrl, wom, cycles, iops, noise_seed, seal_cap=1 <<
                                       noise_seed, seal.ctypes.data_as(u32p), seal_cap, C.byref(n),
                                       mix.ctypes.data_as(u32p)))
     return seal[: n.value].copy(), mix
+
+
+class RawBuffer(C.Structure):
+    """struct r0hip_raw_buffer (RawBuffer, rv32im-sys/src/lib.rs:63-69)"""
+    _fields_ = [("buf", C.c_void_p), ("rows", C.c_size_t), ("cols", C.c_size_t), ("checked", C.c_bool)]
+
+
+class RawExecBuffers(C.Structure):
+    """struct r0hip_raw_exec_buffers (RawExecBuffers, lib.rs:71-75)"""
+    _fields_ = [("glob", RawBuffer), ("data", RawBuffer)]
+
+
+class RawPreflightTrace(C.Structure):
+    """struct r0hip_raw_preflight_trace (RawPreflightTrace, lib.rs:53-61): host pointers"""
+    _fields_ = [("cycles", C.c_void_p), ("txns", C.c_void_p), ("bigint_bytes", C.c_void_p), ("txns_len", C.c_uint32),
+                ("bigint_bytes_len", C.c_uint32), ("table_split_cycle", C.c_uint32)]
+
+
+def rv32im_witgen(data, glob, cycles, txns, table_split, bigint=None, mode=0):
+    """r0hip_rv32im_witgen: the rv32im witness generation (step_Top per cycle, two phases) on
+    the device. data (211 x rows) and glob (90 words) are device buffers as the witness
+    generator prepares them (INVALID with the injector scattered in); cycles / txns are the
+    preflight's RawPreflightCycle / RawMemoryTransaction arrays (numpy structured or raw bytes,
+    one record per row)."""
+    cyc = np.ascontiguousarray(cycles)
+    tx = np.ascontiguousarray(txns)
+    bi = np.ascontiguousarray(bigint if bigint is not None else np.zeros(0, np.uint8), dtype=np.uint8)
+    rows = data.size // 211
+    assert cyc.nbytes == 36 * rows and tx.nbytes % 20 == 0
+    bufs = RawExecBuffers(RawBuffer(glob.ptr, 1, glob.size, True), RawBuffer(data.ptr, rows, 211, True))
+    pf = RawPreflightTrace(cyc.ctypes.data, tx.ctypes.data if tx.nbytes else None, bi.ctypes.data if bi.size else None,
+                           tx.nbytes // 20, bi.size, table_split)
+    check(lib().r0hip_rv32im_witgen(mode, C.byref(bufs), C.byref(pf), rows))
 
 
 class SegmentJob(C.Structure):

@@ -1,0 +1,76 @@
+"""rv32im witness generation on the GPU (r0hip_rv32im_witgen, generated from the reference's
+step_Top) against the reference's compiled risc0_circuit_rv32im_cpu_witgen
+(rv32im-sys/kernels/cxx/ffi.cpp:267-308, forward mode) on traces of the restated preflight
+(tests/rv32im_trace.py): the data and global groups word for word, INVALID words included,
+and the same failures."""
+import numpy as np
+import pytest
+
+import rv32im_trace as T
+import rv32im_witgen_ref as W
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def hal():
+    import risc0_amd as r
+    return r.HipHal("poseidon2")
+
+
+def gpu_witgen(hal, data, glob, cyc, tx, split, mode=0):
+    import risc0_amd as r
+    dd = hal.copy_from_elem("data", data)
+    dg = hal.copy_from_elem("global", glob)
+    r.rv32im_witgen(dd, dg, cyc, tx, split, mode=mode)
+    return dd.to_numpy(), dg.to_numpy()
+
+
+@pytest.mark.parametrize("po2,n,seed", [(13, 1, 1), (13, 300, 2), (14, 2500, 3), (16, 12000, 4), (20, 60000, 5)])
+def test_rv32im_witgen_matches_reference(hal, po2, n, seed):
+    t = T.random_trace(po2, n, seed=seed) if n > 1 else T.Trace(po2, [T.asm("addi", 1, 0, 5)])
+    data, glob, cyc, tx = W.inputs(t)
+    ref_d, ref_g = W.run(data, glob, cyc, tx, t.table_split_cycle, 1 << po2)
+    d, g = gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle)
+    bad = np.flatnonzero(d != ref_d)
+    assert bad.size == 0, f"{bad.size} words differ; first (col, row): {[(int(i) >> po2, int(i) & ((1 << po2) - 1)) for i in bad[:8]]}"
+    assert np.array_equal(g, ref_g)
+    assert (d == W.INVALID).any()  # columns no arm of a row writes stay INVALID, as in the reference
+
+
+def test_rv32im_witgen_modes(hal):
+    """every mode runs the same schedule and gives the reference's forward-mode words"""
+    t = T.random_trace(13, 500, seed=9)
+    data, glob, cyc, tx = W.inputs(t)
+    ref = W.run(data, glob, cyc, tx, t.table_split_cycle, 1 << 13)
+    for mode in (0, 1, 2):
+        d, g = gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle, mode)
+        assert np.array_equal(d, ref[0]) and np.array_equal(g, ref[1])
+
+
+def test_rv32im_witgen_failures(hal):
+    """the reference's throws are errors here too, and a failed call leaves the next one clean"""
+    import risc0_amd as r
+    t = T.random_trace(13, 400, seed=4)
+    data, glob, cyc, tx = W.inputs(t)
+    rows = 1 << 13
+    bad = tx.copy()
+    bad["addr"][int(cyc["txnIdx"][400])] ^= 4
+    with pytest.raises(r.R0HipError, match="memory peek not in preflight"):
+        gpu_witgen(hal, data, glob, cyc, bad, t.table_split_cycle)
+    c2 = cyc.copy()
+    row = next(i for i in range(rows) if c2["state"][i] == T.DECODE and c2["major"][i] == 0 and c2["minor"][i] == 0)
+    c2["minor"][row] = 1
+    with pytest.raises(r.R0HipError, match="eqz failure"):
+        gpu_witgen(hal, data, glob, c2, tx, t.table_split_cycle)
+    d2 = data.copy()
+    d2[W.layout()["next_pc_low"] * rows + 500] = W.encode(12345)
+    with pytest.raises(r.R0HipError, match="Inconsistent set"):
+        gpu_witgen(hal, d2, glob, cyc, tx, t.table_split_cycle)
+    c3 = cyc.copy()
+    c3["major"][77] = 13
+    with pytest.raises(r.R0HipError, match="selects no instruction arm"):
+        gpu_witgen(hal, data, glob, c3, tx, t.table_split_cycle)
+    ref = W.run(data, glob, cyc, tx, t.table_split_cycle, rows)
+    d, g = gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle)
+    assert np.array_equal(d, ref[0]) and np.array_equal(g, ref[1])
