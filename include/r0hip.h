@@ -216,6 +216,23 @@ typedef struct r0hip_raw_preflight_trace {
 const char* r0hip_rv32im_witgen(uint32_t mode, const r0hip_raw_exec_buffers* buffers,
                                 const r0hip_raw_preflight_trace* preflight, uint32_t cycles);
 
+/* ---- rv32im prove_core from a preflight trace: SegmentProverImpl::prove_core
+ * (circuit/rv32im/src/prove/hal/mod.rs:143-224) over WitnessGenerator::new and ::accum
+ * (witgen/mod.rs:106-223), every step on the device ----
+ * h_global: build_global_vec's 90 Montgomery words (INVALID where unset, witgen/mod.rs:272-327).
+ * The injector (Injector, witgen/mod.rs:329-378) as hal.scatter takes it: h_inj_index
+ * (inj_rows + 1 entries), h_inj_offsets / h_inj_values (h_inj_index[inj_rows] entries:
+ * col * 2^po2 + row, Montgomery value). preflight as r0hip_rv32im_witgen takes it (cycles =
+ * 2^po2 records); mode as there. h_bigint / n_bigint: the trace's Back::BigInt records, as
+ * r0hip_prove_segment_accum takes them. Runs: data INVALID, scatter, stepExec (both phases),
+ * zeroize, then the prove_core sequence with the version word 2 (RV32IM_SEAL_VERSION) and the
+ * accumulation on the device. Seal and mix out as r0hip_prove_segment. */
+const char* r0hip_prove_segment_trace(int suite, uint32_t po2, uint32_t mode, const uint32_t* h_global,
+                                      const uint32_t* h_inj_index, size_t inj_rows, const uint32_t* h_inj_offsets,
+                                      const uint32_t* h_inj_values, const r0hip_raw_preflight_trace* preflight,
+                                      const r0hip_bigint_back* h_bigint, size_t n_bigint, uint32_t* h_seal,
+                                      size_t seal_cap, size_t* seal_len, uint32_t* h_mix_out);
+
 /* ---- recursion witness side: the accumulation step (risc0_circuit_recursion_cuda_accum,
  * recursion-sys/kernels/cuda/ffi.cu; CPU driver recursion-sys/kernels/cxx/ffi.cpp:160-217,
  * called from circuit/recursion/src/prove/witgen.rs:162-170): for cycles [0, work_cycles) the

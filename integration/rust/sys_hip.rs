@@ -241,6 +241,24 @@ unsafe extern "C" {
         preflight: *const c_void,
         cycles: u32,
     ) -> *const c_char;
+    /// rv32im SegmentProverImpl::prove_core from a preflight trace (prove/hal/mod.rs:143-224)
+    pub fn r0hip_prove_segment_trace(
+        suite: c_int,
+        po2: u32,
+        mode: u32,
+        h_global: *const u32,
+        h_inj_index: *const u32,
+        inj_rows: usize,
+        h_inj_offsets: *const u32,
+        h_inj_values: *const u32,
+        preflight: *const c_void,
+        h_bigint: *const R0HipBigIntBack,
+        n_bigint: usize,
+        h_seal: *mut u32,
+        seal_cap: usize,
+        seal_len: *mut usize,
+        h_mix_out: *mut u32,
+    ) -> *const c_char;
     /// risc0_circuit_recursion_cuda_witgen's role (recursion-sys ffi.cpp:191-205)
     pub fn r0hip_recursion_witgen(
         d_ctrl: *const u32,

@@ -335,6 +335,46 @@ def prove_segment(name, suite, po2, code, data, accum, glob, version=None):
     return seal[: n.value].copy(), mix, glob
 
 
+ACCUM_CB = C.CFUNCTYPE(C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_void_p)
+
+
+def prove_segment_cb(name, suite, po2, code, data, glob, fill_accum, accum_words, version=None):
+    """oracle_prove_segment_cb: the prover with the accum group filled by
+    fill_accum(mix) -> accum (numpy uint32, accum_words) once the mix is drawn, as prove_core
+    runs WitnessGenerator::accum between the data commit and the accum commit."""
+    c, keep, d = make_circuit(name)
+    glob = glob.copy()
+    cap = 1 << 24
+    seal = np.zeros(cap, np.uint32)
+    n = C.c_size_t(0)
+    mix = np.zeros(d["mix_size"], np.uint32)
+    accum = np.zeros(accum_words, np.uint32)
+    err = []
+
+    def cb(mix_p, acc_p, _ctx):
+        try:
+            m = np.ctypeslib.as_array(mix_p, shape=(d["mix_size"],)).copy()
+            a = np.ascontiguousarray(fill_accum(m), dtype=np.uint32)
+            assert a.size == accum_words
+            np.ctypeslib.as_array(acc_p, shape=(accum_words,))[:] = a
+            return None
+        except Exception as e:  # reported through the prover's error (the buffer outlives the call)
+            err.append(e)
+            msg = C.create_string_buffer(str(e).encode())
+            err.append(msg)
+            return C.cast(msg, C.c_void_p).value
+
+    fcb = ACCUM_CB(cb)
+    f = lib().oracle_prove_segment_cb
+    f.restype = C.c_void_p
+    e = f(C.byref(c), C.c_int(suite), C.c_uint32(po2), ptr(code), ptr(data), ptr(accum), fcb, None, ptr(glob),
+          C.c_int(version is not None), C.c_uint32(version or 0), ptr(seal), sz(cap), C.byref(n), ptr(mix))
+    if err:
+        raise err[0]
+    _check(e)
+    return seal[: n.value].copy(), mix, glob, accum
+
+
 def num_threads():
     return lib().oracle_num_threads()
 

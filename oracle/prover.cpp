@@ -560,11 +560,15 @@ extern "C" const char* oracle_eval_check_sampled(const oracle_circuit_t* c, cons
   return nullptr;
 }
 
-extern "C" const char* oracle_prove_segment(const oracle_circuit_t* c, int suite, uint32_t po2,
-                                            const uint32_t* code, const uint32_t* data,
-                                            const uint32_t* accum, uint32_t* global,
-                                            int write_version, uint32_t version, uint32_t* seal,
-                                            size_t seal_cap, size_t* seal_len, uint32_t* mix_out) {
+// The witness generator's accumulation between the mix draw and the accum commit
+// (WitnessGenerator::accum, circuit/rv32im/src/prove/witgen/mod.rs:178-223): fills `accum`
+// from the drawn mix; returns NULL or a message.
+typedef const char* (*oracle_accum_cb)(const uint32_t* mix, uint32_t* accum, void* ctx);
+
+static const char* prove_segment_impl(const oracle_circuit_t* c, int suite, uint32_t po2, const uint32_t* code,
+                                      const uint32_t* data, uint32_t* accum, oracle_accum_cb cb, void* cb_ctx,
+                                      uint32_t* global, int write_version, uint32_t version, uint32_t* seal,
+                                      size_t seal_cap, size_t* seal_len, uint32_t* mix_out) {
   try {
     Prover p(c, suite);
     if (write_version) p.iop.proof.push_back(version);
@@ -592,6 +596,9 @@ extern "C" const char* oracle_prove_segment(const oracle_circuit_t* c, int suite
     std::vector<uint32_t> mix(c->mix_size);
     for (size_t i = 0; i < c->mix_size; i++) mix[i] = p.iop.rng->random_elem().v;
     if (mix_out) memcpy(mix_out, mix.data(), mix.size() * 4);
+    if (cb) {
+      if (const char* e = cb(mix.data(), accum, cb_ctx)) throw std::runtime_error(std::string("accumulation: ") + e);
+    }
     p.commit_group(0, accum);
     p.finalize(mix.data(), global);
     if (seal_len) *seal_len = p.iop.proof.size();
@@ -601,4 +608,23 @@ extern "C" const char* oracle_prove_segment(const oracle_circuit_t* c, int suite
     return strdup(e.what());
   }
   return nullptr;
+}
+
+extern "C" const char* oracle_prove_segment(const oracle_circuit_t* c, int suite, uint32_t po2,
+                                            const uint32_t* code, const uint32_t* data,
+                                            const uint32_t* accum, uint32_t* global,
+                                            int write_version, uint32_t version, uint32_t* seal,
+                                            size_t seal_cap, size_t* seal_len, uint32_t* mix_out) {
+  return prove_segment_impl(c, suite, po2, code, data, const_cast<uint32_t*>(accum), nullptr, nullptr, global,
+                            write_version, version, seal, seal_cap, seal_len, mix_out);
+}
+
+// the same with the accum group filled by `cb` once the mix is drawn (prove_core's order)
+extern "C" const char* oracle_prove_segment_cb(const oracle_circuit_t* c, int suite, uint32_t po2,
+                                               const uint32_t* code, const uint32_t* data, uint32_t* accum,
+                                               oracle_accum_cb cb, void* cb_ctx, uint32_t* global,
+                                               int write_version, uint32_t version, uint32_t* seal,
+                                               size_t seal_cap, size_t* seal_len, uint32_t* mix_out) {
+  return prove_segment_impl(c, suite, po2, code, data, accum, cb, cb_ctx, global, write_version, version, seal,
+                            seal_cap, seal_len, mix_out);
 }

@@ -105,6 +105,10 @@ enum ScratchSlot : int {
   kSlotRvwgBigint = 77,
   kSlotRvwgLists = 78,
   kSlotRvwgTables = 79,
+  // r0hip_prove_segment_trace (api.cpp): the injector's index, offsets and values
+  kSlotRvInjIndex = 80,
+  kSlotRvInjOffsets = 81,
+  kSlotRvInjValues = 82,
 };
 
 // Scratch buffer reused across calls (grown on demand; stream-ordered use only).

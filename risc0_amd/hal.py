@@ -90,6 +90,8 @@ def _declare(L):
         "r0hip_rv32im_bigint_accum_states": [u32p, vp, sz, sz, u32p],
         "r0hip_recursion_witgen": [vp, vp, vp, sz, u32p, sz, u32p, sz, u32p, sz],
         "r0hip_rv32im_witgen": [C.c_uint32, vp, vp, C.c_uint32],
+        "r0hip_prove_segment_trace": [C.c_int, C.c_uint32, C.c_uint32, u32p, u32p, sz, u32p, u32p, vp, vp, sz, u32p,
+                                      sz, C.POINTER(sz), u32p],
         "r0hip_prove_recursion": [C.c_int, C.c_uint32, vp, u32p, sz, u32p, sz, u32p, sz, C.c_uint64, u32p, sz,
                                   C.POINTER(sz), u32p],
         "r0hip_rv32im_bigint_accum_inject": [vp, sz, u32p, vp, sz],
@@ -479,6 +481,31 @@ def rv32im_witgen(data, glob, cycles, txns, table_split, bigint=None, mode=0):
     pf = RawPreflightTrace(cyc.ctypes.data, tx.ctypes.data if tx.nbytes else None, bi.ctypes.data if bi.size else None,
                            tx.nbytes // 20, bi.size, table_split)
     check(lib().r0hip_rv32im_witgen(mode, C.byref(bufs), C.byref(pf), rows))
+
+
+def prove_segment_trace(hal, po2, glob, inj_index, inj_offsets, inj_values, cycles, txns, table_split, bigint=None,
+                        bigint_records=None, mode=0, seal_cap=1 << 24):
+    """r0hip_prove_segment_trace: rv32im prove_core from a preflight trace on the device
+    (injector scatter, stepExec, zeroize, accumulation, prove). glob: build_global_vec's 90
+    Montgomery words (INVALID where unset); the injector as index / offsets / Montgomery
+    values. Returns (seal, mix)."""
+    u = lambda a: np.ascontiguousarray(a, dtype=np.uint32)
+    g, ix, off, val = u(glob), u(inj_index), u(inj_offsets), u(inj_values)
+    cyc, tx = np.ascontiguousarray(cycles), np.ascontiguousarray(txns)
+    bi = np.ascontiguousarray(bigint if bigint is not None else np.zeros(0, np.uint8), dtype=np.uint8)
+    pf = RawPreflightTrace(cyc.ctypes.data, tx.ctypes.data if tx.nbytes else None, bi.ctypes.data if bi.size else None,
+                           tx.nbytes // 20, bi.size, table_split)
+    backs = bigint_backs(bigint_records)
+    nb = 0 if backs is None else len(backs)
+    backs = None if backs is None else C.cast(backs, C.c_void_p)
+    seal = np.zeros(seal_cap, dtype=np.uint32)
+    n = C.c_size_t(0)
+    mix = np.zeros(36, dtype=np.uint32)
+    check(lib().r0hip_prove_segment_trace(hal.suite, po2, mode, g.ctypes.data_as(u32p), ix.ctypes.data_as(u32p),
+                                          ix.size - 1, off.ctypes.data_as(u32p), val.ctypes.data_as(u32p), C.byref(pf),
+                                          backs, nb, seal.ctypes.data_as(u32p), seal_cap, C.byref(n),
+                                          mix.ctypes.data_as(u32p)))
+    return seal[: n.value].copy(), mix
 
 
 class SegmentJob(C.Structure):

@@ -860,3 +860,23 @@ def random_trace(po2, n_insns, seed=1):
     data = {0x00100000 + 4 * i: int(rng.integers(0, 1 << 32)) for i in range(256)}
     regs = {r: int(rng.integers(0, 1 << 32)) for r in range(1, 31)}
     return Trace(po2, prog, data=data, regs=regs, seed=seed)
+
+
+def loop_program(rng, body_len, data_base=0x00100000, data_words=256):
+    """a loop guest: x31 = data base, then a body of body_len random straight-line
+    instructions (every kind random_program draws, forward branches inside the body) and a
+    backward jal to its start. The segment ends where the executor suspends it (the
+    preflight body's suspend_cycle, preflight.rs:170-185)."""
+    body = random_program(rng, body_len + 1, data_base, data_words)[1:]
+    return [asm("lui", 31, data_base >> 12)] + body + [asm("jal", 0, -4 * body_len)]
+
+
+def loop_trace(po2, body_len=32, seed=1, reserve=4096):
+    """a segment of 2^po2 rows filled with loop iterations: the user cycles stop `reserve`
+    rows short of the lookup tables, leaving room for paging in and out"""
+    rng = np.random.default_rng(seed)
+    prog = loop_program(rng, body_len)
+    data = {0x00100000 + 4 * i: int(rng.integers(0, 1 << 32)) for i in range(256)}
+    regs = {r: int(rng.integers(0, 1 << 32)) for r in range(1, 31)}
+    budget = (1 << po2) - RESERVED_CYCLES - reserve
+    return Trace(po2, prog, data=data, regs=regs, seed=seed, max_user_cycles=budget)

@@ -49,6 +49,44 @@ def inputs(trace, lay=None):
     return data, glob, cyc, tx
 
 
+def global_words(trace, lay=None):
+    """build_global_vec as Montgomery words (INVALID where unset)"""
+    g = trace.global_values(lay or layout())
+    return np.array([INVALID if x is None else int(encode(x)) for x in g], np.uint32)
+
+
+def injector_arrays(trace, lay=None):
+    """the Injector (witgen/mod.rs:329-378) as hal.scatter takes it: index (rows + 1), offsets
+    (col * rows + row), Montgomery values"""
+    rows = 1 << trace.po2
+    r, c, v = trace.injector(lay or layout())
+    index = np.zeros(rows + 1, np.uint32)
+    np.add.at(index, r.astype(np.int64) + 1, 1)
+    index = np.cumsum(index).astype(np.uint32)
+    assert np.all(np.diff(r.astype(np.int64)) >= 0)  # pushed row by row
+    return index, (c.astype(np.uint64) * rows + r).astype(np.uint32), encode(v)
+
+
+def prove_from_trace(trace, suite, oracle, mode=MODE_SEQ_FORWARD):
+    """the reference's prove_core from a preflight on the CPU (SegmentProverImpl::prove_core,
+    prove/hal/mod.rs:143-224): the compiled reference witgen, zeroize, the oracle prover with
+    the compiled reference accumulation run on the drawn mix (oracle_prove_segment_cb), INVALID
+    accum words zeroized. Returns (seal, mix, data, global, accum)."""
+    rows = 1 << trace.po2
+    data, glob, cyc, tx = inputs(trace)
+    d, g = run(data, glob, cyc, tx, trace.table_split_cycle, rows, mode)
+    d = np.where(d == INVALID, 0, d).astype(np.uint32)
+    g = np.where(g == INVALID, 0, g).astype(np.uint32)
+    code = np.zeros(rows, np.uint32)
+
+    def fill(mix):
+        acc = RA.accum(d, g, mix, rows, rows)
+        return np.where(acc == INVALID, 0, acc).astype(np.uint32)
+    seal, mix, _, acc = oracle.prove_segment_cb("rv32im", suite, trace.po2, code, d, g, fill, RA.ACCUM_COLS * rows,
+                                                version=2)
+    return seal, mix, d, g, acc
+
+
 def witgen(trace, mode=MODE_SEQ_FORWARD, lay=None):
     """(data, global) after the reference's witness generation; raises RuntimeError with the
     reference's message when it throws"""

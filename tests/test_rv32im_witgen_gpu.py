@@ -74,3 +74,35 @@ def test_rv32im_witgen_failures(hal):
     ref = W.run(data, glob, cyc, tx, t.table_split_cycle, rows)
     d, g = gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle)
     assert np.array_equal(d, ref[0]) and np.array_equal(g, ref[1])
+
+
+@pytest.mark.parametrize("po2,n,suite,seed", [(13, 250, "poseidon2", 21), (14, 2500, "poseidon2", 3),
+                                              (14, 2000, "sha-256", 8)])
+def test_prove_segment_trace_matches_oracle(po2, n, suite, seed, oracle):
+    """r0hip_prove_segment_trace (injector scatter, stepExec, zeroize, accumulation and the
+    prove core on the device, rv32im prove/hal/mod.rs:143-224) gives the seal and mix of the
+    CPU path: the compiled reference witgen and accumulation around the oracle prover. The
+    rows satisfy the circuit, so the seal verifies with the validity equation."""
+    import risc0_amd as r
+    h = r.HipHal(suite)
+    t = T.random_trace(po2, n, seed=seed)
+    s = {"poseidon2": oracle.POSEIDON2, "sha-256": oracle.SHA256}[suite]
+    ref_seal, ref_mix, _, _, _ = W.prove_from_trace(t, s, oracle)
+    cyc, tx = t.arrays()
+    idx, off, val = W.injector_arrays(t)
+    seal, mix = r.prove_segment_trace(h, po2, W.global_words(t), idx, off, val, cyc, tx, t.table_split_cycle)
+    assert np.array_equal(mix, ref_mix)
+    assert seal.size == ref_seal.size and np.array_equal(seal, ref_seal)
+    assert r.verify_seal("rv32im", h.suite, seal, check_validity=True) == po2
+
+
+def test_prove_segment_trace_full_size_verifies(hal):
+    """BASELINE configs[1] shape from a trace: a po2=20 segment of a random program proved from
+    its preflight on the device; its seal passes the native verifier with the validity
+    equation (the CPU path would take minutes at this size)"""
+    import risc0_amd as r
+    t = T.random_trace(20, 60000, seed=5)
+    cyc, tx = t.arrays()
+    idx, off, val = W.injector_arrays(t)
+    seal, mix = r.prove_segment_trace(hal, 20, W.global_words(t), idx, off, val, cyc, tx, t.table_split_cycle)
+    assert r.verify_seal("rv32im", hal.suite, seal, check_validity=True) == 20

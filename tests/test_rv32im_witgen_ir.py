@@ -82,3 +82,24 @@ def test_failures_match_reference():
     lay = W.layout()
     d2[lay["next_pc_low"] * rows + 500] = W.encode(12345)
     _fails_both(d2, glob, cyc, tx, t.table_split_cycle, rows, "Inconsistent set")
+
+
+@needs_ref
+def test_trace_seal_verifies_with_validity(oracle):
+    """prove_core from a restated preflight on the CPU (the compiled reference witgen and
+    accumulation around the oracle prover): the rows satisfy every rv32im constraint, so the
+    seal passes the native verifier WITH the validity equation (verify/mod.rs:340-394); one
+    flipped data word after witgen makes it fail there"""
+    import risc0_amd as r
+    t = T.random_trace(13, 250, seed=21)
+    seal, mix, d, g, acc = W.prove_from_trace(t, oracle.POSEIDON2, oracle)
+    assert r.verify_seal("rv32im", r.POSEIDON2, seal, check_validity=True) == 13
+    rows = 1 << 13
+    d2 = d.copy()
+    row = next(i for i in range(rows) if t.cycles[i][0] == T.DECODE)
+    d2[W.layout()["cycle"] * rows + row] = W.encode(row + 1)  # the cycle counter of a user row
+    code = np.zeros(rows, np.uint32)
+    bad, _, _ = oracle.prove_segment("rv32im", oracle.POSEIDON2, 13, code, d2, acc, g, version=2)
+    with pytest.raises(r.R0HipError):
+        r.verify_seal("rv32im", r.POSEIDON2, bad, check_validity=True)
+    assert r.verify_seal("rv32im", r.POSEIDON2, bad, check_validity=False) == 13
