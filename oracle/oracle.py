@@ -335,6 +335,16 @@ def prove_segment(name, suite, po2, code, data, accum, glob, version=None):
     return seal[: n.value].copy(), mix, glob
 
 
+def poly_fp_at_taps(name, tap_values, mix, glob, poly_mix):
+    """the reference's compiled poly_fp at a cycle whose taps read tap_values (one base-field
+    Montgomery word per tap, tap order): the mixed constraint sum, 4 words"""
+    c, keep, _ = make_circuit(name)
+    out = np.zeros(4, np.uint32)
+    _check(lib().oracle_poly_fp_at_taps(C.byref(c), ptr(np.ascontiguousarray(tap_values, np.uint32)), ptr(mix),
+                                        ptr(glob), ptr(np.ascontiguousarray(poly_mix, np.uint32)), ptr(out)))
+    return out
+
+
 ACCUM_CB = C.CFUNCTYPE(C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_void_p)
 
 

@@ -560,6 +560,40 @@ extern "C" const char* oracle_eval_check_sampled(const oracle_circuit_t* c, cons
   return nullptr;
 }
 
+// The reference's compiled poly_fp at one cycle whose taps read given base-field values
+// (test infrastructure: pins the verifier's poly_ext to the reference's constraint code).
+// poly_fp reads a tap only as args[col*steps + ((cycle - 4*back) & (steps-1))], so a small
+// window domain per group holds tap i's value at its (col, back) position.
+extern "C" const char* oracle_poly_fp_at_taps(const oracle_circuit_t* c, const uint32_t* tap_values,
+                                              const uint32_t* mix, const uint32_t* global,
+                                              const uint32_t* poly_mix, uint32_t* out) {
+  try {
+    if (!c->poly_fp) throw std::runtime_error("circuit has no poly_fp (oracle/_ref not built?)");
+    TapSet taps{c};
+    uint32_t max_back = 0;
+    for (size_t i = 0; i < c->n_taps; i++) max_back = std::max(max_back, taps.tap(i)->back);
+    size_t win = 1;
+    while (win < INV_RATE * (max_back + 2)) win <<= 1;
+    const size_t local = INV_RATE * (max_back + 1);
+    std::vector<Buf> w(c->n_groups);
+    for (size_t g = 0; g < c->n_groups; g++) w[g].assign(taps.group_size(g) * win, 0);
+    for (size_t i = 0; i < c->n_taps; i++) {
+      const Tap* t = taps.tap(i);
+      w[t->group][t->offset * win + ((local - INV_RATE * t->back) & (win - 1))] = tap_values[i];
+    }
+    std::vector<const uint32_t*> args(c->n_eval_args);
+    for (size_t i = 0; i < c->n_eval_args; i++) {
+      int a = c->eval_args[i];
+      args[i] = a >= 0 ? w[a].data() : (a == -1 ? mix : global);
+    }
+    std::vector<ExtElem> pows = map_pow(ExtElem::raw(poly_mix), c->poly_mix_powers, c->n_poly_mix);
+    if (const char* err = c->poly_fp(local, win, &pows[0].e[0].v, args.data(), out)) return err;
+  } catch (const std::exception& e) {
+    return strdup(e.what());
+  }
+  return nullptr;
+}
+
 // The witness generator's accumulation between the mix draw and the accum commit
 // (WitnessGenerator::accum, circuit/rv32im/src/prove/witgen/mod.rs:178-223): fills `accum`
 // from the drawn mix; returns NULL or a message.

@@ -92,6 +92,32 @@ def test_native_poly_ext_matches_restatement(oracle, circuit):
         assert got == want
 
 
+@pytest.mark.parametrize("circuit", ["rv32im", "recursion"])
+def test_native_poly_ext_matches_compiled_poly_fp(oracle, circuit):
+    """r0hip_poly_ext against the reference's own compiled constraint code: on 1000 random
+    base-field tap assignments, the validity polynomial the verifier evaluates over FpExt
+    (each tap embedded as (u, 0, 0, 0)) equals the reference's risc0_circuit_<c>_cpu_poly_fp
+    (rv32im-sys/kernels/cxx/eval_check.cpp:31-39, recursion-sys poly_fp.cpp) at a cycle whose
+    taps read those values (oracle_poly_fp_at_taps), with a random FpExt poly_mix, mix and
+    globals. For rv32im this is the reference-code pin of the constraint program (its
+    poly_ext.rs is not in the reference tree)."""
+    import risc0_amd as r
+    _native_lib_or_skip(oracle)
+    taps = verifier.Taps(circuit)
+    d = taps.d
+    rng = np.random.default_rng(0x50465450)
+    for _ in range(1000):
+        u = oracle.rand_elems(rng, taps.num_taps)
+        mix = oracle.rand_elems(rng, d["mix_size"])
+        glob = oracle.rand_elems(rng, d["output_size"])
+        pm = oracle.rand_elems(rng, 4)
+        eval_u = np.zeros(4 * taps.num_taps, np.uint32)
+        eval_u[0::4] = u
+        got = r.poly_ext(circuit, mix, glob, eval_u, pm)
+        want = oracle.poly_fp_at_taps(circuit, u, mix, glob, pm)
+        assert np.array_equal(got, want), (got, want)
+
+
 def _poly_ext_golden_inputs(oracle, n):
     import poly_ext_def as D
     d = oracle.load_circuit_json("recursion")
