@@ -233,6 +233,17 @@ const char* r0hip_prove_segment_trace(int suite, uint32_t po2, uint32_t mode, co
                                       const r0hip_bigint_back* h_bigint, size_t n_bigint, uint32_t* h_seal,
                                       size_t seal_cap, size_t* seal_len, uint32_t* h_mix_out);
 
+/* The same with every input already resident in device memory (the global vector, the
+ * injector arrays, and d_preflight's cycles / txns / bigint_bytes are DEVICE pointers; the
+ * struct itself and h_bigint are on the host): what the benchmark times, inputs in HBM.
+ * Injector offsets outside the data group are skipped. */
+const char* r0hip_prove_segment_trace_resident(int suite, uint32_t po2, uint32_t mode, const uint32_t* d_global,
+                                               const uint32_t* d_inj_index, size_t inj_rows,
+                                               const uint32_t* d_inj_offsets, const uint32_t* d_inj_values,
+                                               const r0hip_raw_preflight_trace* d_preflight,
+                                               const r0hip_bigint_back* h_bigint, size_t n_bigint, uint32_t* h_seal,
+                                               size_t seal_cap, size_t* seal_len, uint32_t* h_mix_out);
+
 /* ---- recursion witness side: the accumulation step (risc0_circuit_recursion_cuda_accum,
  * recursion-sys/kernels/cuda/ffi.cu; CPU driver recursion-sys/kernels/cxx/ffi.cpp:160-217,
  * called from circuit/recursion/src/prove/witgen.rs:162-170): for cycles [0, work_cycles) the

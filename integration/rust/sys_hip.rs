@@ -259,6 +259,24 @@ unsafe extern "C" {
         seal_len: *mut usize,
         h_mix_out: *mut u32,
     ) -> *const c_char;
+    /// r0hip_prove_segment_trace with every input resident on the device
+    pub fn r0hip_prove_segment_trace_resident(
+        suite: c_int,
+        po2: u32,
+        mode: u32,
+        d_global: *const u32,
+        d_inj_index: *const u32,
+        inj_rows: usize,
+        d_inj_offsets: *const u32,
+        d_inj_values: *const u32,
+        d_preflight: *const c_void,
+        h_bigint: *const R0HipBigIntBack,
+        n_bigint: usize,
+        h_seal: *mut u32,
+        seal_cap: usize,
+        seal_len: *mut usize,
+        h_mix_out: *mut u32,
+    ) -> *const c_char;
     /// risc0_circuit_recursion_cuda_witgen's role (recursion-sys ffi.cpp:191-205)
     pub fn r0hip_recursion_witgen(
         d_ctrl: *const u32,

@@ -301,62 +301,101 @@ const char* r0hip_rv32im_witgen(uint32_t mode, const r0hip_raw_exec_buffers* buf
   });
 }
 
+namespace {
+
+// SegmentProverImpl::prove_core from a preflight (circuit/rv32im/src/prove/hal/mod.rs:143-224):
+// WitnessGenerator::hal_generate_witness (witgen/mod.rs:135-176: globals, code and data
+// INVALID, the injector scattered into data, stepExec, zeroize), then the prove core with the
+// version word 2 and WitnessGenerator::accum on the device. `resident`: the global vector,
+// the injector and the preflight arrays are device pointers; otherwise host pointers.
+std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const uint32_t* global_in,
+                                  const uint32_t* inj_index, size_t inj_rows, const uint32_t* inj_offsets,
+                                  const uint32_t* inj_values, const r0hip_raw_preflight_trace* pf,
+                                  const r0hip_bigint_back* h_bigint, size_t n_bigint, bool resident,
+                                  std::vector<uint32_t>* mix) {
+  const CircuitDef* c = find_circuit("rv32im");
+  R0_REQUIRE(global_in && inj_index && pf && pf->cycles, "r0hip_prove_segment_trace: null argument");
+  R0_REQUIRE(po2 >= 2 && po2 <= 24, "r0hip_prove_segment_trace: po2 out of range");
+  R0_REQUIRE(n_bigint == 0 || h_bigint, "r0hip_prove_segment_trace: h_bigint is NULL with n_bigint > 0");
+  const size_t n = size_t(1) << po2;
+  R0_REQUIRE(inj_rows <= n, "r0hip_prove_segment_trace: injector longer than the segment");
+  const size_t data_cols = c->group_size(2);
+  hipStream_t s = stream();
+  stage_reset();
+  Span span("prove_segment_trace");
+  DevBuf code(c->group_size(1) * n), data(data_cols * n), global(c->output_size), accum(c->group_size(0) * n);
+  HIP_OK(hipMemsetD32Async(code.p, 0u, code.words, s));  // INVALID, zeroized: nothing writes code
+  HIP_OK(hipMemsetD32Async(data.p, 0xFFFFFFFFu, data.words, s));
+  if (resident) {
+    HIP_OK(hipMemcpyAsync(global.p, global_in, global.words * 4, hipMemcpyDeviceToDevice, s));
+    scatter(s, data.p, inj_index, inj_offsets, inj_values, inj_rows, data.words);
+    Span w("witgen");
+    rv32im_witgen_dev(s, mode, data.p, global.p, n, static_cast<const rvwg::PreflightCycle*>(pf->cycles),
+                      static_cast<const rvwg::MemoryTxn*>(pf->txns), pf->txns_len, pf->bigint_bytes,
+                      pf->bigint_bytes_len, pf->table_split_cycle, uint32_t(n));
+  } else {
+    const size_t n_inj = inj_index[inj_rows];
+    R0_REQUIRE(n_inj == 0 || (inj_offsets && inj_values), "r0hip_prove_segment_trace: null injector arrays");
+    for (size_t i = 0; i < n_inj; i++)
+      R0_REQUIRE(inj_offsets[i] < data_cols * n, "r0hip_prove_segment_trace: injector offset outside the data group");
+    upload_async(global.p, global_in, global.words * 4);
+    if (n_inj) {
+      auto* idx = static_cast<uint32_t*>(scratch((inj_rows + 1) * 4, kSlotRvInjIndex));
+      auto* off = static_cast<uint32_t*>(scratch(n_inj * 4, kSlotRvInjOffsets));
+      auto* val = static_cast<uint32_t*>(scratch(n_inj * 4, kSlotRvInjValues));
+      upload_async(idx, inj_index, (inj_rows + 1) * 4);
+      upload_async(off, inj_offsets, n_inj * 4);
+      upload_async(val, inj_values, n_inj * 4);
+      scatter(s, data.p, idx, off, val, inj_rows);
+    }
+    Span w("witgen");
+    rv32im_witgen(s, mode, data.p, global.p, n, static_cast<const rvwg::PreflightCycle*>(pf->cycles),
+                  static_cast<const rvwg::MemoryTxn*>(pf->txns), pf->txns_len, pf->bigint_bytes, pf->bigint_bytes_len,
+                  pf->table_split_cycle, uint32_t(n));
+  }
+  eltwise_zeroize(s, global.p, global.words);
+  eltwise_zeroize(s, data.p, data.words);
+  HIP_OK(hipMemsetD32Async(accum.p, 0xFFFFFFFFu, accum.words, s));
+  const AccumStep acc{accum.p, n, false, h_bigint, n_bigint};
+  return prove_segment(*c, suite, po2, code.p, data.p, nullptr, global.p, true, 2, mix, nullptr, &acc);
+}
+
+void seal_out(const std::vector<uint32_t>& seal, const std::vector<uint32_t>& mix, uint32_t* h_seal, size_t seal_cap,
+              size_t* seal_len, uint32_t* h_mix_out) {
+  if (seal_len) *seal_len = seal.size();
+  if (h_mix_out) memcpy(h_mix_out, mix.data(), mix.size() * 4);
+  if (h_seal) {
+    R0_REQUIRE(seal.size() <= seal_cap, "seal buffer too small");
+    memcpy(h_seal, seal.data(), seal.size() * 4);
+  }
+}
+
+}  // namespace
+
 const char* r0hip_prove_segment_trace(int suite, uint32_t po2, uint32_t mode, const uint32_t* h_global,
                                       const uint32_t* h_inj_index, size_t inj_rows, const uint32_t* h_inj_offsets,
                                       const uint32_t* h_inj_values, const r0hip_raw_preflight_trace* preflight,
                                       const r0hip_bigint_back* h_bigint, size_t n_bigint, uint32_t* h_seal,
                                       size_t seal_cap, size_t* seal_len, uint32_t* h_mix_out) {
   return wrap([&] {
-    const CircuitDef* c = find_circuit("rv32im");
-    R0_REQUIRE(h_global && h_inj_index && preflight && preflight->cycles, "r0hip_prove_segment_trace: null argument");
-    R0_REQUIRE(po2 >= 2 && po2 <= 24, "r0hip_prove_segment_trace: po2 out of range");
-    R0_REQUIRE(n_bigint == 0 || h_bigint, "r0hip_prove_segment_trace: h_bigint is NULL with n_bigint > 0");
-    const size_t n = size_t(1) << po2;
-    R0_REQUIRE(inj_rows <= n, "r0hip_prove_segment_trace: injector longer than the segment");
-    const size_t n_inj = h_inj_index[inj_rows];
-    R0_REQUIRE(n_inj == 0 || (h_inj_offsets && h_inj_values), "r0hip_prove_segment_trace: null injector arrays");
-    const size_t data_cols = c->group_size(2);
-    for (size_t i = 0; i < n_inj; i++)
-      R0_REQUIRE(h_inj_offsets[i] < data_cols * n, "r0hip_prove_segment_trace: injector offset outside the data group");
-    hipStream_t s = stream();
-    stage_reset();
-    Span span("prove_segment_trace");
-    // WitnessGenerator::hal_generate_witness (witgen/mod.rs:135-176): the globals, code and
-    // data groups (INVALID), the injector scattered into data, stepExec, zeroize
-    DevBuf code(c->group_size(1) * n), data(data_cols * n), global(c->output_size), accum(c->group_size(0) * n);
-    HIP_OK(hipMemsetD32Async(code.p, 0u, code.words, s));  // INVALID, zeroized: nothing writes code
-    HIP_OK(hipMemsetD32Async(data.p, 0xFFFFFFFFu, data.words, s));
-    upload_async(global.p, h_global, global.words * 4);
-    if (n_inj) {
-      auto* idx = static_cast<uint32_t*>(scratch((inj_rows + 1) * 4, kSlotRvInjIndex));
-      auto* off = static_cast<uint32_t*>(scratch(n_inj * 4, kSlotRvInjOffsets));
-      auto* val = static_cast<uint32_t*>(scratch(n_inj * 4, kSlotRvInjValues));
-      upload_async(idx, h_inj_index, (inj_rows + 1) * 4);
-      upload_async(off, h_inj_offsets, n_inj * 4);
-      upload_async(val, h_inj_values, n_inj * 4);
-      scatter(s, data.p, idx, off, val, inj_rows);
-    }
-    {
-      Span w("witgen");
-      rv32im_witgen(s, mode, data.p, global.p, n, static_cast<const rvwg::PreflightCycle*>(preflight->cycles),
-                    static_cast<const rvwg::MemoryTxn*>(preflight->txns), preflight->txns_len, preflight->bigint_bytes,
-                    preflight->bigint_bytes_len, preflight->table_split_cycle, uint32_t(n));
-    }
-    eltwise_zeroize(s, global.p, global.words);
-    eltwise_zeroize(s, data.p, data.words);
-    // prove_core (circuit/rv32im/src/prove/hal/mod.rs:143-224): version word 2, commit code and
-    // data, mix, WitnessGenerator::accum (BigInt states, step_accum, zeroize), commit accum,
-    // finalize
-    HIP_OK(hipMemsetD32Async(accum.p, 0xFFFFFFFFu, accum.words, s));
     std::vector<uint32_t> mix;
-    const AccumStep acc{accum.p, n, false, h_bigint, n_bigint};
-    std::vector<uint32_t> seal = prove_segment(*c, suite, po2, code.p, data.p, nullptr, global.p, true, 2, &mix, nullptr, &acc);
-    if (seal_len) *seal_len = seal.size();
-    if (h_mix_out) memcpy(h_mix_out, mix.data(), mix.size() * 4);
-    if (h_seal) {
-      R0_REQUIRE(seal.size() <= seal_cap, "seal buffer too small");
-      memcpy(h_seal, seal.data(), seal.size() * 4);
-    }
+    auto seal = prove_trace(suite, po2, mode, h_global, h_inj_index, inj_rows, h_inj_offsets, h_inj_values, preflight,
+                            h_bigint, n_bigint, false, &mix);
+    seal_out(seal, mix, h_seal, seal_cap, seal_len, h_mix_out);
+  });
+}
+
+const char* r0hip_prove_segment_trace_resident(int suite, uint32_t po2, uint32_t mode, const uint32_t* d_global,
+                                               const uint32_t* d_inj_index, size_t inj_rows,
+                                               const uint32_t* d_inj_offsets, const uint32_t* d_inj_values,
+                                               const r0hip_raw_preflight_trace* d_preflight,
+                                               const r0hip_bigint_back* h_bigint, size_t n_bigint, uint32_t* h_seal,
+                                               size_t seal_cap, size_t* seal_len, uint32_t* h_mix_out) {
+  return wrap([&] {
+    std::vector<uint32_t> mix;
+    auto seal = prove_trace(suite, po2, mode, d_global, d_inj_index, inj_rows, d_inj_offsets, d_inj_values,
+                            d_preflight, h_bigint, n_bigint, true, &mix);
+    seal_out(seal, mix, h_seal, seal_cap, seal_len, h_mix_out);
   });
 }
 

@@ -77,11 +77,14 @@ __global__ void gather_kernel(uint32_t* dst, const uint32_t* src, uint64_t idx, 
   if (g < size) dst[g] = src[g * stride + idx];
 }
 // cpu.rs:598-615: one lane per cycle walks its CSR slice
+// offsets at or past `limit` (the buffer's words) are skipped: a resident injector the host
+// has not checked cannot write outside the buffer
 __global__ void scatter_kernel(uint32_t* into, const uint32_t* index, const uint32_t* offsets,
-                               const uint32_t* values, uint64_t cycles) {
+                               const uint32_t* values, uint64_t cycles, uint64_t limit) {
   uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (c >= cycles) return;
-  for (uint32_t i = index[c]; i < index[c + 1]; i++) into[offsets[i]] = values[i];
+  for (uint32_t i = index[c]; i < index[c + 1]; i++)
+    if (offsets[i] < limit) into[offsets[i]] = values[i];
 }
 // cpu.rs:617-635
 __global__ void copy_slice_kernel(uint32_t* into, const uint32_t* from, uint64_t rows, uint64_t cols,
@@ -492,10 +495,10 @@ void gather_sample(hipStream_t s, uint32_t* dst, const uint32_t* src, size_t idx
   HIP_OK(hipGetLastError());
 }
 void scatter(hipStream_t s, uint32_t* into, const uint32_t* index, const uint32_t* offsets, const uint32_t* values,
-             size_t cycles) {
+             size_t cycles, uint64_t limit) {
   if (!cycles) return;
   hipLaunchKernelGGL(scatter_kernel, dim3(div_up(cycles, kThreads)), dim3(kThreads), 0, s, into, index, offsets,
-                     values, uint64_t(cycles));
+                     values, uint64_t(cycles), limit);
   HIP_OK(hipGetLastError());
 }
 void copy_elem_slice(hipStream_t s, uint32_t* into, const uint32_t* from, size_t rows, size_t cols,

@@ -264,7 +264,7 @@ void batch_evaluate_any_host(hipStream_t s, const uint32_t* coeffs, size_t poly_
                              bool bitrev = false);
 constexpr uint32_t kEvalBitrevMinLog = 12;
 void scatter(hipStream_t s, uint32_t* into, const uint32_t* index, const uint32_t* offsets,
-             const uint32_t* values, size_t cycles);
+             const uint32_t* values, size_t cycles, uint64_t limit = ~uint64_t(0));
 void copy_elem_slice(hipStream_t s, uint32_t* into, const uint32_t* from, size_t rows, size_t cols,
                      size_t from_offset, size_t from_stride, size_t into_offset, size_t into_stride);
 void prefix_products(hipStream_t s, uint32_t* io, size_t n);

@@ -211,8 +211,12 @@ __device__ __forceinline__ uint32_t bigint_byte(const Args& A, uint32_t cycle, u
 void rv32im_witgen_major(uint32_t major, hipStream_t s, const rvwg::Args& A, const uint32_t* cycles, uint32_t n);
 // EQZ messages of the generated code (steps.cpp locations), by index
 const char* rv32im_witgen_message(uint32_t k);
-// the driver (rv32im_witgen.hip): both phases over cycles [0, last_cycle); synchronises,
-// throws on a failed check
+// the driver (rv32im_witgen.hip): both phases over cycles [0, last_cycle) with the preflight
+// arrays resident on the device; synchronises, throws on a failed check
+void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
+                       const rvwg::PreflightCycle* d_cycles, const rvwg::MemoryTxn* d_txns, size_t n_txns,
+                       const uint8_t* d_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle);
+// the same from host preflight arrays (uploaded first), as RawPreflightTrace hands them over
 void rv32im_witgen(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
                    const rvwg::PreflightCycle* h_cycles, const rvwg::MemoryTxn* h_txns, size_t n_txns,
                    const uint8_t* h_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle);

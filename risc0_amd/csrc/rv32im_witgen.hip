@@ -15,9 +15,10 @@
 // modes give the same words on a trace it accepts (tests/test_rv32im_witgen_ir.py), so every
 // mode runs this schedule.
 //
-// The preflight trace comes from the host, as RawPreflightTrace does (host pointers). Checks
-// that throw in the reference record an error code and the cycle, raised after the kernels
-// drain.
+// The preflight trace comes from the host, as RawPreflightTrace does (host pointers), or is
+// already resident (rv32im_witgen_dev). The cycles are bucketed on the device (counts, one
+// 27-word read-back for the launch sizes, fill). Checks that throw in the reference record an
+// error code and the cycle, raised after the kernels drain.
 #include <string>
 #include <vector>
 
@@ -54,50 +55,58 @@ std::string witgen_error(const uint32_t* e) {
 
 }  // namespace
 
-void rv32im_witgen(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
-                   const rvwg::PreflightCycle* h_cycles, const rvwg::MemoryTxn* h_txns, size_t n_txns,
-                   const uint8_t* h_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle) {
+namespace {
+
+constexpr uint32_t kBins = 2 * rvwg::kMajors;  // (phase, major)
+constexpr uint32_t kBucketThreads = 256;
+
+// per (phase, instruction arm) cycle counts; a major outside the 13 arms is an error (the
+// reference's OneHot EQZ on majorOnehot fails for it)
+__global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(rvwg::Args A, uint32_t split, uint32_t* counts) {
+  __shared__ uint32_t h[kBins];
+  if (threadIdx.x < kBins) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t c = blockIdx.x * kBucketThreads + threadIdx.x;
+  if (c < A.ncycles) {
+    const uint32_t m = A.cycles[c].major;
+    if (m >= rvwg::kMajors)
+      rvwg::fail(A, rvwg::kErrMajor, c, m);
+    else
+      atomicAdd(&h[(c >= split) * rvwg::kMajors + m], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < kBins && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
+}
+
+// each cycle into its bucket (cursor = the bucket's next slot; the order within a bucket does
+// not matter: the cycles of a phase are independent)
+__global__ __launch_bounds__(kBucketThreads) void bucket_fill_kernel(rvwg::Args A, uint32_t split, uint32_t* cursor,
+                                                                    uint32_t* list) {
+  const uint32_t c = blockIdx.x * kBucketThreads + threadIdx.x;
+  if (c >= A.ncycles) return;
+  const uint32_t m = A.cycles[c].major;
+  if (m >= rvwg::kMajors) return;
+  list[atomicAdd(&cursor[(c >= split) * rvwg::kMajors + m], 1u)] = c;
+}
+
+}  // namespace
+
+void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
+                       const rvwg::PreflightCycle* d_cycles, const rvwg::MemoryTxn* d_txns, size_t n_txns,
+                       const uint8_t* d_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle) {
   using namespace rvwg;
   R0_REQUIRE(mode <= 2, "rv32im_witgen: mode must be 0 (parallel), 1 (forward) or 2 (reverse)");
   R0_REQUIRE(rows >= 4 && (rows & (rows - 1)) == 0 && rows <= (size_t(1) << 24),
              "rv32im_witgen: rows must be a power of two in [4, 2^24]");
   R0_REQUIRE(last_cycle <= rows && table_split <= last_cycle, "rv32im_witgen: need tableSplitCycle <= lastCycle <= rows");
-  R0_REQUIRE((last_cycle == 0 || h_cycles) && (n_txns == 0 || h_txns) && (n_bigint == 0 || h_bigint),
+  R0_REQUIRE((last_cycle == 0 || d_cycles) && (n_txns == 0 || d_txns) && (n_bigint == 0 || d_bigint),
              "rv32im_witgen: null trace array with a nonzero count");
   R0_REQUIRE(n_txns < (size_t(1) << 32) && n_bigint < (size_t(1) << 32), "rv32im_witgen: trace too long");
   if (last_cycle == 0) return;
-  // the two phases' cycles bucketed by instruction arm (counting sort on the preflight major)
-  std::vector<uint32_t> list(last_cycle);
-  uint32_t off[2][kMajors + 1] = {};
-  for (uint32_t c = 0; c < last_cycle; c++) {
-    const uint32_t m = h_cycles[c].major;
-    if (m >= kMajors) {
-      const uint32_t e[3] = {kErrMajor, c, m};
-      R0_REQUIRE(false, "rv32im witgen: " + witgen_error(e));
-    }
-    off[c >= table_split][m + 1]++;
-  }
-  for (int p = 0; p < 2; p++) {
-    off[p][0] = p ? table_split : 0;
-    for (uint32_t k = 0; k < kMajors; k++) off[p][k + 1] += off[p][k];
-  }
-  {
-    uint32_t pos[2][kMajors];
-    for (int p = 0; p < 2; p++)
-      for (uint32_t k = 0; k < kMajors; k++) pos[p][k] = off[p][k];
-    for (uint32_t c = 0; c < last_cycle; c++) list[pos[c >= table_split][h_cycles[c].major]++] = c;
-  }
-  auto* d_cycles = static_cast<PreflightCycle*>(scratch(size_t(last_cycle) * sizeof(PreflightCycle), kSlotRvwgCycles));
-  auto* d_txns = static_cast<MemoryTxn*>(scratch(n_txns * sizeof(MemoryTxn) + 16, kSlotRvwgTxns));
-  auto* d_bigint = static_cast<uint8_t*>(scratch(n_bigint + 16, kSlotRvwgBigint));
+  // lookup tables, error record, bucket counts and cursors in one scratch block
+  auto* tab = static_cast<uint32_t*>(scratch((256 + 65536 + 4 + 2 * kBins) * 4, kSlotRvwgTables));
   auto* d_list = static_cast<uint32_t*>(scratch(size_t(last_cycle) * 4, kSlotRvwgLists));
-  auto* d_tables = static_cast<uint32_t*>(scratch((256 + 65536 + 4) * 4, kSlotRvwgTables));
-  upload_async(d_cycles, h_cycles, size_t(last_cycle) * sizeof(PreflightCycle));
-  upload_async(d_txns, h_txns, n_txns * sizeof(MemoryTxn));
-  upload_async(d_bigint, h_bigint, n_bigint);
-  upload_async(d_list, list.data(), size_t(last_cycle) * 4);
-  HIP_OK(hipMemsetD32Async(d_tables, 0, 256 + 65536 + 4, s));
-
+  HIP_OK(hipMemsetD32Async(tab, 0, 256 + 65536 + 4 + 2 * kBins, s));
   Args A{};
   A.data = data;
   A.global = global;
@@ -108,19 +117,59 @@ void rv32im_witgen(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* globa
   A.n_txns = uint32_t(n_txns);
   A.bigint = d_bigint;
   A.n_bigint = uint32_t(n_bigint);
-  A.u8 = d_tables;
-  A.u16 = d_tables + 256;
-  A.err = d_tables + 256 + 65536;
+  A.u8 = tab;
+  A.u16 = tab + 256;
+  A.err = tab + 256 + 65536;
+  uint32_t* counts = A.err + 4;
+  uint32_t* cursor = counts + kBins;
+  const uint32_t g = (last_cycle + kBucketThreads - 1) / kBucketThreads;
+  // the two phases' cycles bucketed by instruction arm (count, host offsets, fill)
+  uint32_t h[4 + kBins];
+  {
+    KScope ks("rv32im_witgen_bucket", double(last_cycle) * 2 * sizeof(PreflightCycle));
+    hipLaunchKernelGGL(bucket_count_kernel, dim3(g), dim3(kBucketThreads), 0, s, A, table_split, counts);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(h, A.err, sizeof(h), hipMemcpyDeviceToHost, s));  // err[0..2], pad, counts
+    HIP_OK(hipStreamSynchronize(s));
+  }
+  R0_REQUIRE(h[0] == 0, "rv32im witgen: " + witgen_error(h));
+  const uint32_t* cnt = h + 4;  // counts start at A.err + 4
+  uint32_t off[kBins + 1];
+  off[0] = 0;
+  for (uint32_t b = 0; b < kBins; b++) off[b + 1] = off[b] + cnt[b];
+  R0_REQUIRE(off[kBins] == last_cycle, "rv32im witgen: bucket counts do not add up");
+  upload_async(cursor, off, kBins * 4);
+  hipLaunchKernelGGL(bucket_fill_kernel, dim3(g), dim3(kBucketThreads), 0, s, A, table_split, cursor, d_list);
+  HIP_OK(hipGetLastError());
   for (int p = 0; p < 2; p++) {
     KScope ks(p ? "rv32im_witgen_tables" : "rv32im_witgen_exec",
-              double(off[p][kMajors] - off[p][0]) * (4.0 * 211 + sizeof(PreflightCycle)));
-    for (uint32_t k = 0; k < kMajors; k++)
-      rv32im_witgen_major(k, s, A, d_list + off[p][k], off[p][k + 1] - off[p][k]);
+              double(off[(p + 1) * kMajors] - off[p * kMajors]) * (4.0 * 211 + sizeof(PreflightCycle)));
+    for (uint32_t k = 0; k < kMajors; k++) {
+      const uint32_t b = p * kMajors + k;
+      rv32im_witgen_major(k, s, A, d_list + off[b], off[b + 1] - off[b]);
+    }
   }
   uint32_t h_err[3] = {0, 0, 0};
   HIP_OK(hipMemcpyAsync(h_err, A.err, 12, hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
   R0_REQUIRE(h_err[0] == 0, "rv32im witgen: " + witgen_error(h_err));
+}
+
+void rv32im_witgen(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
+                   const rvwg::PreflightCycle* h_cycles, const rvwg::MemoryTxn* h_txns, size_t n_txns,
+                   const uint8_t* h_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle) {
+  using namespace rvwg;
+  R0_REQUIRE(last_cycle <= rows && last_cycle <= (size_t(1) << 24), "rv32im_witgen: more cycles than rows");
+  R0_REQUIRE((last_cycle == 0 || h_cycles) && (n_txns == 0 || h_txns) && (n_bigint == 0 || h_bigint),
+             "rv32im_witgen: null trace array with a nonzero count");
+  auto* d_cycles = static_cast<PreflightCycle*>(scratch(size_t(last_cycle) * sizeof(PreflightCycle) + 16, kSlotRvwgCycles));
+  auto* d_txns = static_cast<MemoryTxn*>(scratch(n_txns * sizeof(MemoryTxn) + 16, kSlotRvwgTxns));
+  auto* d_bigint = static_cast<uint8_t*>(scratch(n_bigint + 16, kSlotRvwgBigint));
+  upload_async(d_cycles, h_cycles, size_t(last_cycle) * sizeof(PreflightCycle));
+  upload_async(d_txns, h_txns, n_txns * sizeof(MemoryTxn));
+  upload_async(d_bigint, h_bigint, n_bigint);
+  rv32im_witgen_dev(s, mode, data, global, rows, d_cycles, n_txns ? d_txns : nullptr, n_txns,
+                    n_bigint ? d_bigint : nullptr, n_bigint, table_split, last_cycle);
 }
 
 }  // namespace r0

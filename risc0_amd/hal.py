@@ -90,6 +90,8 @@ def _declare(L):
         "r0hip_rv32im_bigint_accum_states": [u32p, vp, sz, sz, u32p],
         "r0hip_recursion_witgen": [vp, vp, vp, sz, u32p, sz, u32p, sz, u32p, sz],
         "r0hip_rv32im_witgen": [C.c_uint32, vp, vp, C.c_uint32],
+        "r0hip_prove_segment_trace_resident": [C.c_int, C.c_uint32, C.c_uint32, vp, vp, sz, vp, vp, vp, vp, sz,
+                                               u32p, sz, C.POINTER(sz), u32p],
         "r0hip_prove_segment_trace": [C.c_int, C.c_uint32, C.c_uint32, u32p, u32p, sz, u32p, u32p, vp, vp, sz, u32p,
                                       sz, C.POINTER(sz), u32p],
         "r0hip_prove_recursion": [C.c_int, C.c_uint32, vp, u32p, sz, u32p, sz, u32p, sz, C.c_uint64, u32p, sz,
@@ -505,6 +507,47 @@ def prove_segment_trace(hal, po2, glob, inj_index, inj_offsets, inj_values, cycl
                                           ix.size - 1, off.ctypes.data_as(u32p), val.ctypes.data_as(u32p), C.byref(pf),
                                           backs, nb, seal.ctypes.data_as(u32p), seal_cap, C.byref(n),
                                           mix.ctypes.data_as(u32p)))
+    return seal[: n.value].copy(), mix
+
+
+class ResidentTrace:
+    """a preflight trace, its injector and global vector uploaded once to device memory, for
+    r0hip_prove_segment_trace_resident (the benchmark's inputs-in-HBM form of
+    prove_segment_trace)"""
+
+    def __init__(self, hal, po2, glob, inj_index, inj_offsets, inj_values, cycles, txns, table_split, bigint=None):
+        u = lambda a: np.ascontiguousarray(a, dtype=np.uint32).reshape(-1)
+        self.po2 = po2
+        self.glob = hal.copy_from_elem("global", u(glob))
+        self.index = hal.copy_from_elem("inj_index", u(inj_index))
+        self.inj_rows = self.index.size - 1
+        n_inj = max(1, int(np.asarray(inj_index)[-1]))
+        self.offsets = hal.copy_from_elem("inj_offsets", u(inj_offsets) if len(inj_offsets) else np.zeros(n_inj, np.uint32))
+        self.values = hal.copy_from_elem("inj_values", u(inj_values) if len(inj_values) else np.zeros(n_inj, np.uint32))
+        cyc = np.ascontiguousarray(cycles).view(np.uint32).reshape(-1)
+        tx = np.ascontiguousarray(txns).view(np.uint32).reshape(-1)
+        self.cycles = hal.copy_from_elem("cycles", cyc)
+        self.txns = hal.copy_from_elem("txns", tx if tx.size else np.zeros(5, np.uint32))
+        bi = np.ascontiguousarray(bigint if bigint is not None else np.zeros(4, np.uint8), dtype=np.uint8)
+        pad = (-bi.size) % 4
+        self.bigint = hal.copy_from_elem("bigint", np.concatenate([bi, np.zeros(pad, np.uint8)]).view(np.uint32))
+        self.pf = RawPreflightTrace(self.cycles.ptr, self.txns.ptr if tx.size else None,
+                                    self.bigint.ptr if bigint is not None and len(bigint) else None, tx.size // 5,
+                                    0 if bigint is None else len(bigint), table_split)
+
+
+def prove_segment_trace_resident(hal, t, mode=0, bigint_records=None, seal_cap=1 << 24):
+    """r0hip_prove_segment_trace_resident over a ResidentTrace; returns (seal, mix)"""
+    backs = bigint_backs(bigint_records)
+    nb = 0 if backs is None else len(backs)
+    backs = None if backs is None else C.cast(backs, C.c_void_p)
+    seal = np.zeros(seal_cap, dtype=np.uint32)
+    n = C.c_size_t(0)
+    mix = np.zeros(36, dtype=np.uint32)
+    check(lib().r0hip_prove_segment_trace_resident(hal.suite, t.po2, mode, t.glob.ptr, t.index.ptr, t.inj_rows,
+                                                   t.offsets.ptr, t.values.ptr, C.byref(t.pf), backs, nb,
+                                                   seal.ctypes.data_as(u32p), seal_cap, C.byref(n),
+                                                   mix.ctypes.data_as(u32p)))
     return seal[: n.value].copy(), mix
 
 

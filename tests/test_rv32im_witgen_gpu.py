@@ -106,3 +106,29 @@ def test_prove_segment_trace_full_size_verifies(hal):
     idx, off, val = W.injector_arrays(t)
     seal, mix = r.prove_segment_trace(hal, 20, W.global_words(t), idx, off, val, cyc, tx, t.table_split_cycle)
     assert r.verify_seal("rv32im", hal.suite, seal, check_validity=True) == 20
+
+
+def test_prove_segment_trace_resident_matches_host_path(hal):
+    """the benchmark's form (global vector, injector and preflight already in device memory,
+    r0hip_prove_segment_trace_resident) proves the same seal as the host-pointer ABI, also with
+    two segments in flight on their own threads"""
+    import threading
+    import risc0_amd as r
+    t = T.loop_trace(14, body_len=24, seed=13)
+    cyc, tx = t.arrays()
+    idx, off, val = W.injector_arrays(t)
+    g = W.global_words(t)
+    seal, mix = r.prove_segment_trace(hal, 14, g, idx, off, val, cyc, tx, t.table_split_cycle)
+    rt = r.ResidentTrace(hal, 14, g, idx, off, val, cyc, tx, t.table_split_cycle)
+    out = [None, None]
+
+    def run(i):
+        out[i] = r.prove_segment_trace_resident(hal, rt)
+    ts = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for x in ts:
+        x.start()
+    for x in ts:
+        x.join()
+    for s2, m2 in out:
+        assert np.array_equal(s2, seal) and np.array_equal(m2, mix)
+    assert r.verify_seal("rv32im", hal.suite, seal, check_validity=True) == 14
