@@ -36,6 +36,9 @@ def parse():
     ap.add_argument("--circuit", default="rv32im")
     ap.add_argument("--hashfn", default="poseidon2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--witness", action="store_true",
+                    help="rv32im: time the prove core on a resident synthetic witness instead of the default "
+                         "trace -> witness generation -> accumulation -> seal unit")
     ap.add_argument("--e2e-steps", type=int, default=6,
                     help="segments of the end-to-end (pinned host witness -> H2D -> seal) leg; 0 = skip")
     ap.add_argument("--accum-steps", type=int, default=8,
@@ -106,48 +109,78 @@ def main():
         dg = hal.copy_from_elem("global", glob)
         host_witness = None
 
-    from risc0_amd.segments import segments_for_rank, timed_segments
-    # global segment ids of this rank (segment-per-GPU, no collective on the prove path);
-    # every segment of a rank proves the rank's resident witness
-    segs = segments_for_rank(rank, world, world * args.steps)
-    phase_tot = {}
-    last = {}
+    from risc0_amd.segments import segments_for_rank, timed_segments, gather_results
+    import hashlib
     import threading
+    # global segment ids of this rank (segment-per-GPU, no collective on the prove path);
+    # every segment of a rank proves the rank's resident inputs
+    segs = segments_for_rank(rank, world, world * args.steps)
     # segments in flight per GPU: small segments are latency-bound (6 at po2<=18 measured
-    # 5.32 -> 4.67 ms for recursion po2=18), po2=20 gains nothing past 2, po2>22 fits one
+    # 5.32 -> 4.67 ms for recursion po2=18), po2=20 gains nothing past 3, po2>22 fits one
     inflight = args.inflight if args.inflight is not None else (6 if args.po2 <= 18 else 3 if args.po2 <= 20 else 2 if args.po2 <= 22 else 1)
     k = max(1, min(inflight, len(segs) or 1))
     # per-thread globals buffer: prove_segment zeroizes it in place; the witness
     # groups are only read and are shared
     globs = [dg] + [hal.copy_from_elem("global", glob) for _ in range(k - 1)]
-    lock = threading.Lock()
+    trace_mode = args.circuit == "rv32im" and args.po2 <= 22 and not args.witness
 
-    def prove_on(slot, n):
-        for _ in range(n):
-            seal, mix = r.prove_segment(hal, args.circuit, args.po2, dc, dd, da, globs[slot], version=version)
-            prof = r.last_profile()
-            with lock:
-                last["seal"], last["mix"] = seal, mix
-                for key, v in prof.items():
-                    phase_tot[key] = phase_tot.get(key, 0.0) + v
+    def prove_witness(slot):
+        return r.prove_segment(hal, args.circuit, args.po2, dc, dd, da, globs[slot], version=version)
 
-    def prove_batch(batch):
-        # `batch` segments over k host threads (r0vm-style queue depth)
-        n = len(batch)
-        share = [n // k + (1 if i < n % k else 0) for i in range(k)]
-        ts = [threading.Thread(target=prove_on, args=(i, share[i])) for i in range(k) if share[i]]
-        for t_ in ts:
-            t_.start()
-        for t_ in ts:
-            t_.join()
+    rt = trace = None
+    if trace_mode:
+        # the headline unit is the reference's prove_core (prove/hal/mod.rs:143-224): a
+        # preflight trace -> witness generation -> accumulation -> seal. The trace (a loop
+        # guest, restated preflight: tests/rv32im_trace.py) is built and uploaded once, before
+        # the timed region.
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import rv32im_trace as T
+        import rv32im_witgen_ref as W
+        t0 = time.perf_counter()
+        trace = T.loop_trace(args.po2, body_len=32, seed=0x5249534330 + rank)
+        cyc, tx = trace.arrays()
+        idx, off, val = W.injector_arrays(trace)
+        rt = r.ResidentTrace(hal, args.po2, W.global_words(trace), idx, off, val, cyc, tx, trace.table_split_cycle)
+        print(f"rank {rank}: trace built in {time.perf_counter() - t0:.1f} s ({trace.table_split_cycle} rows before "
+              f"the tables, {len(tx)} memory transactions)", file=sys.stderr)
 
-    prove_batch([None] * max(args.warmup, k))  # warm every thread's stream, pool and tables
-    phase_tot.clear()
-    _t, t = timed_segments(prove_batch, [segs], 0, hal.synchronize, dist)
-    seal = last["seal"]
+    def timed_leg(prove_one, label):
+        phase_tot, last = {}, {}
+        lock = threading.Lock()
+
+        def prove_on(slot, n):
+            for _ in range(n):
+                seal, mix = prove_one(slot)
+                prof = r.last_profile()
+                with lock:
+                    last["seal"], last["mix"] = seal, mix
+                    for key, v in prof.items():
+                        phase_tot[key] = phase_tot.get(key, 0.0) + v
+
+        def prove_batch(batch):
+            # `batch` segments over k host threads (r0vm-style queue depth)
+            n = len(batch)
+            share = [n // k + (1 if i < n % k else 0) for i in range(k)]
+            ts = [threading.Thread(target=prove_on, args=(i, share[i])) for i in range(k) if share[i]]
+            for t_ in ts:
+                t_.start()
+            for t_ in ts:
+                t_.join()
+
+        prove_batch([None] * max(args.warmup, k))  # warm every thread's stream, pool and tables
+        phase_tot.clear()
+        _t, t = timed_segments(prove_batch, [segs], 0, hal.synchronize, dist)
+        phases = {key: round(v / args.steps, 3) for key, v in phase_tot.items()}
+        if rank == 0:
+            print(json.dumps({label + "_phases_ms": phases, "seal_words": int(last["seal"].size)}), file=sys.stderr)
+        return t, last["seal"], last["mix"]
+
+    if trace_mode:
+        t, seal, mix = timed_leg(lambda slot: r.prove_segment_trace_resident(hal, rt), "trace")
+        t_w, seal_w, _ = timed_leg(prove_witness, "prove_only")
+    else:
+        t, seal, mix = timed_leg(prove_witness, "prove")
     # host-side gather of one seal digest per rank (the receipts stay on their hosts)
-    from risc0_amd.segments import gather_results
-    import hashlib
     digests = gather_results({rank: hashlib.sha256(seal.tobytes()).hexdigest()[:16]}, dist)
     # ranks that had to share a device (segments.narrow_visible_devices, or the rehearsal switch)
     shared = gather_results({rank: os.environ.get("R0_RANKS_SHARE_DEVICES") == "1"
@@ -155,6 +188,13 @@ def main():
     cycles_total = world * args.steps * (1 << args.po2)
     value = cycles_total / t
     ms_per_step = 1000.0 * t / args.steps
+    prove_only = None
+    if trace_mode:
+        prove_only = {"value": round(cycles_total / t_w, 1), "unit": "cycles/s",
+                      "ms_per_step": round(1000.0 * t_w / args.steps, 3),
+                      "seal_sha256_rank0": hashlib.sha256(seal_w.tobytes()).hexdigest()[:16],
+                      "note": "the prove core alone (r0hip_prove_segment) on a uniform synthetic witness (code, data "
+                              "and accum groups) resident in HBM: no witness generation, no accumulation"}
 
     # kernel-level timing of the dominant kernel + roofline (rank 0)
     roofline = None
@@ -162,10 +202,8 @@ def main():
     e2e = None
     acc_leg = None
     if rank == 0:
-        kt = kernel_roofline(r, hal, args, circ, dc, dd, da, dg, version)
-        roofline = kt
-        phases = {key: round(v / args.steps, 3) for key, v in phase_tot.items()}
-        print(json.dumps({"phases_ms": phases, "seal_words": int(seal.size)}), file=sys.stderr)
+        prove_timed = (lambda: r.prove_segment_trace_resident(hal, rt)) if trace_mode else (lambda: prove_witness(0))
+        roofline = kernel_roofline(r, args, prove_timed)
         # the side legs keep 2 in flight below po2 21 unless --inflight says otherwise: the
         # pipeline's uploader and a third prover measured slower there (63.1 against 57.6 ms)
         kl = k if args.inflight is not None else min(k, 2)
@@ -174,10 +212,17 @@ def main():
         if args.accum_steps > 0 and args.circuit == "rv32im" and host_witness is not None:
             acc_leg = with_accumulation(r, hal, args, host_witness, kl, version)
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(args, circ, seal, last["mix"])
+            cpu = cpu_baseline_trace(args, trace, seal, mix) if trace_mode else cpu_baseline(args, circ, seal, mix)
     del host_witness
 
     if rank == 0:
+        workload = (f"{args.circuit} segment po2={args.po2}, {args.hashfn} hashfn, preflight trace resident in HBM "
+                    "-> witness generation -> accumulation -> seal on host (the reference's prove_core)"
+                    if trace_mode else
+                    f"{args.circuit} segment po2={args.po2}, {args.hashfn} hashfn, witness resident in HBM -> seal on host")
+        data = ("synthetic (a loop guest: random 32-instruction RV32IM body, repeated until the segment suspends; "
+                "preflight restated from the reference executor, tests/rv32im_trace.py; seeded per rank)"
+                if trace_mode else "synthetic (uniform BabyBear witness, seeded per segment)")
         line = {
             "metric": f"RISC-V cycles proved/sec at segment po2={args.po2}",
             "value": round(value, 1),
@@ -190,9 +235,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32 (BabyBear Montgomery, exact modular integer)",
-            "data": "synthetic (uniform BabyBear witness, seeded per segment)",
-            "config": {"workload": f"{args.circuit} segment po2={args.po2}, {args.hashfn} hashfn, "
-                                   "witness resident in HBM -> seal on host",
+            "data": data,
+            "config": {"workload": workload,
                        "circuit": args.circuit, "po2": args.po2, "hashfn": args.hashfn,
                        "segments_per_gpu": args.steps, "segments_in_flight_per_gpu": k,
                        "parallelism": f"segment-per-gpu x{world}",
@@ -201,6 +245,8 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if prove_only:
+            line["prove_only"] = prove_only
         if e2e:
             line["end_to_end"] = e2e
         if acc_leg:
@@ -210,7 +256,7 @@ def main():
         dist.destroy_process_group()
     if rank == 0 and cpu and (cpu.get("seal_equal") is False or cpu.get("mix_equal") is False):
         # full-size oracle parity failed: the line above carries both digests
-        print("bench: GPU seal differs from the CPU oracle's on the same witness", file=sys.stderr)
+        print("bench: GPU seal differs from the CPU oracle's on the same input", file=sys.stderr)
         sys.exit(1)
 
 
@@ -226,7 +272,7 @@ VALU_PEAK_GIPS = 256 * 4 * 2.4e9 / 4 / 1e9
 VALU_BOUND = {"eval_check", "hash_rows", "merkle_fold", "batch_evaluate_any"}
 
 
-def kernel_roofline(r, hal, args, circ, dc, dd, da, dg, version):
+def kernel_roofline(r, args, prove):
     """Time every kernel family of one proof with HIP events on the library stream
     (r0hip_kernel_times) and quote the dominant one against the resource that binds it:
     VALU instruction issue (SQ_INSTS_VALU per launch from the committed PMC pass of this
@@ -234,9 +280,9 @@ def kernel_roofline(r, hal, args, circ, dc, dd, da, dg, version):
     the HBM view is always reported beside it."""
     # the main thread has its own stream/pool: warm it first so no first-use
     # allocation lands inside a timed launcher
-    r.prove_segment(hal, args.circuit, args.po2, dc, dd, da, dg, version=version)
+    prove()
     r.set_kernel_timing(True)
-    r.prove_segment(hal, args.circuit, args.po2, dc, dd, da, dg, version=version)
+    prove()
     times = r.kernel_times()
     r.set_kernel_timing(False)
     if not times:
@@ -460,6 +506,65 @@ def host_cores():
     if quota:
         n = min(n, max(1, int(quota)))
     return n
+
+
+def cpu_baseline_trace(args, trace, gpu_seal, gpu_mix):
+    """The reference's prove_core from the same preflight trace on the host CPU: the compiled
+    reference witness generation (risc0_circuit_rv32im_cpu_witgen, parallel mode) and
+    accumulation (risc0_circuit_rv32im_cpu_accum) from oracle/_ref around the CPU oracle
+    prover (C++ restatement of CpuHal + Prover, eval_check through the reference's compiled
+    poly_fp), on every host core the process may use. Its seal and mix are compared with the
+    last timed GPU seal and mix of that trace (`seal_equal`), as the reference prover verifies
+    its own receipt before returning it (zkvm/src/host/server/prove/prover_impl.rs:277-280);
+    main() exits nonzero on a mismatch."""
+    try:
+        cores = host_cores()
+        os.environ["ORACLE_THREADS"] = str(cores)  # read once, at the oracle's first parallel op
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle
+        import rv32im_accum_ref as RA
+        import rv32im_witgen_ref as W
+        if oracle.ref_lib() is None or not RA.available():
+            return None
+        import hashlib
+        suite = {"poseidon2": oracle.POSEIDON2, "sha-256": oracle.SHA256, "poseidon_254": oracle.POSEIDON254}[args.hashfn]
+        rows = 1 << trace.po2
+        data, glob, cyc, tx = W.inputs(trace)  # PreflightResults::new's injector and globals (not timed)
+        oracle.op_times(reset=True)
+        t0 = time.perf_counter()
+        d, g = W.run(data, glob, cyc, tx, trace.table_split_cycle, rows, W.MODE_PARALLEL)
+        t_wg = time.perf_counter() - t0
+        d = np.where(d == W.INVALID, 0, d).astype(np.uint32)
+        g = np.where(g == W.INVALID, 0, g).astype(np.uint32)
+        acc_s = []
+
+        def fill(mix):
+            ta = time.perf_counter()
+            a = RA.accum(d, g, mix, rows, rows)
+            a = np.where(a == W.INVALID, 0, a).astype(np.uint32)
+            acc_s.append(time.perf_counter() - ta)
+            return a
+        cseal, cmix, _, _ = oracle.prove_segment_cb("rv32im", suite, trace.po2, np.zeros(rows, np.uint32), d, g, fill,
+                                                    RA.ACCUM_COLS * rows, version=2)
+        t = time.perf_counter() - t0
+        ops = {"witgen (reference risc0_circuit_rv32im_cpu_witgen)": round(t_wg, 3),
+               "accumulate (reference risc0_circuit_rv32im_cpu_accum)": round(sum(acc_s), 3)}
+        ops.update({k: round(v[0], 3) for k, v in sorted(oracle.op_times().items(), key=lambda kv: -kv[1][0])})
+        ops["other (zeroize, transcript, openings, host polys)"] = round(t - sum(ops.values()), 3)
+        dig = lambda a: hashlib.sha256(np.ascontiguousarray(a, dtype=np.uint32).tobytes()).hexdigest()
+        return {"value": round(rows / t, 1), "unit": "cycles/s", "cores": int(oracle.num_threads()), "kind": "port",
+                "sample": f"one rv32im segment at po2={trace.po2} ({args.hashfn}) from the bench's own preflight trace, "
+                          f"{t:.1f} s wall: the reference's compiled witgen and accumulation (oracle/_ref) and the "
+                          "oracle prover with the reference's compiled poly_fp",
+                "seconds_by_hal_op": ops,
+                "seal_equal": bool(np.array_equal(cseal, gpu_seal)), "mix_equal": bool(np.array_equal(cmix, gpu_mix)),
+                "oracle_seal_sha256": dig(cseal), "gpu_seal_sha256": dig(gpu_seal),
+                "oracle_mix_sha256": dig(cmix), "gpu_mix_sha256": dig(gpu_mix),
+                "parity_note": "CPU prove_core of rank 0's own trace against the last timed GPU seal of that trace"}
+    except Exception as e:  # the baseline is reported, never required
+        print(f"cpu baseline failed: {e}", file=sys.stderr)
+        return None
 
 
 def cpu_baseline(args, circ, gpu_seal=None, gpu_mix=None):

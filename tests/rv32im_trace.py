@@ -328,7 +328,7 @@ class Trace:
     """the restated preflight of one segment"""
 
     def __init__(self, po2, program, *, base_pc=0x10000, data=None, regs=None, seed=1, max_user_cycles=None,
-                 read_nodes=True):
+                 read_nodes=True, discover_cycles=None):
         self.po2 = po2
         self.rng = np.random.default_rng(seed)
         # image: code, data, registers, suspend state, input/output digests
@@ -348,13 +348,15 @@ class Trace:
         self.nonce = [int(x) for x in self.rng.integers(0, 1 << 32, 8, dtype=np.uint64)]
         self.rand_z = [int(x) for x in self.rng.integers(0, P, 4)]
         self.program_end = base_pc + 4 * len(program)
-        self.max_user_cycles = max_user_cycles
         # pass 1 (the executor's run that fixes the segment's partial image): the pages the
         # body touches and dirties
         self.reset(mem, {})
         self.discover = True
         self.touched, self.dirty = set(), set()
+        # a loop's pages are all touched within its first iterations: discovery may stop early
+        self.max_user_cycles = max_user_cycles if discover_cycles is None else min(discover_cycles, max_user_cycles)
         self.body()
+        self.max_user_cycles = max_user_cycles
         touched, dirty = sorted(self.touched), sorted(self.dirty)
         # the sparse Merkle image: page digests, their ancestors hashed from the children,
         # arbitrary digests for the siblings off the paths (PagingActivity::new, preflight.rs:720-736)
@@ -879,4 +881,4 @@ def loop_trace(po2, body_len=32, seed=1, reserve=4096):
     data = {0x00100000 + 4 * i: int(rng.integers(0, 1 << 32)) for i in range(256)}
     regs = {r: int(rng.integers(0, 1 << 32)) for r in range(1, 31)}
     budget = (1 << po2) - RESERVED_CYCLES - reserve
-    return Trace(po2, prog, data=data, regs=regs, seed=seed, max_user_cycles=budget)
+    return Trace(po2, prog, data=data, regs=regs, seed=seed, max_user_cycles=budget, discover_cycles=64 * body_len)
