@@ -45,7 +45,10 @@ const char* r0hip_host_free(void* h_ptr);
 const char* r0hip_synchronize(void);
 void r0hip_free_error(const char* err);
 
-/* ---- NTT family (sppark_batch_* in sys/src/cuda.rs:22-46; CPU semantics cpu.rs:305-408) ---- */
+/* ---- NTT family (sppark_batch_* in sys/src/cuda.rs:22-46; CPU semantics cpu.rs:305-408) ----
+ * Inputs must be canonical field words (< p), as every buffer the Hal hands over is: the first
+ * butterfly stage skips its unit twiddle (no Montgomery multiply reduces a staged word), so a
+ * non-canonical input word is not reduced there. */
 /* expand each of `count` polys of 2^(lg_out-expand_bits) bit-reversed coeffs into out (count x 2^lg_out)
  * and evaluate: Hal::batch_expand_into_evaluate_ntt (hal/mod.rs:102-108; cuda.rs:529-570) */
 const char* r0hip_batch_expand_into_evaluate_ntt(uint32_t* d_out, const uint32_t* d_in, size_t count,
@@ -100,7 +103,10 @@ const char* r0hip_fill_uniform(uint32_t* d_out, size_t count, uint64_t seed);
 
 /* ---- hashing (sppark_poseidon2_{rows,fold}, sppark_poseidon254_{rows,fold}, risc0_zkp_cuda_sha_{rows,fold};
  * sys/src/cuda.rs:49-72) ---- */
-/* out[row] = H(matrix[col*rows + row] for col < cols) */
+/* out[row] = H(matrix[col*rows + row] for col < cols). Poseidon2 / Poseidon254 inputs must be
+ * canonical field words (< p): the Poseidon2 full rounds read a word as a signed 32-bit value,
+ * which is its value mod p for any word below 2^31 (tests/native/field_equiv.cpp pins
+ * [p, 2^31)) but not above. */
 const char* r0hip_hash_rows(int suite, uint32_t* d_out, const uint32_t* d_matrix, size_t rows, size_t cols);
 /* io[output_size + i] = H(io[input_size + 2i], io[input_size + 2i + 1]) (cpu.rs:569-581) */
 const char* r0hip_hash_fold(int suite, uint32_t* d_io, size_t input_size, size_t output_size);
