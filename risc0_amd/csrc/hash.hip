@@ -250,9 +250,10 @@ __global__ __launch_bounds__(kThreads) void sha_fold_kernel(uint32_t* io, uint64
   store_digest(io + (out_off + i) * 8, d);
 }
 
-// Poseidon2 tree top in one workgroup of 512 lanes: layers of >= 256 nodes one lane per
-// node, smaller layers one quad per node (measured per layer size).
-constexpr uint32_t kTopThreads = 512;
+// Poseidon2 tree top in one workgroup of 1024 lanes: layers above quad_max nodes one lane
+// per node, smaller layers one quad per node (poseidon2_mix_quad: a quarter of the
+// permutation's dependent instructions per lane, so a layer's latency is about a quarter)
+constexpr uint32_t kTopThreads = 1024;
 __global__ __launch_bounds__(kTopThreads) void p2_fold_top_kernel(uint32_t* io, uint32_t top_layer_size,
                                                                  uint32_t quad_max) {
   for (uint32_t out = top_layer_size; out >= 1; out >>= 1) {
@@ -267,17 +268,20 @@ __global__ __launch_bounds__(kTopThreads) void p2_fold_top_kernel(uint32_t* io, 
         poseidon2_mix(c);
         store_digest(io + (uint64_t(out) + i) * 8, c);
       }
-    } else if (threadIdx.x < 4 * out) {
-      const uint32_t i = threadIdx.x >> 2, q = threadIdx.x & 3;
-      const uint32_t* src = io + (uint64_t(2 * out) + 2 * i) * 8;
-      uint32_t c[6];
+    } else {
+      // whole quads per iteration (kTopThreads is a multiple of 4)
+      for (uint32_t t = threadIdx.x; t < 4 * out; t += kTopThreads) {
+        const uint32_t i = t >> 2, q = t & 3;
+        const uint32_t* src = io + (uint64_t(2 * out) + 2 * i) * 8;
+        uint32_t c[6];
 #pragma unroll
-      for (int j = 0; j < 4; j++) c[j] = src[4 * j + q];
-      c[4] = c[5] = 0;
-      poseidon2_mix_quad(c);
-      uint32_t* dst = io + (uint64_t(out) + i) * 8;
-      dst[q] = c[0];
-      dst[4 + q] = c[1];
+        for (int j = 0; j < 4; j++) c[j] = src[4 * j + q];
+        c[4] = c[5] = 0;
+        poseidon2_mix_quad(c);
+        uint32_t* dst = io + (uint64_t(out) + i) * 8;
+        dst[q] = c[0];
+        dst[4 + q] = c[1];
+      }
     }
     __threadfence_block();
     __syncthreads();
