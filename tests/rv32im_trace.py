@@ -42,12 +42,20 @@ MERKLE_TREE_END_WADDR = 0x44000000
 POVW_NONCE_START_WADDR = 0x44000000
 ZERO_PAGE_END = 0x10000
 KERNEL_START = 0xC0000000
+KERNEL_END = 0xFF000000
+SAFE_WRITE_WADDR = 0xFFFF0100 // 4
+MEPC_WADDR = 0xFFFF0200 // 4
+ECALL_DISPATCH_WADDR = 0xFFFF1000 // 4
+MAX_IO_BYTES, MAX_IO_WORDS = 1024, 4
+PFLAG_IS_ELEM, PFLAG_CHECK_OUT = 0x80000000, 0x40000000
+REG_A0, REG_A1, REG_A2, REG_A3, REG_A7 = 10, 11, 12, 13, 17
 LOOKUP_TABLE_CYCLES = ((1 << 8) + (1 << 16)) // 16
 RESERVED_CYCLES = LOOKUP_TABLE_CYCLES + 1
 REG_MAX = 32
 
 # CycleState (platform.rs:101-131)
 LOAD_ROOT_AND_NONCE, RESUME, SUSPEND, STORE_ROOT, CONTROL_TABLE, CONTROL_DONE = 0, 1, 4, 5, 6, 7
+MACHINE_ECALL, TERMINATE, HOST_READ_SETUP, HOST_WRITE, HOST_READ_BYTES, HOST_READ_WORDS = 8, 9, 10, 11, 12, 13
 POSEIDON_ENTRY, POSEIDON_PAGING = 16, 22
 DECODE = 48
 
@@ -62,7 +70,8 @@ KINDS = {"add": 0, "sub": 1, "xor": 2, "or": 3, "and": 4, "slt": 5, "sltu": 6, "
          "andi": 10, "slti": 11, "sltiu": 12, "beq": 13, "bne": 14, "blt": 15, "bge": 16, "bltu": 17, "bgeu": 18,
          "jal": 19, "jalr": 20, "lui": 21, "auipc": 22, "sll": 24, "slli": 25, "mul": 26, "mulh": 27, "mulhsu": 28,
          "mulhu": 29, "srl": 32, "sra": 33, "srli": 34, "srai": 35, "div": 36, "divu": 37, "rem": 38, "remu": 39,
-         "lb": 40, "lh": 41, "lw": 42, "lbu": 43, "lhu": 44, "sb": 48, "sh": 49, "sw": 50, "fence": 58}
+         "lb": 40, "lh": 41, "lw": 42, "lbu": 43, "lhu": 44, "sb": 48, "sh": 49, "sw": 50, "eany": 56, "mret": 57,
+         "fence": 58}
 
 
 def node_idx_to_waddr(idx):
@@ -124,6 +133,10 @@ def asm(op, *a):
                 | ((off >> 12) & 0xFF) << 12 | rd << 7 | 0b1101111)
     if op == "fence":
         return 0b0001111
+    if op == "ecall":
+        return 0b1110011
+    if op == "mret":
+        return 0b0011000 << 25 | 0b00010 << 20 | 0b1110011
     raise ValueError(op)
 
 
@@ -219,7 +232,10 @@ class Poseidon2State:
     def rest(self, tr, final_state):
         f = self.f
         cur = [f["next_state"]]
-        assert f["has_state"] == 0, "state-carrying sponges are not modelled"
+        if f["has_state"]:
+            self.step(tr, cur, POSEIDON_LOAD_STATE, 0)
+            for i in range(8):
+                self.inner[16 + i] = tr.load_u32(f["state_addr"] + i)
         addr = f["buf_in_addr"]
         while f["count"] > 0:
             self.step(tr, cur, POSEIDON_LOAD_IN, 0)
@@ -260,6 +276,10 @@ class Poseidon2State:
             for i in range(8):
                 tr.store_u32(out + i, self.inner[i])
         f["buf_in_addr"] = 0
+        if f["has_state"]:
+            self.step(tr, cur, POSEIDON_STORE_STATE, 0)
+            for i in range(8):
+                tr.store_u32(f["state_addr"] + i, self.inner[16 + i])
         self.step(tr, cur, final_state, 0)
 
 
@@ -328,18 +348,31 @@ class Trace:
     """the restated preflight of one segment"""
 
     def __init__(self, po2, program, *, base_pc=0x10000, data=None, regs=None, seed=1, max_user_cycles=None,
-                 read_nodes=True, discover_cycles=None):
+                 read_nodes=True, discover_cycles=None, kernel=None, kernel_pc=KERNEL_START, machine_regs=None,
+                 read_record=(), write_record=()):
+        """program: user code at base_pc. kernel: machine-mode code at kernel_pc, entered by a
+        user `ecall` through ECALL_DISPATCH_ADDR (r0vm.rs:342-352); it leaves with `mret` or
+        a machine ecall (terminate, host read/write, Poseidon2). read_record / write_record:
+        the segment's host-read payloads (bytes) and host-write return values."""
         self.po2 = po2
         self.rng = np.random.default_rng(seed)
         # image: code, data, registers, suspend state, input/output digests
         mem = {}
         for i, w in enumerate(program):
             mem[base_pc // 4 + i] = w
+        for i, w in enumerate(kernel or ()):
+            mem[kernel_pc // 4 + i] = w
+        if kernel:
+            mem[ECALL_DISPATCH_WADDR] = kernel_pc
         for a, w in (data or {}).items():
             mem[a // 4] = w
         regs = regs or {}
         for r in range(REG_MAX):
             mem[USER_REGS_WADDR + r] = regs.get(r, 0) if r else 0
+        for r, v in (machine_regs or {}).items():
+            mem[MACHINE_REGS_WADDR + r] = v
+        self.read_record = [list(x) for x in read_record]
+        self.write_record = list(write_record)
         mem[SUSPEND_PC_WADDR] = base_pc
         mem[SUSPEND_MODE_WADDR] = 0
         self.input_words = [int(x) for x in self.rng.integers(0, 1 << 32, 8, dtype=np.uint64)]
@@ -397,6 +430,11 @@ class Trace:
         self.page_memory = dict(page_memory)  # Merkle node digests (word address -> word)
         self.orig_words = {}
         self.prev_cycle = {}
+        self.user_cycles = 0
+        self.terminated = False
+        self.term_a0 = self.term_a1 = 0
+        self.cur_read = 0
+        self.cur_write = 0
 
     # ---- memory (preflight.rs:571-634)
     def load_u32(self, addr):
@@ -444,18 +482,25 @@ class Trace:
     def p2_cycle(self, cur, p2):  # on_poseidon2_cycle (preflight.rs:688-697): the state as of now
         self.add_cycle_special(cur, p2.f["next_state"], self.pc, node_waddr_to_idx(p2.f["buf_out_addr"]),
                                ("p2", p2.copy()))
+        self.user_cycles += 1
 
     # ---- registers (r0vm.rs:674-695), user mode only
+    def regs_base(self):  # r0vm.rs:599-605
+        return MACHINE_REGS_WADDR if self.machine_mode else USER_REGS_WADDR
+
     def load_reg(self, idx):
-        return self.load_u32(USER_REGS_WADDR + idx)
+        return self.load_u32(self.regs_base() + idx)
 
     def store_reg(self, idx, word):
-        self.store_u32(USER_REGS_WADDR + (REG_MAX * 2 if idx == 0 else idx), word & U32_MAX)
+        self.store_u32(self.regs_base() + (REG_MAX * 2 if idx == 0 else idx), word & U32_MAX)
+
+    def data_ok(self, addr):  # check_data_load / check_data_store (r0vm.rs:712-718)
+        return (addr >= ZERO_PAGE_END and self.machine_mode != 0) or ZERO_PAGE_END <= addr < KERNEL_START
 
     # ---- one instruction (rv32im.rs: step, step_compute, step_load, step_store, step_system)
     def step(self):
         pc = self.pc
-        assert pc >= ZERO_PAGE_END and pc < KERNEL_START and pc % 4 == 0, hex(pc)
+        assert pc >= ZERO_PAGE_END and (self.machine_mode or pc < KERNEL_START) and pc % 4 == 0, hex(pc)
         insn = self.load_u32(pc // 4)
         assert insn & 3 == 3
         opc, f3, f7 = insn & 0x7F, (insn >> 12) & 7, insn >> 25
@@ -476,7 +521,7 @@ class Trace:
             kind = {0: "lb", 1: "lh", 2: "lw", 4: "lbu", 5: "lhu"}[f3]
             rs1 = self.load_reg(rs1i)
             addr = (rs1 + imm_i) & M
-            assert addr >= ZERO_PAGE_END and addr < KERNEL_START, hex(addr)
+            assert self.data_ok(addr), hex(addr)
             data = self.load_u32(addr // 4)
             sh = 8 * (addr & 3)
             if kind == "lb":
@@ -504,7 +549,7 @@ class Trace:
             rs2 = rs1 if rs1i == rs2i else self.load_reg(rs2i)
             addr = (rs1 + imm_s) & M
             sh = 8 * (addr & 3)
-            assert addr >= ZERO_PAGE_END and addr < KERNEL_START, hex(addr)
+            assert self.data_ok(addr), hex(addr)
             data = self.load_u32(addr // 4)
             if kind == "sb":
                 data = (data & ~(0xFF << sh) & M) | ((rs2 & 0xFF) << sh)
@@ -517,6 +562,26 @@ class Trace:
             self.store_u32(addr // 4, data)
             self.pc = pc + 4
             self.end_insn(kind)
+            return
+        if opc == 0b1110011:  # step_system (rv32im.rs:561-586): ecall, mret
+            if f7 == 0b0011000 and f3 == 0:
+                # mret (r0vm.rs:633-642)
+                assert self.machine_mode, "mret in user mode"
+                self.pc = (self.load_u32(MEPC_WADDR) + 4) & M
+                self.machine_mode = 0
+                self.end_insn("mret")
+                return
+            assert f3 == 0 and f7 == 0 and rs2i == 0, "only ecall is modelled"
+            if self.machine_mode:
+                self.machine_ecall()  # returns false: no instruction-end row
+                return
+            # user_ecall + enter_trap (r0vm.rs:342-352, 587-597)
+            dispatch = self.load_u32(ECALL_DISPATCH_WADDR)
+            assert dispatch % 4 == 0 and KERNEL_START <= dispatch < KERNEL_END
+            self.store_u32(MEPC_WADDR, pc)
+            self.pc = dispatch
+            self.machine_mode = 1
+            self.end_insn("eany")
             return
         # step_compute
         if opc == 0b0110011:
@@ -564,13 +629,112 @@ class Trace:
         self.pc = new_pc
         self.end_insn(kind)
 
-    def end_insn(self, kind):  # on_insn_end (preflight.rs:559-564)
+    def end_insn(self, kind):  # on_insn_end (preflight.rs:559-564) -> add_cycle_insn (406-454)
         k = KINDS[kind]
         if kind == "fence":
-            self.add_cycle(DECODE, self.pc, 7, 2)  # CONTROL0 / FENCE (preflight.rs:440-449)
+            self.add_cycle(DECODE, self.pc, 7, 2)  # CONTROL0 / FENCE
+        elif kind == "eany":
+            # switched on the machine mode entering the EANY: the last row's
+            if self.cycles[-1][4] != 0:
+                self.add_cycle(DECODE, self.pc, 8, 0)  # ECALL0 / MACHINE_ECALL
+            else:
+                self.add_cycle(DECODE, self.pc, 7, 2)  # CONTROL0 / USER_ECALL
+        elif kind == "mret":
+            self.add_cycle(DECODE, self.pc, 7, 3)  # CONTROL0 / MRET
         else:
             self.add_cycle(DECODE, self.pc, k // 8, k % 8)
         self.user_cycle += 1
+        self.user_cycles += 1
+
+    # ---- machine ecalls (r0vm.rs:354-585)
+    def ecall_cycle(self, cur, nxt, s0=0, s1=0, s2=0):  # on_ecall_cycle (preflight.rs:636-648)
+        self.add_cycle_special(cur, nxt, self.pc, 0, ("ecall", (s0, s1, s2)))
+        self.user_cycles += 1
+
+    def machine_ecall(self):
+        a7 = self.load_reg(REG_A7)
+        if a7 == 0:  # ecall_terminate
+            self.ecall_cycle(MACHINE_ECALL, TERMINATE)
+            self.term_a0, self.term_a1 = self.load_reg(REG_A0), self.load_reg(REG_A1)
+            self.pc += 4
+            self.ecall_cycle(TERMINATE, SUSPEND)
+            self.terminated = True
+        elif a7 == 1:
+            self.ecall_read()
+        elif a7 == 2:  # ecall_write
+            self.ecall_cycle(MACHINE_ECALL, HOST_WRITE)
+            fd, ptr, n = self.load_reg(REG_A0), self.load_reg(REG_A1), self.load_reg(REG_A2)
+            assert n <= MAX_IO_BYTES
+            self.cur_write += 1  # host_write (preflight.rs:669-675): the record after the cursor
+            self.store_reg(REG_A0, self.write_record[self.cur_write])
+            self.pc += 4
+            self.ecall_cycle(HOST_WRITE, DECODE)
+        elif a7 == 3:  # ecall_poseidon2 (r0vm.rs:547-558, poseidon2.rs:279-289)
+            self.pc += 4
+            self.ecall_cycle(MACHINE_ECALL, POSEIDON_ENTRY)
+            sa, bi, bo, bc = (self.load_u32(MACHINE_REGS_WADDR + r) for r in (REG_A0, REG_A1, REG_A2, REG_A3))
+            # the registers hold byte addresses: the circuit's ReadAddr reads them as reg / 4
+            # (steps.cpp exec_ReadAddr, exec_PoseidonEcall). execute/poseidon2.rs:285-292 passes
+            # the raw register values into the state; a trace built that way fails the
+            # reference witgen's checked store of stateAddr (tests: ecall traces)
+            sa, bi, bo = sa // 4, bi // 4, bo // 4
+            p2 = Poseidon2State(state_addr=sa, buf_in_addr=bi, buf_out_addr=bo, has_state=int(sa != 0),
+                                is_elem=int(bc & PFLAG_IS_ELEM != 0), check_out=int(bc & PFLAG_CHECK_OUT != 0),
+                                count=bc & 0xFFFF, mode=1, load_tx_type=TX_READ, next_state=POSEIDON_ENTRY)
+            p2.rest(self, DECODE)
+        else:
+            raise ValueError(f"machine ecall {a7} is not modelled")
+
+    def store_u8(self, addr, byte):  # Risc0Context::store_u8 (r0vm.rs:125-133)
+        w = self.load_u32(addr // 4)
+        sh = 8 * (addr & 3)
+        self.store_u32(addr // 4, (w & ~(0xFF << sh) & U32_MAX) | (byte << sh))
+
+    def ecall_read(self):  # r0vm.rs:394-506
+        self.ecall_cycle(MACHINE_ECALL, HOST_READ_SETUP)
+        cur = [HOST_READ_SETUP]
+        fd, ptr, n = self.load_reg(REG_A0), self.load_reg(REG_A1), self.load_reg(REG_A2)
+        assert n <= MAX_IO_BYTES and ptr + n < (1 << 32)
+        rec = self.read_record[self.cur_read]
+        self.cur_read += 1
+        assert len(rec) <= n
+        rlen = len(rec)
+        self.store_reg(REG_A0, rlen)
+        if rlen == 0:
+            self.pc += 4
+
+        def nxt_state(p, r):
+            return DECODE if r == 0 else (HOST_READ_BYTES if p % 4 or r < 4 else HOST_READ_WORDS)
+
+        def add(p, r):
+            ns = nxt_state(p, r)
+            self.ecall_cycle(cur[0], ns, p // 4, p % 4, r)
+            cur[0] = ns
+        add(ptr, rlen)
+        i = 0
+        while rlen > 0 and ptr % 4:
+            self.store_u8(ptr, rec[i])
+            ptr, i, rlen = ptr + 1, i + 1, rlen - 1
+            if rlen == 0:
+                self.pc += 4
+            add(ptr, rlen)
+        while rlen >= MAX_IO_WORDS:
+            words = min(rlen // MAX_IO_WORDS, MAX_IO_WORDS)
+            for j in range(MAX_IO_WORDS):
+                if j < words:
+                    self.store_u32(ptr // 4, int.from_bytes(bytes(rec[i:i + 4]), "little"))
+                    ptr, i, rlen = ptr + 4, i + 4, rlen - 4
+                else:
+                    self.store_u32(SAFE_WRITE_WADDR + j, 0)
+            if rlen == 0:
+                self.pc += 4
+            add(ptr, rlen)
+        while rlen > 0:
+            self.store_u8(ptr, rec[i])
+            ptr, i, rlen = ptr + 1, i + 1, rlen - 1
+            if rlen == 0:
+                self.pc += 4
+            add(ptr, rlen)
 
     # ---- the segment (preflight.rs:91-107)
     def build(self):
@@ -616,10 +780,11 @@ class Trace:
             self.add_cycle_special(CONTROL_TABLE, CONTROL_TABLE, i)
         self.machine_mode = 0
         self.add_cycle_special(CONTROL_TABLE, CONTROL_DONE, 0)
-        # not a terminating segment: the shutdown threshold is this cycle count
+        # a segment that does not terminate: the shutdown threshold is this cycle count
         self.segment_threshold = len(self.cycles)
-        diff = len(self.cycles) - self.segment_threshold
-        self.cycles[diff // 2][9 + diff % 2] += 1
+        if not self.terminated:
+            diff = len(self.cycles) - self.segment_threshold
+            self.cycles[diff // 2][9 + diff % 2] += 1
         self.machine_mode = 1
         self.add_cycle_special(CONTROL_DONE, CONTROL_DONE, 0)
         assert len(self.cycles) - start == RESERVED_CYCLES
@@ -677,12 +842,13 @@ class Trace:
         for i, w in enumerate(self.input_words):
             self.store_u32(GLOBAL_INPUT_WADDR + i, w)
         self.add_cycle_special(RESUME, DECODE, self.pc)
-        n = 0
-        while self.pc < self.program_end:
-            if self.max_user_cycles is not None and n >= self.max_user_cycles:
+        # the executor's segment ends at its suspend cycle (preflight.rs:174-176); a program
+        # ends at a terminate ecall or (user code) past its last instruction
+        self.user_cycles = 0
+        while not self.terminated and (self.machine_mode or self.pc < self.program_end):
+            if self.max_user_cycles is not None and self.user_cycles >= self.max_user_cycles:
                 break
             self.step()
-            n += 1
         # suspend (r0vm.rs:316-321, preflight.rs:528-543)
         self.store_u32(SUSPEND_PC_WADDR, self.pc)
         self.store_u32(SUSPEND_MODE_WADDR, self.machine_mode)
@@ -722,6 +888,9 @@ class Trace:
             if back is not None and back[0] == "p2":
                 for col, v in zip(lay["poseidon2_state"], back[1].as_array()):
                     put(row, col, v)
+            elif back is not None and back[0] == "ecall":
+                for col, v in zip(lay["ecall_s"], back[1]):
+                    put(row, col, v)
             put(row, lay["cycle"], row)
             put(row, lay["next_pc_low"], cyc[1] & 0xFFFF)
             put(row, lay["next_pc_high"], cyc[1] >> 16)
@@ -739,7 +908,7 @@ class Trace:
             g[gl["input"][i][0]], g[gl["input"][i][1]] = w & 0xFFFF, w >> 16
         for i, e in enumerate(self.rand_z):
             g[gl["rng"] + i] = e
-        g[gl["is_terminate"]] = 0
+        g[gl["is_terminate"]] = int(self.terminated)
         g[gl["shutdown_cycle"]] = self.segment_threshold
         for i, w in enumerate(self.nonce):
             g[gl["povw_nonce"][i][0]], g[gl["povw_nonce"][i][1]] = w & 0xFFFF, w >> 16
@@ -882,3 +1051,49 @@ def loop_trace(po2, body_len=32, seed=1, reserve=4096):
     regs = {r: int(rng.integers(0, 1 << 32)) for r in range(1, 31)}
     budget = (1 << po2) - RESERVED_CYCLES - reserve
     return Trace(po2, prog, data=data, regs=regs, seed=seed, max_user_cycles=budget, discover_cycles=64 * body_len)
+
+
+def li(rd, value):
+    """load a 32-bit constant: lui + addi"""
+    value &= U32_MAX
+    lo = value & 0xFFF
+    hi = (value + (0x800 if lo & 0x800 else 0)) >> 12
+    return [asm("lui", rd, hi & 0xFFFFF), asm("addi", rd, rd, lo - (0x1000 if lo & 0x800 else 0))]
+
+
+def ecall_trace(po2, seed=1, n_user=60, data_base=0x00100000, terminate=True):
+    """user code that traps into a machine-mode kernel twice through `ecall` (Poseidon2 buffer
+    registers as byte addresses). The first entry
+    runs a Poseidon2 ecall with state (is_elem 0, two blocks), one without state on field
+    elements, a host write and an unaligned host read, then `mret`s back; the second entry
+    terminates (or, terminate=False, `mret`s again and the program runs off its end)."""
+    rng = np.random.default_rng(seed)
+    user = random_program(rng, n_user, data_base) + [asm("ecall")] + random_program(rng, n_user, data_base)[1:] + \
+        [asm("lui", 31, data_base >> 12), asm("ecall")] + random_program(rng, 20, data_base)[1:]
+    w = data_base // 4
+    k = []
+    k += [asm("addi", 5, 5, 1), asm("addi", 6, 0, 2)]
+    body = []
+    # Poseidon2 with state: a0 = state (word address), a1 = input, a2 = output, a3 = count
+    body += li(10, 4 * (w + 200)) + li(11, 4 * (w + 16)) + li(12, 4 * (w + 64)) + li(13, 2) + \
+        [asm("addi", 17, 0, 3), asm("ecall")]
+    # Poseidon2 over field elements, no state
+    body += [asm("addi", 10, 0, 0)] + li(11, 4 * (w + 128)) + li(12, 4 * (w + 72)) + li(13, PFLAG_IS_ELEM | 1) + \
+        [asm("addi", 17, 0, 3), asm("ecall")]
+    # host write (fd 1, 8 bytes at data_base), host read (fd 0, 23 bytes at data_base + 301)
+    body += [asm("addi", 10, 0, 1)] + li(11, data_base) + [asm("addi", 12, 0, 8), asm("addi", 17, 0, 2),
+                                                           asm("ecall")]
+    body += [asm("addi", 10, 0, 0)] + li(11, data_base + 301) + [asm("addi", 12, 0, 23), asm("addi", 17, 0, 1),
+                                                                 asm("ecall")]
+    body += [asm("mret")]
+    second = [asm("addi", 17, 0, 0), asm("ecall")] if terminate else [asm("mret")]
+    k += [asm("bge", 5, 6, 4 * (len(body) + 1))] + body + second
+    data = {data_base + 4 * i: int(rng.integers(0, 1 << 32)) for i in range(256)}
+    for i in range(16):  # field elements for the is_elem sponge
+        data[data_base + 4 * (128 + i)] = int(rng.integers(0, P))
+    for i in range(8):  # the sponge state: field elements
+        data[data_base + 4 * (200 + i)] = int(rng.integers(0, P))
+    regs = {r: int(rng.integers(0, 1 << 32)) for r in range(1, 31)}
+    mregs = {5: 0}
+    return Trace(po2, user, data=data, regs=regs, seed=seed, kernel=k, machine_regs=mregs,
+                 read_record=[bytes(int(x) for x in rng.integers(0, 256, 23))], write_record=[0, 8, 0])

@@ -38,6 +38,17 @@ def test_rv32im_witgen_matches_reference(hal, po2, n, seed):
     assert (d == W.INVALID).any()  # columns no arm of a row writes stay INVALID, as in the reference
 
 
+@pytest.mark.parametrize("terminate", [True, False])
+def test_rv32im_witgen_ecalls_match_reference(hal, terminate):
+    """machine-mode rows: user ecall, Poseidon2 ecalls (state / no state, bytes / elements),
+    host write, unaligned host read, mret, terminate"""
+    t = T.ecall_trace(14, seed=3, terminate=terminate)
+    data, glob, cyc, tx = W.inputs(t)
+    ref_d, ref_g = W.run(data, glob, cyc, tx, t.table_split_cycle, 1 << 14)
+    d, g = gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle)
+    assert np.array_equal(d, ref_d) and np.array_equal(g, ref_g)
+
+
 def test_rv32im_witgen_modes(hal):
     """every mode runs the same schedule and gives the reference's forward-mode words"""
     t = T.random_trace(13, 500, seed=9)
@@ -77,7 +88,7 @@ def test_rv32im_witgen_failures(hal):
 
 
 @pytest.mark.parametrize("po2,n,suite,seed", [(13, 250, "poseidon2", 21), (14, 2500, "poseidon2", 3),
-                                              (14, 2000, "sha-256", 8)])
+                                              (14, 2000, "sha-256", 8), (14, 0, "poseidon2", 4)])
 def test_prove_segment_trace_matches_oracle(po2, n, suite, seed, oracle):
     """r0hip_prove_segment_trace (injector scatter, stepExec, zeroize, accumulation and the
     prove core on the device, rv32im prove/hal/mod.rs:143-224) gives the seal and mix of the
@@ -85,7 +96,7 @@ def test_prove_segment_trace_matches_oracle(po2, n, suite, seed, oracle):
     rows satisfy the circuit, so the seal verifies with the validity equation."""
     import risc0_amd as r
     h = r.HipHal(suite)
-    t = T.random_trace(po2, n, seed=seed)
+    t = T.random_trace(po2, n, seed=seed) if n else T.ecall_trace(po2, seed=seed)  # n = 0: the ecall trace
     s = {"poseidon2": oracle.POSEIDON2, "sha-256": oracle.SHA256}[suite]
     ref_seal, ref_mix, _, _, _ = W.prove_from_trace(t, s, oracle)
     cyc, tx = t.arrays()

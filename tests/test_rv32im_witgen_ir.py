@@ -45,6 +45,21 @@ def test_ir_matches_reference(po2, n, seed):
 
 
 @needs_ref
+@pytest.mark.parametrize("terminate", [True, False])
+def test_ir_matches_reference_with_ecalls(terminate):
+    """user ecalls into a machine-mode kernel: Poseidon2 ecalls (with and without state, bytes
+    and field elements), host write, an unaligned host read, mret, and terminate"""
+    t = T.ecall_trace(14, seed=3, terminate=terminate)
+    assert t.terminated == terminate
+    data, glob, cyc, tx = W.inputs(t)
+    majors = set(int(m) for m in cyc["major"][:t.table_split_cycle])
+    assert {0, 1, 7, 8, 9, 10} <= majors
+    ref_d, ref_g = W.run(data, glob, cyc, tx, t.table_split_cycle, 1 << 14)
+    d, g = I.witgen(data.copy(), glob.copy(), cyc.copy(), tx, 1 << 14)
+    assert np.array_equal(d, ref_d) and np.array_equal(g, ref_g)
+
+
+@needs_ref
 def test_reference_modes_agree():
     """the reference's parallel schedule (phase 1 before tableSplitCycle, phase 2 after)
     gives the forward mode's words: the lookup-table reads of phase 2 see every count"""
@@ -94,6 +109,10 @@ def test_trace_seal_verifies_with_validity(oracle):
     t = T.random_trace(13, 250, seed=21)
     seal, mix, d, g, acc = W.prove_from_trace(t, oracle.POSEIDON2, oracle)
     assert r.verify_seal("rv32im", r.POSEIDON2, seal, check_validity=True) == 13
+    # a terminating segment with machine-mode ecalls is valid too
+    te = T.ecall_trace(14, seed=4, terminate=True)
+    seal_e, _, _, _, _ = W.prove_from_trace(te, oracle.POSEIDON2, oracle)
+    assert r.verify_seal("rv32im", r.POSEIDON2, seal_e, check_validity=True) == 14
     rows = 1 << 13
     d2 = d.copy()
     row = next(i for i in range(rows) if t.cycles[i][0] == T.DECODE)
