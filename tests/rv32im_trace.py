@@ -56,6 +56,7 @@ REG_MAX = 32
 # CycleState (platform.rs:101-131)
 LOAD_ROOT_AND_NONCE, RESUME, SUSPEND, STORE_ROOT, CONTROL_TABLE, CONTROL_DONE = 0, 1, 4, 5, 6, 7
 MACHINE_ECALL, TERMINATE, HOST_READ_SETUP, HOST_WRITE, HOST_READ_BYTES, HOST_READ_WORDS = 8, 9, 10, 11, 12, 13
+SHA_ECALL, SHA_LOAD_STATE, SHA_LOAD_DATA, SHA_MIX, SHA_STORE_STATE = 32, 33, 34, 35, 36
 POSEIDON_ENTRY, POSEIDON_PAGING = 16, 22
 DECODE = 48
 
@@ -682,8 +683,90 @@ class Trace:
                                 is_elem=int(bc & PFLAG_IS_ELEM != 0), check_out=int(bc & PFLAG_CHECK_OUT != 0),
                                 count=bc & 0xFFFF, mode=1, load_tx_type=TX_READ, next_state=POSEIDON_ENTRY)
             p2.rest(self, DECODE)
+        elif a7 == 4:  # ecall_sha2 (r0vm.rs:559-571)
+            self.pc += 4
+            self.ecall_cycle(MACHINE_ECALL, SHA_ECALL)
+            self.sha2_ecall()
         else:
             raise ValueError(f"machine ecall {a7} is not modelled")
+
+    def sha_cycle(self, cur, st):  # on_sha2_cycle (preflight.rs:677-686)
+        self.add_cycle_special(cur[0], st["next_state"], self.pc, node_waddr_to_idx(st["state_out_addr"]),
+                               ("sha2", dict(st)))
+        self.user_cycles += 1
+        cur[0] = st["next_state"]
+
+    def sha2_ecall(self):  # execute/sha2.rs:56-160
+        M = U32_MAX
+        regs = [self.load_u32(MACHINE_REGS_WADDR + r) for r in (REG_A0, REG_A1, REG_A2, REG_A3, 14)]
+        sin, sout, dat = regs[0] // 4, regs[1] // 4, regs[2] // 4
+        count, kad = regs[3] & 0xFFFF, regs[4] // 4
+        assert all(r >= ZERO_PAGE_END for r in (regs[0], regs[1], regs[2], regs[4])) and count <= 10
+        st = dict(state_in_addr=sin, state_out_addr=sout, data_addr=dat, count=count, k_addr=kad, round=0,
+                  next_state=SHA_ECALL, a=0, e=0, w=0)
+        cur = [SHA_ECALL]
+        old_a, old_e, old_w = [0] * 68, [0] * 68, [0] * 16  # ring buffers: back(i) = list[-i]
+        bswap = lambda x: int.from_bytes(x.to_bytes(4, "little"), "big")
+        rotr = lambda x, n: ((x >> n) | (x << (32 - n))) & M
+
+        def step(nxt):
+            st["next_state"] = nxt
+            self.sha_cycle(cur, st)
+
+        def ae(k, w):
+            a, b, c, d = old_a[-1], old_a[-2], old_a[-3], old_a[-4]
+            e, f, g, h = old_e[-1], old_e[-2], old_e[-3], old_e[-4]
+            t1 = (h + (rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25)) + ((e & f) ^ (~e & M & g)) + k + w) & M
+            t2 = ((rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c))) & M
+            return (t1 + t2) & M, (d + t1) & M
+        for i in range(4):
+            st["round"] = i
+            step(SHA_LOAD_STATE)
+            a = self.load_u32(sin + 3 - i)
+            e = self.load_u32(sin + 7 - i)
+            st["a"], st["e"] = bswap(a), bswap(e)
+            old_a.append(st["a"])
+            old_e.append(st["e"])
+            self.store_u32(sout + 3 - i, a)
+            self.store_u32(sout + 7 - i, e)
+        while st["count"]:
+            for i in range(16):
+                st["round"] = i
+                step(SHA_LOAD_DATA)
+                k = self.load_u32(kad + i)
+                st["w"] = bswap(self.load_u32(st["data_addr"]))
+                st["data_addr"] += 1
+                old_w.append(st["w"])
+                st["a"], st["e"] = ae(k, st["w"])
+                old_a.append(st["a"])
+                old_e.append(st["e"])
+            for i in range(48):
+                st["round"] = i
+                step(SHA_MIX)
+                k = self.load_u32(kad + 16 + i)
+                w2, w7, w15, w16 = old_w[-2], old_w[-7], old_w[-15], old_w[-16]
+                s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10)
+                s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3)
+                st["w"] = (s1 + w7 + s0 + w16) & M
+                old_w.append(st["w"])
+                st["a"], st["e"] = ae(k, st["w"])
+                old_a.append(st["a"])
+                old_e.append(st["e"])
+            for i in range(4):
+                st["round"] = i
+                step(SHA_STORE_STATE)
+                st["a"] = (old_a[-4] + old_a[-68]) & M
+                st["e"] = (old_e[-4] + old_e[-68]) & M
+                st["w"] = 0
+                if i == 3:
+                    st["count"] -= 1
+                old_a.append(st["a"])
+                old_e.append(st["e"])
+                self.store_u32(sout + 3 - i, bswap(st["a"]))
+                self.store_u32(sout + 7 - i, bswap(st["e"]))
+            del old_a[:-68], old_e[:-68], old_w[:-16]
+        st["round"] = 0
+        step(DECODE)
 
     def store_u8(self, addr, byte):  # Risc0Context::store_u8 (r0vm.rs:125-133)
         w = self.load_u32(addr // 4)
@@ -891,6 +974,14 @@ class Trace:
             elif back is not None and back[0] == "ecall":
                 for col, v in zip(lay["ecall_s"], back[1]):
                     put(row, col, v)
+            elif back is not None and back[0] == "sha2":  # fp_array, then u32 bits (witgen/mod.rs:253-260)
+                st = back[1]
+                for col, v in zip(lay["sha2_fp"], (st["state_in_addr"], st["state_out_addr"], st["data_addr"],
+                                                   st["count"], st["k_addr"], st["round"], st["next_state"])):
+                    put(row, col, v)
+                for col, v in zip(lay["sha2_u32"], (st["a"], st["e"], st["w"])):
+                    for b in range(32):
+                        put(row, col + b, (v >> b) & 1)
             put(row, lay["cycle"], row)
             put(row, lay["next_pc_low"], cyc[1] & 0xFFFF)
             put(row, lay["next_pc_high"], cyc[1] >> 16)
@@ -1061,12 +1152,24 @@ def li(rd, value):
     return [asm("lui", rd, hi & 0xFFFFF), asm("addi", rd, rd, lo - (0x1000 if lo & 0x800 else 0))]
 
 
-def ecall_trace(po2, seed=1, n_user=60, data_base=0x00100000, terminate=True):
+SHA256_K = [
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5, 0xd807aa98,
+    0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174, 0xe49b69c1, 0xefbe4786,
+    0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da, 0x983e5152, 0xa831c66d, 0xb00327c8,
+    0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967, 0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13,
+    0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85, 0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819,
+    0xd6990624, 0xf40e3585, 0x106aa070, 0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a,
+    0x5b9cca4f, 0x682e6ff3, 0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7,
+    0xc67178f2]
+
+
+def ecall_trace(po2, seed=1, n_user=60, data_base=0x00100000, terminate=True, sha=True):
     """user code that traps into a machine-mode kernel twice through `ecall` (Poseidon2 buffer
     registers as byte addresses). The first entry
     runs a Poseidon2 ecall with state (is_elem 0, two blocks), one without state on field
     elements, a host write and an unaligned host read, then `mret`s back; the second entry
-    terminates (or, terminate=False, `mret`s again and the program runs off its end)."""
+    terminates (or, terminate=False, `mret`s again and the program runs off its end). sha: the
+    first entry also runs a two-block SHA-256 ecall."""
     rng = np.random.default_rng(seed)
     user = random_program(rng, n_user, data_base) + [asm("ecall")] + random_program(rng, n_user, data_base)[1:] + \
         [asm("lui", 31, data_base >> 12), asm("ecall")] + random_program(rng, 20, data_base)[1:]
@@ -1085,6 +1188,10 @@ def ecall_trace(po2, seed=1, n_user=60, data_base=0x00100000, terminate=True):
                                                            asm("ecall")]
     body += [asm("addi", 10, 0, 0)] + li(11, data_base + 301) + [asm("addi", 12, 0, 23), asm("addi", 17, 0, 1),
                                                                  asm("ecall")]
+    # SHA-256 compression of two blocks: a0 state in, a1 state out, a2 data, a3 count, a4 K table
+    if sha:
+        body += li(10, data_base + 4 * 208) + li(11, data_base + 4 * 216) + li(12, data_base + 4 * 160) + \
+            li(13, 2) + li(14, data_base + 0x400) + [asm("addi", 17, 0, 4), asm("ecall")]
     body += [asm("mret")]
     second = [asm("addi", 17, 0, 0), asm("ecall")] if terminate else [asm("mret")]
     k += [asm("bge", 5, 6, 4 * (len(body) + 1))] + body + second
@@ -1093,6 +1200,8 @@ def ecall_trace(po2, seed=1, n_user=60, data_base=0x00100000, terminate=True):
         data[data_base + 4 * (128 + i)] = int(rng.integers(0, P))
     for i in range(8):  # the sponge state: field elements
         data[data_base + 4 * (200 + i)] = int(rng.integers(0, P))
+    for i, k_ in enumerate(SHA256_K):  # the SHA-256 round constants the kernel points a4 at
+        data[data_base + 0x400 + 4 * i] = k_
     regs = {r: int(rng.integers(0, 1 << 32)) for r in range(1, 31)}
     mregs = {5: 0}
     return Trace(po2, user, data=data, regs=regs, seed=seed, kernel=k, machine_regs=mregs,

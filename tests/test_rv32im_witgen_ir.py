@@ -53,7 +53,7 @@ def test_ir_matches_reference_with_ecalls(terminate):
     assert t.terminated == terminate
     data, glob, cyc, tx = W.inputs(t)
     majors = set(int(m) for m in cyc["major"][:t.table_split_cycle])
-    assert {0, 1, 7, 8, 9, 10} <= majors
+    assert {0, 1, 7, 8, 9, 10, 11} <= majors
     ref_d, ref_g = W.run(data, glob, cyc, tx, t.table_split_cycle, 1 << 14)
     d, g = I.witgen(data.copy(), glob.copy(), cyc.copy(), tx, 1 << 14)
     assert np.array_equal(d, ref_d) and np.array_equal(g, ref_g)

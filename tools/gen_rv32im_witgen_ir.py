@@ -443,6 +443,10 @@ def layout_offsets(lay):
     p2 = [leaf(st[f]) for f in names] + [leaf(c) for c in d(st["inner"])]
     z = leaf(st["zcheck"])
     out["poseidon2_state"] = p2 + [z, z + 1, z + 2, z + 3]
+    sha = d(d(res["arm11"])["state"])  # Sha2State::fp_offsets / u32_offsets (witgen/sha2.rs:28-50)
+    out["sha2_fp"] = [leaf(sha[f]) for f in ("stateInAddr", "stateOutAddr", "dataAddr", "count", "kAddr", "round",
+                                              "nextState")]
+    out["sha2_u32"] = [leaf(d(sha[f])[0]) for f in ("a", "e", "w")]
     g = lay.get("kLayoutGlobal")
 
     def u32s(name):
