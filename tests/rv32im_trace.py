@@ -49,6 +49,8 @@ ECALL_DISPATCH_WADDR = 0xFFFF1000 // 4
 MAX_IO_BYTES, MAX_IO_WORDS = 1024, 4
 PFLAG_IS_ELEM, PFLAG_CHECK_OUT = 0x80000000, 0x40000000
 REG_A0, REG_A1, REG_A2, REG_A3, REG_A7 = 10, 11, 12, 13, 17
+REG_T0, REG_T1, REG_T2, REG_T3 = 5, 6, 7, 28
+USER_BIGINT_END_WADDR = 0xBFFF0000 // 4
 LOOKUP_TABLE_CYCLES = ((1 << 8) + (1 << 16)) // 16
 RESERVED_CYCLES = LOOKUP_TABLE_CYCLES + 1
 REG_MAX = 32
@@ -58,6 +60,7 @@ LOAD_ROOT_AND_NONCE, RESUME, SUSPEND, STORE_ROOT, CONTROL_TABLE, CONTROL_DONE = 
 MACHINE_ECALL, TERMINATE, HOST_READ_SETUP, HOST_WRITE, HOST_READ_BYTES, HOST_READ_WORDS = 8, 9, 10, 11, 12, 13
 SHA_ECALL, SHA_LOAD_STATE, SHA_LOAD_DATA, SHA_MIX, SHA_STORE_STATE = 32, 33, 34, 35, 36
 POSEIDON_ENTRY, POSEIDON_PAGING = 16, 22
+BIGINT_ECALL, BIGINT_STEP = 40, 41
 DECODE = 48
 
 CYCLE_DTYPE = np.dtype([("state", "<u4"), ("pc", "<u4"), ("major", "u1"), ("minor", "u1"), ("machineMode", "u1"),
@@ -345,17 +348,80 @@ def ext_add(a, b):
     return [(x + y) % P for x, y in zip(a, b)]
 
 
+# ------------------------------------------------------------------ BigInt (prove/witgen/bigint.rs, byte_poly.rs)
+BI_READ, BI_WRITE, BI_CHECK = range(3)  # MemoryOp (bigint.rs:72-77)
+BI_RESET, BI_SHIFT, BI_SET_TERM, BI_ADD_TOTAL, BI_CARRY1, BI_CARRY2, BI_EQ_ZERO = range(7)  # PolyOp (62-70)
+
+
+def bigint_insn(mem_op, poly_op, reg, offset=0, coeff=0):
+    """Instruction::decode's encoding mmmmppppcccaaaaaoooooooooooooooo (bigint.rs:79-95)"""
+    return mem_op << 28 | poly_op << 24 | (coeff + 4) << 21 | reg << 16 | offset
+
+
+def _bp_add(a, b):
+    n = max(len(a), len(b))
+    return [(a[i] if i < len(a) else 0) + (b[i] if i < len(b) else 0) for i in range(n)]
+
+
+def _bp_mul(a, b):  # lengths in lanes: chunks add up (byte_poly.rs:226-252)
+    r = [0] * (len(a) + len(b))
+    for i, x in enumerate(a):
+        for j, y in enumerate(b):
+            r[i + j] += x * y
+    return r
+
+
+class BytePolyProgram:
+    """BytePolyProgram (byte_poly.rs:32-123): polynomials as coefficient lists whose length
+    is a multiple of the 4-lane chunk, as the reference's SmallVec of i32x4"""
+
+    def __init__(self):
+        self.in_carry = False
+        self.total_carry = []
+        self.reset()
+
+    def reset(self):
+        self.poly, self.term, self.total = [0] * 4, [1, 0, 0, 0], [0] * 4
+
+    def step(self, poly_op, coeff, witness):
+        delta = list(witness)
+        new_poly = _bp_add(self.poly, delta)
+        if poly_op == BI_RESET:
+            self.reset()
+        elif poly_op == BI_SHIFT:
+            self.poly = [0] * 16 + new_poly
+        elif poly_op == BI_SET_TERM:
+            self.poly, self.term = [0] * 4, new_poly
+        elif poly_op == BI_ADD_TOTAL:
+            self.total = _bp_add(self.total, [x * coeff for x in _bp_mul(new_poly, self.term)])
+            self.term, self.poly = [1, 0, 0, 0], [0] * 4
+        elif poly_op == BI_CARRY1:
+            self.poly = _bp_add(self.poly, [(d - 128) * 64 * 256 for d in delta])
+        elif poly_op == BI_CARRY2:
+            self.poly = _bp_add(self.poly, [d * 256 for d in delta])
+        else:  # EqZero
+            self.total = _bp_add(self.total, _bp_mul([-256, 1, 0, 0], new_poly))
+            assert not any(self.total), "Invalid eqz in bigint program"
+            self.reset()
+            self.in_carry = False
+        for v in self.poly + self.term + self.total:
+            assert -(1 << 31) <= v < (1 << 31), "i32 overflow"
+
+
 class Trace:
     """the restated preflight of one segment"""
 
     def __init__(self, po2, program, *, base_pc=0x10000, data=None, regs=None, seed=1, max_user_cycles=None,
                  read_nodes=True, discover_cycles=None, kernel=None, kernel_pc=KERNEL_START, machine_regs=None,
-                 read_record=(), write_record=()):
+                 read_record=(), write_record=(), bigint_nondet=None):
         """program: user code at base_pc. kernel: machine-mode code at kernel_pc, entered by a
         user `ecall` through ECALL_DISPATCH_ADDR (r0vm.rs:342-352); it leaves with `mret` or
         a machine ecall (terminate, host read/write, Poseidon2). read_record / write_record:
-        the segment's host-read payloads (bytes) and host-write return values."""
+        the segment's host-read payloads (bytes) and host-write return values. bigint_nondet:
+        the BigInt ecall's nondeterministic witness, f(trace, mode) -> {word address: 16 bytes},
+        standing in for the bibc nondet program's evaluation (execute/bigint.rs:190-194)."""
         self.po2 = po2
+        self.bigint_nondet = bigint_nondet
         self.rng = np.random.default_rng(seed)
         # image: code, data, registers, suspend state, input/output digests
         mem = {}
@@ -436,9 +502,12 @@ class Trace:
         self.term_a0 = self.term_a1 = 0
         self.cur_read = 0
         self.cur_write = 0
+        self.bigint_bytes = []
+        self.bigint_idx = 0
 
     # ---- memory (preflight.rs:571-634)
-    def load_u32(self, addr):
+    def load_u32(self, addr, record=True):
+        """LoadOp::Record (record=False: LoadOp::Load, the page is loaded but no txn is kept)"""
         cycle = 2 * len(self.cycles)
         if addr >= MERKLE_TREE_START_WADDR:
             if addr < MERKLE_TREE_END_WADDR:
@@ -449,6 +518,8 @@ class Trace:
             word = self.mem.get(addr, 0)
             if self.discover:
                 self.touched.add(addr // 256)
+        if not record:
+            return word
         self.orig_words.setdefault(addr, word)
         prev = self.prev_cycle.get(addr, U32_MAX)
         self.prev_cycle[addr] = cycle
@@ -473,9 +544,10 @@ class Trace:
     # ---- cycles (preflight.rs:373-469)
     def add_cycle(self, state, pc, major, minor, paging_idx=0, back=None):
         self.cycles.append([state, pc, major, minor, self.machine_mode, self.user_cycle, self.txn_idx, paging_idx,
-                            0, 0, 0])
+                            self.bigint_idx, 0, 0])
         self.backs.append(back)
         self.txn_idx = len(self.txns)
+        self.bigint_idx = len(self.bigint_bytes)
 
     def add_cycle_special(self, cur, nxt, pc, paging_idx=0, back=None):
         self.add_cycle(nxt, pc, 7 + cur // 8, cur % 8, paging_idx, back)
@@ -687,6 +759,10 @@ class Trace:
             self.pc += 4
             self.ecall_cycle(MACHINE_ECALL, SHA_ECALL)
             self.sha2_ecall()
+        elif a7 == 5:  # ecall_bigint (r0vm.rs:573-584)
+            self.pc += 4
+            self.ecall_cycle(MACHINE_ECALL, BIGINT_ECALL)
+            self.bigint_ecall()
         else:
             raise ValueError(f"machine ecall {a7} is not modelled")
 
@@ -767,6 +843,73 @@ class Trace:
             del old_a[:-68], old_e[:-68], old_w[:-16]
         st["round"] = 0
         step(DECODE)
+
+    def machine_addr(self, reg, record):  # load_aligned_addr_from_machine_register (r0vm.rs:72-78)
+        v = self.load_u32(MACHINE_REGS_WADDR + reg, record)
+        assert v % 4 == 0, "unaligned bigint address"
+        return v // 4
+
+    def bigint_ecall(self):
+        """ecall_preflight (prove/witgen/bigint.rs:241-256) over execute::bigint::ecall
+        (execute/bigint.rs:162-210); the nondet program's witness comes from bigint_nondet"""
+        mode = self.load_u32(MACHINE_REGS_WADDR + REG_T0)
+        assert mode in (0, 1), f"Invalid mode for bigint ecall: {mode}"
+        blob = self.machine_addr(REG_A0, False)
+        nondet = self.machine_addr(REG_T1, False)
+        verify = self.machine_addr(REG_T2, True) - 1
+        consts = self.machine_addr(REG_T3, False)
+        n_nondet, n_verify, n_consts = (self.load_u32(blob + i, False) for i in range(3))
+        for i in range(n_nondet):
+            self.load_u32(nondet + i, False)
+        witness = self.bigint_nondet(self, mode)
+        for i in range(n_verify):
+            self.load_u32(verify + i, False)
+        for i in range(n_consts):
+            self.load_u32(consts + i, False)
+        st = dict(is_ecall=1, mode=mode, pc=verify, poly_op=BI_RESET, coeff=0, bytes=[0] * 16, next_state=BIGINT_STEP)
+        prog = BytePolyProgram()
+        self.bigint_cycle(BIGINT_ECALL, st)
+        while st["next_state"] == BIGINT_STEP:  # BigInt::step (bigint.rs:103-183)
+            st["pc"] += 1
+            insn = self.load_u32(st["pc"])
+            mem_op, poly_op = (insn >> 28) & 0xF, (insn >> 24) & 0xF
+            assert mem_op <= BI_CHECK and poly_op <= BI_EQ_ZERO, "Invalid bigint instruction"
+            coeff, reg, offset = ((insn >> 21) & 7) - 4, (insn >> 16) & 0x1F, insn & 0xFFFF
+            addr = self.machine_addr(reg, True) + offset * 4
+            if mem_op == BI_CHECK and poly_op != BI_RESET:
+                if not prog.in_carry:  # carry propagation
+                    prog.in_carry = True
+                    prog.total_carry = list(prog.total)
+                    carry = 0
+                    for i in range(len(prog.total_carry)):
+                        c = prog.total_carry[i] + carry
+                        assert c % 256 == 0, "bad carry"
+                        prog.total_carry[i] = carry = c // 256
+                for i in range(16):
+                    value = (prog.total_carry[offset * 16 + i] + 128 * 256 * 64) & U32_MAX
+                    st["bytes"][i] = ((value >> 14) & 0xFF if poly_op == BI_CARRY1 else (value >> 8) & 0x3F
+                                      if poly_op == BI_CARRY2 else value & 0xFF)
+                    assert poly_op in (BI_CARRY1, BI_CARRY2, BI_SHIFT, BI_EQ_ZERO), "Invalid poly_op in bigint program"
+            elif mem_op == BI_READ:
+                for i in range(4):
+                    w = self.load_u32(addr + i)
+                    st["bytes"][4 * i:4 * i + 4] = list(w.to_bytes(4, "little"))
+            elif addr != 0:
+                st["bytes"] = list(witness[addr])
+                if mem_op == BI_WRITE:
+                    for i in range(4):
+                        self.store_u32(addr + i, int.from_bytes(bytes(st["bytes"][4 * i:4 * i + 4]), "little"))
+            prog.step(poly_op, coeff, st["bytes"])
+            st["is_ecall"] = 0
+            st["poly_op"] = poly_op
+            st["coeff"] = coeff + 4
+            st["next_state"] = DECODE if poly_op == BI_RESET else BIGINT_STEP
+            self.bigint_cycle(BIGINT_STEP, st)
+
+    def bigint_cycle(self, cur, st):  # on_bigint_cycle (preflight.rs:471-480)
+        self.bigint_bytes.extend(st["bytes"])
+        self.add_cycle_special(cur, st["next_state"], self.pc, 0, ("bigint", dict(st, bytes=list(st["bytes"]))))
+        self.user_cycles += 1
 
     def store_u8(self, addr, byte):  # Risc0Context::store_u8 (r0vm.rs:125-133)
         w = self.load_u32(addr // 4)
@@ -958,6 +1101,16 @@ class Trace:
                 tx[f] = t[:, j]
         return cyc, tx
 
+    def bigint_array(self):
+        """PreflightTrace::bigint_bytes"""
+        return np.array(self.bigint_bytes, np.uint8)
+
+    def bigint_records(self):
+        """the Back::BigInt rows as the accumulation's records [(row, poly_op, coeff, bytes)]
+        (witgen/mod.rs:187-199)"""
+        return [(row, b[1]["poly_op"], b[1]["coeff"], list(b[1]["bytes"])) for row, b in enumerate(self.backs)
+                if b is not None and b[0] == "bigint"]
+
     def injector(self, lay):
         """(rows, cols, plain values) of build_injector (witgen/mod.rs:226-270), in push order"""
         rows, cols, vals = [], [], []
@@ -982,6 +1135,12 @@ class Trace:
                 for col, v in zip(lay["sha2_u32"], (st["a"], st["e"], st["w"])):
                     for b in range(32):
                         put(row, col + b, (v >> b) & 1)
+            elif back is not None and back[0] == "bigint":  # BigIntState::as_array (witgen/bigint.rs:213-238)
+                st = back[1]
+                arr = [st["is_ecall"], st["mode"], st["pc"], st["poly_op"], st["coeff"]] + st["bytes"] + \
+                    [st["next_state"]]
+                for col, v in zip(lay["bigint_state"], arr):
+                    put(row, col, v)
             put(row, lay["cycle"], row)
             put(row, lay["next_pc_low"], cyc[1] & 0xFFFF)
             put(row, lay["next_pc_high"], cyc[1] >> 16)
@@ -1163,13 +1322,45 @@ SHA256_K = [
     0xc67178f2]
 
 
-def ecall_trace(po2, seed=1, n_user=60, data_base=0x00100000, terminate=True, sha=True):
+BIGINT_A, BIGINT_B, BIGINT_C, BIGINT_BLOB, BIGINT_VERIFY, BIGINT_NONDET, BIGINT_CONSTS = \
+    0x800, 0x810, 0x820, 0x900, 0x940, 0x9C0, 0x9E0  # offsets from ecall_trace's data_base
+
+
+def bigint_mul_add_program():
+    """a BigInt verify program checking c = a * b (16-byte a, b; 32-byte c written at a3,
+    chunks 0-1) and d = a + b (written at a3, chunk 2): every PolyOp and MemoryOp, the carries
+    of a two-chunk and a one-chunk total, and the closing Reset. Operands: a1 = a, a2 = b,
+    a3 = c."""
+    I = bigint_insn
+    return [I(BI_READ, BI_SET_TERM, 11), I(BI_READ, BI_ADD_TOTAL, 12, 0, 1),
+            I(BI_WRITE, BI_SHIFT, 13, 1), I(BI_WRITE, BI_ADD_TOTAL, 13, 0, -1),
+            I(BI_CHECK, BI_CARRY1, 13, 1), I(BI_CHECK, BI_CARRY2, 13, 1), I(BI_CHECK, BI_SHIFT, 13, 1),
+            I(BI_CHECK, BI_CARRY1, 13, 0), I(BI_CHECK, BI_CARRY2, 13, 0), I(BI_CHECK, BI_EQ_ZERO, 13, 0),
+            I(BI_READ, BI_ADD_TOTAL, 11, 0, 1), I(BI_READ, BI_ADD_TOTAL, 12, 0, 1),
+            I(BI_WRITE, BI_ADD_TOTAL, 13, 2, -1),
+            I(BI_CHECK, BI_CARRY1, 13, 0), I(BI_CHECK, BI_CARRY2, 13, 0), I(BI_CHECK, BI_EQ_ZERO, 13, 0),
+            I(BI_READ, BI_RESET, 11)]
+
+
+def bigint_mul_add_nondet(tr, mode):
+    """the witness bigint_mul_add_program needs, laid out as BigIntIOImpl::store does
+    (execute/bigint.rs:94-135): 16-byte chunks keyed by word address; operands read with
+    LoadOp::Load"""
+    wa, wb, wc = (tr.machine_addr(r, False) for r in (11, 12, 13))
+    num = lambda w: sum(tr.load_u32(w + i, False) << (32 * i) for i in range(4))
+    a, b = num(wa), num(wb)
+    c, d = (a * b).to_bytes(32, "little"), (a + b).to_bytes(16, "little")
+    return {wc: c[:16], wc + 4: c[16:], wc + 8: d}
+
+
+def ecall_trace(po2, seed=1, n_user=60, data_base=0x00100000, terminate=True, sha=True, bigint=False):
     """user code that traps into a machine-mode kernel twice through `ecall` (Poseidon2 buffer
     registers as byte addresses). The first entry
     runs a Poseidon2 ecall with state (is_elem 0, two blocks), one without state on field
     elements, a host write and an unaligned host read, then `mret`s back; the second entry
     terminates (or, terminate=False, `mret`s again and the program runs off its end). sha: the
-    first entry also runs a two-block SHA-256 ecall."""
+    first entry also runs a two-block SHA-256 ecall. bigint: the first entry also runs a
+    BigInt ecall (bigint_mul_add_program, mode 0)."""
     rng = np.random.default_rng(seed)
     user = random_program(rng, n_user, data_base) + [asm("ecall")] + random_program(rng, n_user, data_base)[1:] + \
         [asm("lui", 31, data_base >> 12), asm("ecall")] + random_program(rng, 20, data_base)[1:]
@@ -1192,6 +1383,13 @@ def ecall_trace(po2, seed=1, n_user=60, data_base=0x00100000, terminate=True, sh
     if sha:
         body += li(10, data_base + 4 * 208) + li(11, data_base + 4 * 216) + li(12, data_base + 4 * 160) + \
             li(13, 2) + li(14, data_base + 0x400) + [asm("addi", 17, 0, 4), asm("ecall")]
+    # BigInt: t0 = mode 0 (the entry counter saved in s1), a0 = blob, t1 = nondet program,
+    # t2 = verify program, t3 = constants; a1, a2, a3 = a, b, c
+    if bigint:
+        B = data_base
+        body += [asm("addi", 9, 5, 0), asm("addi", 5, 0, 0)] + li(10, B + BIGINT_BLOB) + li(6, B + BIGINT_NONDET) + \
+            li(7, B + BIGINT_VERIFY) + li(28, B + BIGINT_CONSTS) + li(11, B + BIGINT_A) + li(12, B + BIGINT_B) + \
+            li(13, B + BIGINT_C) + [asm("addi", 17, 0, 5), asm("ecall"), asm("addi", 5, 9, 0)]
     body += [asm("mret")]
     second = [asm("addi", 17, 0, 0), asm("ecall")] if terminate else [asm("mret")]
     k += [asm("bge", 5, 6, 4 * (len(body) + 1))] + body + second
@@ -1202,7 +1400,19 @@ def ecall_trace(po2, seed=1, n_user=60, data_base=0x00100000, terminate=True, sh
         data[data_base + 4 * (200 + i)] = int(rng.integers(0, P))
     for i, k_ in enumerate(SHA256_K):  # the SHA-256 round constants the kernel points a4 at
         data[data_base + 0x400 + 4 * i] = k_
+    if bigint:
+        prog = bigint_mul_add_program()
+        for i in range(4):  # a, b < 2^127, so a + b fits the 16-byte chunk
+            data[data_base + BIGINT_A + 4 * i] = int(rng.integers(0, 1 << 32)) >> (1 if i == 3 else 0)
+            data[data_base + BIGINT_B + 4 * i] = int(rng.integers(0, 1 << 32)) >> (1 if i == 3 else 0)
+        for i, w in enumerate([2, len(prog), 0]):
+            data[data_base + BIGINT_BLOB + 4 * i] = w
+        for i, w in enumerate(prog):
+            data[data_base + BIGINT_VERIFY + 4 * i] = w
+        for i in range(2):  # a stand-in nondet program (its evaluation is bigint_mul_add_nondet)
+            data[data_base + BIGINT_NONDET + 4 * i] = int(rng.integers(0, 1 << 32))
     regs = {r: int(rng.integers(0, 1 << 32)) for r in range(1, 31)}
     mregs = {5: 0}
     return Trace(po2, user, data=data, regs=regs, seed=seed, kernel=k, machine_regs=mregs,
-                 read_record=[bytes(int(x) for x in rng.integers(0, 256, 23))], write_record=[0, 8, 0])
+                 read_record=[bytes(int(x) for x in rng.integers(0, 256, 23))], write_record=[0, 8, 0],
+                 bigint_nondet=bigint_mul_add_nondet if bigint else None)

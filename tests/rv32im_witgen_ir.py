@@ -178,7 +178,7 @@ class Ctx:
     def __init__(self, data, glob, rows, cycles, txns, bigint=None):
         self.data, self.glob, self.rows = data, glob, rows
         self.cycles, self.txns = cycles, txns
-        self.bigint = bigint if bigint is not None else np.zeros(0, np.uint8)
+        self.bigint_bytes = bigint if bigint is not None else np.zeros(0, np.uint8)
         self.u8 = np.zeros(1 << 8, np.int64)
         self.u16 = np.zeros(1 << 16, np.int64)
         self.strings = step_fn()[1]
@@ -259,7 +259,9 @@ class Ctx:
 
     def bigint(self, cycle):
         i = int(self.cycles["bigintIdx"][cycle])
-        return tuple(enc(int(b)) for b in self.bigint[i:i + 16])
+        if i + 16 > len(self.bigint_bytes):
+            raise WitgenError("bigint bytes past the preflight's")
+        return tuple(enc(int(b)) for b in self.bigint_bytes[i:i + 16])
 
 
 def witgen(data, glob, cycles, txns, rows, bigint=None):

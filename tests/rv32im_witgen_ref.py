@@ -9,6 +9,7 @@ import os
 
 import numpy as np
 
+import bigint_accum as BA
 import rv32im_accum_ref as RA
 import rv32im_trace as T
 
@@ -74,13 +75,18 @@ def prove_from_trace(trace, suite, oracle, mode=MODE_SEQ_FORWARD):
     accum words zeroized. Returns (seal, mix, data, global, accum)."""
     rows = 1 << trace.po2
     data, glob, cyc, tx = inputs(trace)
-    d, g = run(data, glob, cyc, tx, trace.table_split_cycle, rows, mode)
+    d, g = run(data, glob, cyc, tx, trace.table_split_cycle, rows, mode, trace.bigint_array())
     d = np.where(d == INVALID, 0, d).astype(np.uint32)
     g = np.where(g == INVALID, 0, g).astype(np.uint32)
     code = np.zeros(rows, np.uint32)
 
+    records = trace.bigint_records()
+
     def fill(mix):
-        acc = RA.accum(d, g, mix, rows, rows)
+        init = None
+        if records:  # WitnessGenerator::accum's BigIntAccum injection (witgen/mod.rs:187-205)
+            init = BA.inject(np.full(RA.ACCUM_COLS * rows, INVALID, np.uint32), rows, mix, records)
+        acc = RA.accum(d, g, mix, rows, rows, accum_init=init)
         return np.where(acc == INVALID, 0, acc).astype(np.uint32)
     seal, mix, _, acc = oracle.prove_segment_cb("rv32im", suite, trace.po2, code, d, g, fill, RA.ACCUM_COLS * rows,
                                                 version=2)
@@ -91,21 +97,23 @@ def witgen(trace, mode=MODE_SEQ_FORWARD, lay=None):
     """(data, global) after the reference's witness generation; raises RuntimeError with the
     reference's message when it throws"""
     data, glob, cyc, tx = inputs(trace, lay)
-    return run(data, glob, cyc, tx, trace.table_split_cycle, 1 << trace.po2, mode)
+    return run(data, glob, cyc, tx, trace.table_split_cycle, 1 << trace.po2, mode, trace.bigint_array())
 
 
-def run(data, glob, cyc, tx, split, rows, mode=MODE_SEQ_FORWARD):
+def run(data, glob, cyc, tx, split, rows, mode=MODE_SEQ_FORWARD, bigint=None):
     data = np.array(data, np.uint32)
     glob = np.array(glob, np.uint32)
     cyc = np.array(cyc)  # the reference advances txnIdx in place
     tx = np.ascontiguousarray(tx)
-    bigint = np.zeros(16, np.uint8)
+    n_bigint = 0 if bigint is None else len(bigint)
+    bigint = np.concatenate([np.zeros(0, np.uint8) if bigint is None else np.asarray(bigint, np.uint8),
+                             np.zeros(16, np.uint8)])
     lib = C.CDLL(RA.LIB)
     f = lib.risc0_circuit_rv32im_cpu_witgen
     f.restype = C.c_void_p
     f.argtypes = [C.c_uint32, C.POINTER(ExecBuffers), C.POINTER(RA.PreflightTrace), C.c_uint32]
     bufs = ExecBuffers(RA.Buffer(glob.ctypes.data, 1, GLOBAL_WORDS, True), RA.Buffer(data.ctypes.data, rows, DATA_COLS, True))
-    pf = RA.PreflightTrace(cyc.ctypes.data, tx.ctypes.data, bigint.ctypes.data, len(tx), 0, split)
+    pf = RA.PreflightTrace(cyc.ctypes.data, tx.ctypes.data, bigint.ctypes.data, len(tx), n_bigint, split)
     err = f(mode, C.byref(bufs), C.byref(pf), rows)
     if err:
         raise RuntimeError(C.cast(err, C.c_char_p).value.decode())

@@ -18,11 +18,11 @@ def hal():
     return r.HipHal("poseidon2")
 
 
-def gpu_witgen(hal, data, glob, cyc, tx, split, mode=0):
+def gpu_witgen(hal, data, glob, cyc, tx, split, mode=0, bigint=None):
     import risc0_amd as r
     dd = hal.copy_from_elem("data", data)
     dg = hal.copy_from_elem("global", glob)
-    r.rv32im_witgen(dd, dg, cyc, tx, split, mode=mode)
+    r.rv32im_witgen(dd, dg, cyc, tx, split, bigint=bigint, mode=mode)
     return dd.to_numpy(), dg.to_numpy()
 
 
@@ -38,15 +38,22 @@ def test_rv32im_witgen_matches_reference(hal, po2, n, seed):
     assert (d == W.INVALID).any()  # columns no arm of a row writes stay INVALID, as in the reference
 
 
-@pytest.mark.parametrize("terminate", [True, False])
-def test_rv32im_witgen_ecalls_match_reference(hal, terminate):
+@pytest.mark.parametrize("terminate,bigint", [(True, True), (False, False)])
+def test_rv32im_witgen_ecalls_match_reference(hal, terminate, bigint):
     """machine-mode rows: user ecall, Poseidon2 ecalls (state / no state, bytes / elements),
-    host write, unaligned host read, mret, terminate"""
-    t = T.ecall_trace(14, seed=3, terminate=terminate)
+    host write, unaligned host read, SHA-256, mret, terminate, and a BigInt ecall (arm 12:
+    every PolyOp and MemoryOp, the witness bytes from the trace's bigint array)"""
+    import risc0_amd as r
+    t = T.ecall_trace(14, seed=3, terminate=terminate, bigint=bigint)
     data, glob, cyc, tx = W.inputs(t)
-    ref_d, ref_g = W.run(data, glob, cyc, tx, t.table_split_cycle, 1 << 14)
-    d, g = gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle)
+    bi = t.bigint_array()
+    assert (12 in set(cyc["major"][:t.table_split_cycle].tolist())) == bigint
+    ref_d, ref_g = W.run(data, glob, cyc, tx, t.table_split_cycle, 1 << 14, bigint=bi)
+    d, g = gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle, bigint=bi)
     assert np.array_equal(d, ref_d) and np.array_equal(g, ref_g)
+    if bigint:  # a bigint array shorter than the cycles' bigintIdx + 16 is refused, not read past
+        with pytest.raises(r.R0HipError, match="bigint bytes past"):
+            gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle, bigint=bi[:-8])
 
 
 def test_rv32im_witgen_modes(hal):
@@ -96,12 +103,14 @@ def test_prove_segment_trace_matches_oracle(po2, n, suite, seed, oracle):
     rows satisfy the circuit, so the seal verifies with the validity equation."""
     import risc0_amd as r
     h = r.HipHal(suite)
-    t = T.random_trace(po2, n, seed=seed) if n else T.ecall_trace(po2, seed=seed)  # n = 0: the ecall trace
+    # n = 0: the ecall trace, with a BigInt ecall whose accumulator states the prover injects
+    t = T.random_trace(po2, n, seed=seed) if n else T.ecall_trace(po2, seed=seed, bigint=True)
     s = {"poseidon2": oracle.POSEIDON2, "sha-256": oracle.SHA256}[suite]
     ref_seal, ref_mix, _, _, _ = W.prove_from_trace(t, s, oracle)
     cyc, tx = t.arrays()
     idx, off, val = W.injector_arrays(t)
-    seal, mix = r.prove_segment_trace(h, po2, W.global_words(t), idx, off, val, cyc, tx, t.table_split_cycle)
+    seal, mix = r.prove_segment_trace(h, po2, W.global_words(t), idx, off, val, cyc, tx, t.table_split_cycle,
+                                      bigint=t.bigint_array(), bigint_records=t.bigint_records())
     assert np.array_equal(mix, ref_mix)
     assert seal.size == ref_seal.size and np.array_equal(seal, ref_seal)
     assert r.verify_seal("rv32im", h.suite, seal, check_validity=True) == po2
@@ -142,4 +151,14 @@ def test_prove_segment_trace_resident_matches_host_path(hal):
         x.join()
     for s2, m2 in out:
         assert np.array_equal(s2, seal) and np.array_equal(m2, mix)
+    assert r.verify_seal("rv32im", hal.suite, seal, check_validity=True) == 14
+    # with BigInt bytes resident too
+    te = T.ecall_trace(14, seed=6, bigint=True)
+    cyc, tx = te.arrays()
+    idx, off, val = W.injector_arrays(te)
+    args = (W.global_words(te), idx, off, val, cyc, tx, te.table_split_cycle)
+    seal, mix = r.prove_segment_trace(hal, 14, *args, bigint=te.bigint_array(), bigint_records=te.bigint_records())
+    rt = r.ResidentTrace(hal, 14, *args, bigint=te.bigint_array())
+    s2, m2 = r.prove_segment_trace_resident(hal, rt, bigint_records=te.bigint_records())
+    assert np.array_equal(s2, seal) and np.array_equal(m2, mix)
     assert r.verify_seal("rv32im", hal.suite, seal, check_validity=True) == 14

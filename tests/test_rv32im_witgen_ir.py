@@ -45,17 +45,20 @@ def test_ir_matches_reference(po2, n, seed):
 
 
 @needs_ref
-@pytest.mark.parametrize("terminate", [True, False])
-def test_ir_matches_reference_with_ecalls(terminate):
+@pytest.mark.parametrize("terminate,bigint", [(True, True), (False, False)])
+def test_ir_matches_reference_with_ecalls(terminate, bigint):
     """user ecalls into a machine-mode kernel: Poseidon2 ecalls (with and without state, bytes
-    and field elements), host write, an unaligned host read, mret, and terminate"""
-    t = T.ecall_trace(14, seed=3, terminate=terminate)
+    and field elements), host write, an unaligned host read, SHA-256, mret, terminate, and a
+    BigInt ecall (every PolyOp and MemoryOp; its witness bytes in the trace's bigint array)"""
+    t = T.ecall_trace(14, seed=3, terminate=terminate, bigint=bigint)
     assert t.terminated == terminate
     data, glob, cyc, tx = W.inputs(t)
     majors = set(int(m) for m in cyc["major"][:t.table_split_cycle])
-    assert {0, 1, 7, 8, 9, 10, 11} <= majors
-    ref_d, ref_g = W.run(data, glob, cyc, tx, t.table_split_cycle, 1 << 14)
-    d, g = I.witgen(data.copy(), glob.copy(), cyc.copy(), tx, 1 << 14)
+    assert {0, 1, 7, 8, 9, 10, 11} <= majors and (12 in majors) == bigint
+    bi = t.bigint_array()
+    assert len(bi) == 16 * (12 in majors) * 18
+    ref_d, ref_g = W.run(data, glob, cyc, tx, t.table_split_cycle, 1 << 14, bigint=bi)
+    d, g = I.witgen(data.copy(), glob.copy(), cyc.copy(), tx, 1 << 14, bigint=bi)
     assert np.array_equal(d, ref_d) and np.array_equal(g, ref_g)
 
 
@@ -109,8 +112,8 @@ def test_trace_seal_verifies_with_validity(oracle):
     t = T.random_trace(13, 250, seed=21)
     seal, mix, d, g, acc = W.prove_from_trace(t, oracle.POSEIDON2, oracle)
     assert r.verify_seal("rv32im", r.POSEIDON2, seal, check_validity=True) == 13
-    # a terminating segment with machine-mode ecalls is valid too
-    te = T.ecall_trace(14, seed=4, terminate=True)
+    # a terminating segment with machine-mode ecalls (BigInt included) is valid too
+    te = T.ecall_trace(14, seed=4, terminate=True, bigint=True)
     seal_e, _, _, _, _ = W.prove_from_trace(te, oracle.POSEIDON2, oracle)
     assert r.verify_seal("rv32im", r.POSEIDON2, seal_e, check_validity=True) == 14
     rows = 1 << 13

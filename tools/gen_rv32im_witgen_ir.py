@@ -447,6 +447,9 @@ def layout_offsets(lay):
     out["sha2_fp"] = [leaf(sha[f]) for f in ("stateInAddr", "stateOutAddr", "dataAddr", "count", "kAddr", "round",
                                               "nextState")]
     out["sha2_u32"] = [leaf(d(sha[f])[0]) for f in ("a", "e", "w")]
+    bi = d(d(res["arm12"])["state"])  # BigIntState::offsets (witgen/bigint.rs:185-211)
+    out["bigint_state"] = [leaf(bi[f]) for f in ("isEcall", "mode", "pc", "polyOp", "coeff")] + \
+        [leaf(b) for b in d(bi["bytes"])] + [leaf(bi["nextState"])]
     g = lay.get("kLayoutGlobal")
 
     def u32s(name):
