@@ -180,6 +180,7 @@ def main():
         t_w, seal_w, _ = timed_leg(prove_witness, "prove_only")
     else:
         t, seal, mix = timed_leg(prove_witness, "prove")
+    mem = r.mem_stats()  # this rank's device footprint with k segments in flight
     # host-side gather of one seal digest per rank (the receipts stay on their hosts)
     digests = gather_results({rank: hashlib.sha256(seal.tobytes()).hexdigest()[:16]}, dist)
     # ranks that had to share a device (segments.narrow_visible_devices, or the rehearsal switch)
@@ -244,6 +245,8 @@ def main():
                        "ranks_share_devices": any(shared[i] for i in range(world))},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "device_memory_gb": {"peak_reserved": round(mem["peak_reserved"] / 1e9, 2),
+                                 "peak_live": round(mem["peak_live"] / 1e9, 2)},
         }
         if prove_only:
             line["prove_only"] = prove_only
