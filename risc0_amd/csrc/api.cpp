@@ -301,6 +301,8 @@ const char* r0hip_rv32im_witgen(uint32_t mode, const r0hip_raw_exec_buffers* buf
   });
 }
 
+}  // extern "C"
+
 namespace {
 
 // SegmentProverImpl::prove_core from a preflight (circuit/rv32im/src/prove/hal/mod.rs:143-224):
@@ -371,6 +373,8 @@ void seal_out(const std::vector<uint32_t>& seal, const std::vector<uint32_t>& mi
 }
 
 }  // namespace
+
+extern "C" {
 
 const char* r0hip_prove_segment_trace(int suite, uint32_t po2, uint32_t mode, const uint32_t* h_global,
                                       const uint32_t* h_inj_index, size_t inj_rows, const uint32_t* h_inj_offsets,

@@ -105,6 +105,8 @@ enum ScratchSlot : int {
   kSlotRvwgBigint = 77,
   kSlotRvwgLists = 78,
   kSlotRvwgTables = 79,
+  kSlotRvwgKeys = 83,
+  kSlotRvwgSortTemp = 84,
   // r0hip_prove_segment_trace (api.cpp): the injector's index, offsets and values
   kSlotRvInjIndex = 80,
   kSlotRvInjOffsets = 81,

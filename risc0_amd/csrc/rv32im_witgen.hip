@@ -19,8 +19,11 @@
 // already resident (rv32im_witgen_dev). The cycles are bucketed on the device (counts, one
 // 27-word read-back for the launch sizes, fill). Checks that throw in the reference record an
 // error code and the cycle, raised after the kernels drain.
+#include <cstdlib>
 #include <string>
 #include <vector>
+
+#include <hipcub/hipcub.hpp>
 
 #include "devmem.h"
 #include "rv32im_witgen.h"
@@ -61,18 +64,25 @@ constexpr uint32_t kBins = 2 * rvwg::kMajors;  // (phase, major)
 constexpr uint32_t kBucketThreads = 256;
 
 // per (phase, instruction arm) cycle counts; a major outside the 13 arms is an error (the
-// reference's OneHot EQZ on majorOnehot fails for it)
-__global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(rvwg::Args A, uint32_t split, uint32_t* counts) {
+// reference's OneHot EQZ on majorOnehot fails for it). keys/vals (optional): each cycle's bin
+// and index, for the stable sort into cycle order within each bin.
+__global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(rvwg::Args A, uint32_t split, uint32_t* counts,
+                                                                     uint8_t* keys, uint32_t* vals) {
   __shared__ uint32_t h[kBins];
   if (threadIdx.x < kBins) h[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t c = blockIdx.x * kBucketThreads + threadIdx.x;
   if (c < A.ncycles) {
     const uint32_t m = A.cycles[c].major;
+    const uint32_t b = (c >= split) * rvwg::kMajors + m;
     if (m >= rvwg::kMajors)
       rvwg::fail(A, rvwg::kErrMajor, c, m);
     else
-      atomicAdd(&h[(c >= split) * rvwg::kMajors + m], 1u);
+      atomicAdd(&h[b], 1u);
+    if (keys) {
+      keys[c] = uint8_t(m >= rvwg::kMajors ? kBins : b);
+      vals[c] = c;
+    }
   }
   __syncthreads();
   if (threadIdx.x < kBins && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
@@ -123,11 +133,25 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
   uint32_t* counts = A.err + 4;
   uint32_t* cursor = counts + kBins;
   const uint32_t g = (last_cycle + kBucketThreads - 1) / kBucketThreads;
-  // the two phases' cycles bucketed by instruction arm (count, host offsets, fill)
+  // the two phases' cycles bucketed by instruction arm: counts (one read-back for the launch
+  // sizes), then either a stable radix sort of (bin, cycle) — each bucket in cycle order, so a
+  // wave's lanes write nearby rows of each data column — or atomic cursors (R0_RVWG_SORT=0:
+  // arbitrary order within a bucket)
+  static const bool sorted = [] {
+    const char* e = std::getenv("R0_RVWG_SORT");
+    return !(e && e[0] == '0');
+  }();
+  uint8_t* keys = nullptr;
+  uint32_t* vals = nullptr;
+  if (sorted) {
+    auto* kb = static_cast<uint8_t*>(scratch(size_t(last_cycle) * 6 + 64, kSlotRvwgKeys));
+    keys = kb;
+    vals = reinterpret_cast<uint32_t*>(kb + ((size_t(last_cycle) * 2 + 15) & ~size_t(15)));
+  }
   uint32_t h[4 + kBins];
   {
     KScope ks("rv32im_witgen_bucket", double(last_cycle) * 2 * sizeof(PreflightCycle));
-    hipLaunchKernelGGL(bucket_count_kernel, dim3(g), dim3(kBucketThreads), 0, s, A, table_split, counts);
+    hipLaunchKernelGGL(bucket_count_kernel, dim3(g), dim3(kBucketThreads), 0, s, A, table_split, counts, keys, vals);
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(h, A.err, sizeof(h), hipMemcpyDeviceToHost, s));  // err[0..2], pad, counts
     HIP_OK(hipStreamSynchronize(s));
@@ -138,9 +162,17 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
   off[0] = 0;
   for (uint32_t b = 0; b < kBins; b++) off[b + 1] = off[b] + cnt[b];
   R0_REQUIRE(off[kBins] == last_cycle, "rv32im witgen: bucket counts do not add up");
-  upload_async(cursor, off, kBins * 4);
-  hipLaunchKernelGGL(bucket_fill_kernel, dim3(g), dim3(kBucketThreads), 0, s, A, table_split, cursor, d_list);
-  HIP_OK(hipGetLastError());
+  if (sorted) {
+    uint8_t* keys_out = keys + last_cycle;
+    size_t temp_bytes = 0;
+    HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, keys_out, vals, d_list, int(last_cycle), 0, 5, s));
+    void* temp = scratch(temp_bytes + 256, kSlotRvwgSortTemp);
+    HIP_OK(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys_out, vals, d_list, int(last_cycle), 0, 5, s));
+  } else {
+    upload_async(cursor, off, kBins * 4);
+    hipLaunchKernelGGL(bucket_fill_kernel, dim3(g), dim3(kBucketThreads), 0, s, A, table_split, cursor, d_list);
+    HIP_OK(hipGetLastError());
+  }
   for (int p = 0; p < 2; p++) {
     KScope ks(p ? "rv32im_witgen_tables" : "rv32im_witgen_exec",
               double(off[(p + 1) * kMajors] - off[p * kMajors]) * (4.0 * 211 + sizeof(PreflightCycle)));

@@ -1,10 +1,15 @@
-# tests for the new paths, the default bench, then a Merkle-top A/B (quads for layers <= 128 vs <= 512)
+# tests for the new paths, the witgen micro-bench (sorted vs atomic buckets), the default bench,
+# then a Merkle-top A/B (quads for layers <= 128 vs <= 512)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r4e; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests/test_rv32im_witgen_gpu.py -v -m gpu --timeout 400 --timeout-method thread > $O/pytest_witgen.log 2>&1
 rc=$?
 tail -15 $O/pytest_witgen.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+for s in 1 0; do
+  R0_RVWG_SORT=$s timeout -k 10 300 python -u tools/micro/rv32im_witgen_bench.py 20 5 > $O/witgen_sort$s.json 2> $O/witgen_sort$s.err || { tail -30 $O/witgen_sort$s.err; exit 1; }
+  cat $O/witgen_sort$s.json
+done
 timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
 cat $O/bench.json
 for q in 128 512 128 512; do
