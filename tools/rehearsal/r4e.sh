@@ -10,6 +10,7 @@ for s in 1 0; do
   R0_RVWG_SORT=$s timeout -k 10 300 python -u tools/micro/rv32im_witgen_bench.py 20 5 > $O/witgen_sort$s.json 2> $O/witgen_sort$s.err || { tail -30 $O/witgen_sort$s.err; exit 1; }
   cat $O/witgen_sort$s.json
 done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/wgstats -o run -- python3 tools/micro/rv32im_witgen_bench.py 20 3 --no-ref > $O/wgstats.log 2>&1 || { tail -20 $O/wgstats.log; exit 1; }
 timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
 cat $O/bench.json
 for q in 128 512 128 512; do
