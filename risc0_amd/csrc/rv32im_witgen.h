@@ -132,8 +132,10 @@ __device__ __forceinline__ uint32_t host_word(const Args& A, uint32_t cycle, uin
   return from_u32(A.txns[cur].word);
 }
 
-// LookupTables::lookupDelta (tables.h:33-53; the count argument is not used there either)
-__device__ __forceinline__ void lookup_delta(const Args& A, uint32_t cycle, uint32_t table_w, uint32_t index_w) {
+// LookupTables::lookupDelta (tables.h:33-53; the count argument is not used there either);
+// u8 counts go to the workgroup's LDS copy h8, flushed by the kernel's last lines
+__device__ __forceinline__ void lookup_delta(const Args& A, uint32_t cycle, uint32_t table_w, uint32_t index_w,
+                                             uint32_t* h8) {
   const uint32_t table = to_u32(table_w), index = to_u32(index_w);
   if (table == 0u) return;
   if (table != 8u && table != 16u) {
@@ -144,7 +146,10 @@ __device__ __forceinline__ void lookup_delta(const Args& A, uint32_t cycle, uint
     fail(A, kErrLookupIndex, cycle, index);
     return;
   }
-  atomicAdd((table == 8u ? A.u8 : A.u16) + index, 1u);
+  if (table == 8u)
+    atomicAdd(h8 + index, 1u);
+  else
+    atomicAdd(A.u16 + index, 1u);
 }
 
 // LookupTables::lookupCurrent (tables.h:55-66)

@@ -67,7 +67,7 @@ constexpr uint32_t kBucketThreads = 256;
 // reference's OneHot EQZ on majorOnehot fails for it). keys/vals (optional): each cycle's bin
 // and index, for the stable sort into cycle order within each bin.
 __global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(rvwg::Args A, uint32_t split, uint32_t* counts,
-                                                                     uint8_t* keys, uint32_t* vals) {
+                                                                     uint8_t* keys, uint32_t* vals, bool by_minor) {
   __shared__ uint32_t h[kBins];
   if (threadIdx.x < kBins) h[threadIdx.x] = 0;
   __syncthreads();
@@ -80,7 +80,8 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(rvwg::Args
     else
       atomicAdd(&h[b], 1u);
     if (keys) {
-      keys[c] = uint8_t(m >= rvwg::kMajors ? kBins : b);
+      const uint32_t key = m >= rvwg::kMajors ? kBins : b;
+      keys[c] = uint8_t(by_minor ? key * 8u + (A.cycles[c].minor & 7u) : key);
       vals[c] = c;
     }
   }
@@ -136,11 +137,13 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
   // the two phases' cycles bucketed by instruction arm: counts (one read-back for the launch
   // sizes), then either a stable radix sort of (bin, cycle) — each bucket in cycle order, so a
   // wave's lanes write nearby rows of each data column — or atomic cursors (R0_RVWG_SORT=0:
-  // arbitrary order within a bucket)
-  static const bool sorted = [] {
+  // arbitrary order within a bucket). R0_RVWG_SORT=2 sorts by (bin, minor, cycle): a wave's
+  // lanes then mostly share the arm's minor mux branch, at the cost of row locality.
+  static const int sort_mode = [] {
     const char* e = std::getenv("R0_RVWG_SORT");
-    return !(e && e[0] == '0');
+    return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
   }();
+  const bool sorted = sort_mode != 0, by_minor = sort_mode == 2;
   uint8_t* keys = nullptr;
   uint32_t* vals = nullptr;
   if (sorted) {
@@ -151,7 +154,8 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
   uint32_t h[4 + kBins];
   {
     KScope ks("rv32im_witgen_bucket", double(last_cycle) * 2 * sizeof(PreflightCycle));
-    hipLaunchKernelGGL(bucket_count_kernel, dim3(g), dim3(kBucketThreads), 0, s, A, table_split, counts, keys, vals);
+    hipLaunchKernelGGL(bucket_count_kernel, dim3(g), dim3(kBucketThreads), 0, s, A, table_split, counts, keys, vals,
+                       by_minor);
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(h, A.err, sizeof(h), hipMemcpyDeviceToHost, s));  // err[0..2], pad, counts
     HIP_OK(hipStreamSynchronize(s));
@@ -165,9 +169,12 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
   if (sorted) {
     uint8_t* keys_out = keys + last_cycle;
     size_t temp_bytes = 0;
-    HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, keys_out, vals, d_list, int(last_cycle), 0, 5, s));
+    const int end_bit = by_minor ? 8 : 5;
+    HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, keys_out, vals, d_list, int(last_cycle), 0,
+                                              end_bit, s));
     void* temp = scratch(temp_bytes + 256, kSlotRvwgSortTemp);
-    HIP_OK(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys_out, vals, d_list, int(last_cycle), 0, 5, s));
+    HIP_OK(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys_out, vals, d_list, int(last_cycle), 0,
+                                              end_bit, s));
   } else {
     upload_async(cursor, off, kBins * 4);
     hipLaunchKernelGGL(bucket_fill_kernel, dim3(g), dim3(kBucketThreads), 0, s, A, table_split, cursor, d_list);
