@@ -134,13 +134,15 @@ def main():
         # guest, restated preflight: tests/rv32im_trace.py) is built and uploaded once, before
         # the timed region.
         sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import rv32im_trace as T
-        import rv32im_witgen_ref as W
+        import rv32im_trace as T  # the input generator: a restated preflight (test infrastructure, no oracle)
         t0 = time.perf_counter()
         trace = T.loop_trace(args.po2, body_len=32, seed=0x5249534330 + rank)
         cyc, tx = trace.arrays()
-        idx, off, val = W.injector_arrays(trace)
-        rt = r.ResidentTrace(hal, args.po2, W.global_words(trace), idx, off, val, cyc, tx, trace.table_split_cycle)
+        idx, off, val = trace.injector_arrays()
+        bi = trace.bigint_array()
+        rt = r.ResidentTrace(hal, args.po2, trace.global_words(), idx, off, val, cyc, tx, trace.table_split_cycle,
+                             bigint=bi if len(bi) else None)
+        bigint_records = trace.bigint_records() or None
         print(f"rank {rank}: trace built in {time.perf_counter() - t0:.1f} s ({trace.table_split_cycle} rows before "
               f"the tables, {len(tx)} memory transactions)", file=sys.stderr)
 
@@ -176,7 +178,8 @@ def main():
         return t, last["seal"], last["mix"]
 
     if trace_mode:
-        t, seal, mix = timed_leg(lambda slot: r.prove_segment_trace_resident(hal, rt), "trace")
+        t, seal, mix = timed_leg(lambda slot: r.prove_segment_trace_resident(hal, rt, bigint_records=bigint_records),
+                                 "trace")
         t_w, seal_w, _ = timed_leg(prove_witness, "prove_only")
     else:
         t, seal, mix = timed_leg(prove_witness, "prove")
@@ -203,7 +206,8 @@ def main():
     e2e = None
     acc_leg = None
     if rank == 0:
-        prove_timed = (lambda: r.prove_segment_trace_resident(hal, rt)) if trace_mode else (lambda: prove_witness(0))
+        prove_timed = ((lambda: r.prove_segment_trace_resident(hal, rt, bigint_records=bigint_records)) if trace_mode
+                       else (lambda: prove_witness(0)))
         roofline = kernel_roofline(r, args, prove_timed)
         # the side legs keep 2 in flight below po2 21 unless --inflight says otherwise: the
         # pipeline's uploader and a third prover measured slower there (63.1 against 57.6 ms)
@@ -536,15 +540,20 @@ def cpu_baseline_trace(args, trace, gpu_seal, gpu_mix):
         data, glob, cyc, tx = W.inputs(trace)  # PreflightResults::new's injector and globals (not timed)
         oracle.op_times(reset=True)
         t0 = time.perf_counter()
-        d, g = W.run(data, glob, cyc, tx, trace.table_split_cycle, rows, W.MODE_PARALLEL)
+        d, g = W.run(data, glob, cyc, tx, trace.table_split_cycle, rows, W.MODE_PARALLEL, trace.bigint_array())
         t_wg = time.perf_counter() - t0
         d = np.where(d == W.INVALID, 0, d).astype(np.uint32)
         g = np.where(g == W.INVALID, 0, g).astype(np.uint32)
         acc_s = []
+        records = trace.bigint_records()
 
         def fill(mix):
             ta = time.perf_counter()
-            a = RA.accum(d, g, mix, rows, rows)
+            init = None
+            if records:  # WitnessGenerator::accum's BigIntAccum injection (witgen/mod.rs:187-205)
+                import bigint_accum as BA
+                init = BA.inject(np.full(RA.ACCUM_COLS * rows, W.INVALID, np.uint32), rows, mix, records)
+            a = RA.accum(d, g, mix, rows, rows, accum_init=init)
             a = np.where(a == W.INVALID, 0, a).astype(np.uint32)
             acc_s.append(time.perf_counter() - ta)
             return a

@@ -94,6 +94,24 @@ def s32(x):
     return x - (1 << 32) if x & 0x80000000 else x
 
 
+INVALID = 0xFFFFFFFF  # Val::INVALID
+
+
+def layout():
+    """the injector's and the global vector's layout columns (tools/gen_rv32im_witgen_ir.py)"""
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "risc0_amd", "circuits", "rv32im.witgen.json")) as f:
+        return json.load(f)
+
+
+def encode(v):
+    """Val::new (plain integer -> Montgomery word)"""
+    v = np.asarray(v, dtype=np.uint64) % P
+    return ((v << np.uint64(32)) % np.uint64(P)).astype(np.uint32)
+
+
 # ------------------------------------------------------------------ a tiny assembler
 R_OPS = {"add": (0, 0), "sub": (0, 0x20), "sll": (1, 0), "slt": (2, 0), "sltu": (3, 0), "xor": (4, 0), "srl": (5, 0),
          "sra": (5, 0x20), "or": (6, 0), "and": (7, 0), "mul": (0, 1), "mulh": (1, 1), "mulhsu": (2, 1),
@@ -146,15 +164,29 @@ def asm(op, *a):
 
 # ------------------------------------------------------------------ Poseidon2 (execute/poseidon2.rs)
 def _p2_consts():
-    """ROUND_CONSTANTS and M_INT_DIAG_HZN (risc0_zkp poseidon2/consts.rs, plain integers) from
-    the oracle's extracted table"""
+    """ROUND_CONSTANTS and M_INT_DIAG_HZN (risc0_zkp poseidon2/consts.rs:51-184) as plain
+    integers, decoded from the product's Montgomery table (risc0_amd/csrc/poseidon2_consts.inc,
+    tools/extract_poseidon2.py) so the bench's input generator reads nothing under oracle/;
+    test_rv32im_witgen_ir pins it to the oracle's table. Full rounds 0-3 and 4-7 sit at rows
+    0-3 and 25-28 of the 29 x 24 layout, partial round i's constant at row 4 + i, cell 0."""
     import os
-    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "poseidon2_consts.inc")
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "risc0_amd", "csrc",
+                        "poseidon2_consts.inc")
     text = open(path).read()
     tabs = {}
-    for m in re.finditer(r"static const uint32_t (\w+)\[[^\]]*\] = \{(.*?)\};", text, re.S):
+    for m in re.finditer(r"#define (P2_\w+_MONT) \{(.*?)\}", text, re.S):
         tabs[m.group(1)] = [int(x, 16) for x in re.findall(r"0x[0-9a-fA-F]+", m.group(2))]
-    return tabs["ROUND_CONSTANTS_INT"], tabs["M_INT_DIAG_HZN_INT"]
+    rinv = pow(2**32, P - 2, P)
+    dec = lambda x: x * rinv % P
+    full, part, diag = tabs["P2_FULL_RC_MONT"], tabs["P2_PARTIAL_RC_MONT"], tabs["P2_DIAG_MONT"]
+    assert len(full) == 8 * 24 and len(part) == 21 and len(diag) == 24
+    rc = [0] * (29 * 24)
+    for r in range(8):
+        row = r if r < 4 else r + 21
+        rc[row * 24:(row + 1) * 24] = [dec(x) for x in full[r * 24:(r + 1) * 24]]
+    for i in range(21):
+        rc[(4 + i) * 24] = dec(part[i])
+    return rc, [dec(x) for x in diag]
 
 
 RC, M_INT_DIAG = _p2_consts()
@@ -1100,6 +1132,22 @@ class Trace:
             for j, f in enumerate(TXN_DTYPE.names):
                 tx[f] = t[:, j]
         return cyc, tx
+
+    def injector_arrays(self, lay=None):
+        """the Injector (witgen/mod.rs:329-378) as hal.scatter takes it: index (rows + 1),
+        offsets (col * rows + row), Montgomery values"""
+        rows = 1 << self.po2
+        r, c, v = self.injector(lay or layout())
+        index = np.zeros(rows + 1, np.uint32)
+        np.add.at(index, r.astype(np.int64) + 1, 1)
+        index = np.cumsum(index).astype(np.uint32)
+        assert np.all(np.diff(r.astype(np.int64)) >= 0)  # pushed row by row
+        return index, (c.astype(np.uint64) * rows + r).astype(np.uint32), encode(v)
+
+    def global_words(self, lay=None):
+        """build_global_vec as Montgomery words (INVALID where unset)"""
+        g = self.global_values(lay or layout())
+        return np.array([INVALID if x is None else int(encode(x)) for x in g], np.uint32)
 
     def bigint_array(self):
         """PreflightTrace::bigint_bytes"""

@@ -26,14 +26,10 @@ class ExecBuffers(C.Structure):
 
 
 def layout():
-    with open(os.path.join(ROOT, "risc0_amd", "circuits", "rv32im.witgen.json")) as f:
-        return json.load(f)
+    return T.layout()
 
 
-def encode(v):
-    """Val::new (plain integer -> Montgomery word)"""
-    v = np.asarray(v, dtype=np.uint64) % P
-    return ((v << np.uint64(32)) % np.uint64(P)).astype(np.uint32)
+encode = T.encode
 
 
 def inputs(trace, lay=None):
@@ -52,20 +48,12 @@ def inputs(trace, lay=None):
 
 def global_words(trace, lay=None):
     """build_global_vec as Montgomery words (INVALID where unset)"""
-    g = trace.global_values(lay or layout())
-    return np.array([INVALID if x is None else int(encode(x)) for x in g], np.uint32)
+    return trace.global_words(lay)
 
 
 def injector_arrays(trace, lay=None):
-    """the Injector (witgen/mod.rs:329-378) as hal.scatter takes it: index (rows + 1), offsets
-    (col * rows + row), Montgomery values"""
-    rows = 1 << trace.po2
-    r, c, v = trace.injector(lay or layout())
-    index = np.zeros(rows + 1, np.uint32)
-    np.add.at(index, r.astype(np.int64) + 1, 1)
-    index = np.cumsum(index).astype(np.uint32)
-    assert np.all(np.diff(r.astype(np.int64)) >= 0)  # pushed row by row
-    return index, (c.astype(np.uint64) * rows + r).astype(np.uint32), encode(v)
+    """the Injector (witgen/mod.rs:329-378) as hal.scatter takes it"""
+    return trace.injector_arrays(lay)
 
 
 def prove_from_trace(trace, suite, oracle, mode=MODE_SEQ_FORWARD):

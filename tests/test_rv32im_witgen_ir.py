@@ -125,3 +125,19 @@ def test_trace_seal_verifies_with_validity(oracle):
     with pytest.raises(r.R0HipError):
         r.verify_seal("rv32im", r.POSEIDON2, bad, check_validity=True)
     assert r.verify_seal("rv32im", r.POSEIDON2, bad, check_validity=False) == 13
+
+
+def test_trace_poseidon2_constants_match_oracle():
+    """the restated preflight decodes its Poseidon2 constants from the product's Montgomery
+    table (so the bench's input generator reads nothing under oracle/); they equal the oracle's
+    plain-integer table (poseidon2/consts.rs:51-184) wherever the rounds use them"""
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    text = open(os.path.join(root, "oracle", "poseidon2_consts.inc")).read()
+    tabs = {m.group(1): [int(x, 16) for x in re.findall(r"0x[0-9a-fA-F]+", m.group(2))]
+            for m in re.finditer(r"static const uint32_t (\w+)\[[^\]]*\] = \{(.*?)\};", text, re.S)}
+    rc, diag = tabs["ROUND_CONSTANTS_INT"], tabs["M_INT_DIAG_HZN_INT"]
+    for r in list(range(4)) + list(range(25, 29)):
+        assert T.RC[r * 24:(r + 1) * 24] == rc[r * 24:(r + 1) * 24]
+    assert [T.RC[(4 + i) * 24] for i in range(21)] == [rc[(4 + i) * 24] for i in range(21)]
+    assert T.M_INT_DIAG == diag
