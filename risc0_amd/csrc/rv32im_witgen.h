@@ -78,18 +78,26 @@ __device__ __forceinline__ void fail(const Args& A, uint32_t code, uint32_t cycl
   }
 }
 
-// Buffer::get / Buffer::set with checked = true
-__device__ __forceinline__ uint32_t ld(const Args& A, uint32_t col, uint32_t row, uint32_t cycle) {
-  const uint32_t v = A.data[uint64_t(col) * A.rows + row];
+// Buffer::get / Buffer::set with checked = true. `view` is A.data, or for the injected
+// columns a read-only alias the generated kernels declare __restrict__ (see
+// tools/gen_rv32im_witgen.py, Path)
+__device__ __forceinline__ uint32_t ld(const Args& A, const uint32_t* view, uint32_t col, uint32_t row, uint32_t cycle) {
+  const uint32_t v = view[uint64_t(col) * A.rows + row];
   if (v == kInvalid) fail(A, kErrUnset, cycle, col);
   return v;
 }
 
-__device__ __forceinline__ void st(const Args& A, uint32_t col, uint32_t cycle, uint32_t v) {
-  uint32_t* p = A.data + uint64_t(col) * A.rows + cycle;
-  const uint32_t old = *p;
+__device__ __forceinline__ void st(const Args& A, const uint32_t* view, uint32_t col, uint32_t cycle, uint32_t v) {
+  const uint64_t i = uint64_t(col) * A.rows + cycle;
+  const uint32_t old = view[i];
   if (old != kInvalid && old != v) fail(A, kErrInconsistent, cycle, col);
-  *p = v;
+  A.data[i] = v;
+}
+
+// a store whose cell the generator knows to be INVALID (set by no injector and by no earlier
+// store of this cycle): the checked set cannot fail
+__device__ __forceinline__ void st_fresh(const Args& A, uint32_t col, uint32_t cycle, uint32_t v) {
+  A.data[uint64_t(col) * A.rows + cycle] = v;
 }
 
 __device__ __forceinline__ uint32_t gld(const Args& A, uint32_t idx, uint32_t cycle) {
@@ -105,14 +113,14 @@ __device__ __forceinline__ void gst(const Args& A, uint32_t idx, uint32_t cycle,
 }
 
 // extern_getMemoryTxn (ffi.cpp:84-113): the cycle's next transaction
-__device__ __forceinline__ void txn(const Args& A, uint32_t cycle, uint32_t& cur, uint32_t addr_w, uint32_t& prev_cycle,
-                                    uint32_t& prev_lo, uint32_t& prev_hi, uint32_t& lo, uint32_t& hi) {
+__device__ __forceinline__ void txn(const Args& A, const MemoryTxn* txs, uint32_t cycle, uint32_t& cur, uint32_t addr_w,
+                                    uint32_t& prev_cycle, uint32_t& prev_lo, uint32_t& prev_hi, uint32_t& lo, uint32_t& hi) {
   if (cur >= A.n_txns) {
     fail(A, kErrTxnRange, cycle, cur);
     prev_cycle = prev_lo = prev_hi = lo = hi = 0u;
     return;
   }
-  const MemoryTxn t = A.txns[cur++];
+  const MemoryTxn t = txs[cur++];
   if (t.cycle / 2 != cycle) fail(A, kErrTxnCycle, cycle, t.cycle);
   if (t.addr != to_u32(addr_w)) fail(A, kErrTxnAddr, cycle, t.addr);
   prev_cycle = from_u32(t.prev_cycle);
@@ -124,12 +132,12 @@ __device__ __forceinline__ void txn(const Args& A, uint32_t cycle, uint32_t& cur
 
 // extern_hostReadPrepare / extern_hostWrite (ffi.cpp:201-212): the word of the cycle's next
 // transaction, without advancing
-__device__ __forceinline__ uint32_t host_word(const Args& A, uint32_t cycle, uint32_t cur) {
+__device__ __forceinline__ uint32_t host_word(const Args& A, const MemoryTxn* txs, uint32_t cycle, uint32_t cur) {
   if (cur >= A.n_txns) {
     fail(A, kErrTxnRange, cycle, cur);
     return 0u;
   }
-  return from_u32(A.txns[cur].word);
+  return from_u32(txs[cur].word);
 }
 
 // LookupTables::lookupDelta (tables.h:33-53; the count argument is not used there either);

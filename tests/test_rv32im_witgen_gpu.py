@@ -51,9 +51,9 @@ def test_rv32im_witgen_ecalls_match_reference(hal, terminate, bigint):
     ref_d, ref_g = W.run(data, glob, cyc, tx, t.table_split_cycle, 1 << 14, bigint=bi)
     d, g = gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle, bigint=bi)
     assert np.array_equal(d, ref_d) and np.array_equal(g, ref_g)
-    if bigint:  # a bigint array shorter than the cycles' bigintIdx + 16 is refused, not read past
+    if bigint:  # cut inside the bytes of the call's first Write row (its 4th cycle): refused, not read past
         with pytest.raises(r.R0HipError, match="bigint bytes past"):
-            gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle, bigint=bi[:-8])
+            gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle, bigint=bi[:56])
 
 
 def test_rv32im_witgen_modes(hal):
