@@ -140,10 +140,53 @@ __device__ __forceinline__ uint32_t host_word(const Args& A, const MemoryTxn* tx
   return from_u32(txs[cur].word);
 }
 
-// LookupTables::lookupDelta (tables.h:33-53; the count argument is not used there either);
-// u8 counts go to the workgroup's LDS copy h8, flushed by the kernel's last lines
+// The workgroup's lookup counts in LDS, added to the device tables once at the kernel's end:
+// the u8 table whole (256 counters), the u16 table through a small open-addressing table of
+// (index, count) slots. A few u16 indices take most lookups (index 0: 43% of the shift/divide
+// arm's 19 lookups per cycle on the bench guest), and device atomics on one address serialise
+// (≈14 ns each), so the counts are summed per workgroup first; an index that finds no slot
+// within kU16Probe probes goes to the device table directly.
+constexpr uint32_t kU16Slots = 1024, kU16Probe = 4, kEmpty = 0xFFFFFFFFu;
+struct LdsTables {
+  uint32_t* h8;    // [256]
+  uint32_t* keys;  // [kU16Slots], kEmpty when free
+  uint32_t* cnt;   // [kU16Slots]
+};
+
+__device__ __forceinline__ void lds_tables_init(const LdsTables& T) {
+  for (uint32_t t = threadIdx.x; t < 256u; t += kThreads) T.h8[t] = 0u;
+  for (uint32_t t = threadIdx.x; t < kU16Slots; t += kThreads) {
+    T.keys[t] = kEmpty;
+    T.cnt[t] = 0u;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void lds_tables_flush(const Args& A, const LdsTables& T) {
+  __syncthreads();
+  for (uint32_t t = threadIdx.x; t < 256u; t += kThreads)
+    if (T.h8[t]) atomicAdd(A.u8 + t, T.h8[t]);
+  for (uint32_t t = threadIdx.x; t < kU16Slots; t += kThreads)
+    if (T.keys[t] != kEmpty) atomicAdd(A.u16 + T.keys[t], T.cnt[t]);
+}
+
+__device__ __forceinline__ void u16_count(const Args& A, const LdsTables& T, uint32_t index) {
+  const uint32_t h = (index * 2654435761u) >> 22;  // 10-bit multiplicative hash
+#pragma unroll
+  for (uint32_t p = 0; p < kU16Probe; p++) {
+    const uint32_t slot = (h + p) & (kU16Slots - 1);
+    const uint32_t k = atomicCAS(T.keys + slot, kEmpty, index);
+    if (k == kEmpty || k == index) {
+      atomicAdd(T.cnt + slot, 1u);
+      return;
+    }
+  }
+  atomicAdd(A.u16 + index, 1u);
+}
+
+// LookupTables::lookupDelta (tables.h:33-53; the count argument is not used there either)
 __device__ __forceinline__ void lookup_delta(const Args& A, uint32_t cycle, uint32_t table_w, uint32_t index_w,
-                                             uint32_t* h8) {
+                                             const LdsTables& T) {
   const uint32_t table = to_u32(table_w), index = to_u32(index_w);
   if (table == 0u) return;
   if (table != 8u && table != 16u) {
@@ -155,9 +198,9 @@ __device__ __forceinline__ void lookup_delta(const Args& A, uint32_t cycle, uint
     return;
   }
   if (table == 8u)
-    atomicAdd(h8 + index, 1u);
+    atomicAdd(T.h8 + index, 1u);
   else
-    atomicAdd(A.u16 + index, 1u);
+    u16_count(A, T, index);
 }
 
 // LookupTables::lookupCurrent (tables.h:55-66)
