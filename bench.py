@@ -37,6 +37,8 @@ def parse():
     ap.add_argument("--circuit", default="rv32im")
     ap.add_argument("--hashfn", default="poseidon2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-prove-only", action="store_true",
+                    help="trace mode: skip the prove_only leg (profiling runs count only trace proofs)")
     ap.add_argument("--witness", action="store_true",
                     help="rv32im: time the prove core on a resident synthetic witness instead of the default "
                          "trace -> witness generation -> accumulation -> seal unit")
@@ -181,7 +183,8 @@ def main():
     if trace_mode:
         t, seal, mix = timed_leg(lambda slot: r.prove_segment_trace_resident(hal, rt, bigint_records=bigint_records),
                                  "trace")
-        t_w, seal_w, _ = timed_leg(prove_witness, "prove_only")
+        if not args.no_prove_only:
+            t_w, seal_w, _ = timed_leg(prove_witness, "prove_only")
     else:
         t, seal, mix = timed_leg(prove_witness, "prove")
     mem = r.mem_stats()  # this rank's device footprint with k segments in flight
@@ -194,7 +197,7 @@ def main():
     value = cycles_total / t
     ms_per_step = 1000.0 * t / args.steps
     prove_only = None
-    if trace_mode:
+    if trace_mode and not args.no_prove_only:
         prove_only = {"value": round(cycles_total / t_w, 1), "unit": "cycles/s",
                       "ms_per_step": round(1000.0 * t_w / args.steps, 3),
                       "seal_sha256_rank0": hashlib.sha256(seal_w.tobytes()).hexdigest()[:16],

@@ -19,6 +19,8 @@ FAMILIES = [
     (r"eval_any|eval_chunk|eval_tables", "batch_evaluate_any"),
     (r"mix_kernel", "mix_poly_coeffs"),
     (r"div_", "poly_divide"),
+    (r"rvwg::witgen_major_|bucket_count_kernel|bucket_fill_kernel|rocprim::", "rv32im_witgen"),
+    (r"rvacc::|accum_k\d|rv32im_accum|scan_|finalize", "rv32im_accum"),
 ]
 
 
