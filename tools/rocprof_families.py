@@ -20,7 +20,8 @@ FAMILIES = [
     (r"mix_kernel", "mix_poly_coeffs"),
     (r"div_", "poly_divide"),
     (r"rvwg::witgen_major_|bucket_count_kernel|bucket_fill_kernel|rocprim::", "rv32im_witgen"),
-    (r"rvacc::|accum_k\d|rv32im_accum|scan_|finalize", "rv32im_accum"),
+    (r"rv_accum::|tile_sums_kernel|scan_sums_kernel|tile_scan_kernel|finalize_kernel|bigint_scatter_kernel",
+     "rv32im_accum"),
 ]
 
 
