@@ -334,7 +334,7 @@ std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const 
     Span w("witgen");
     rv32im_witgen_dev(s, mode, data.p, global.p, n, static_cast<const rvwg::PreflightCycle*>(pf->cycles),
                       static_cast<const rvwg::MemoryTxn*>(pf->txns), pf->txns_len, pf->bigint_bytes,
-                      pf->bigint_bytes_len, pf->table_split_cycle, uint32_t(n));
+                      pf->bigint_bytes_len, pf->table_split_cycle, uint32_t(n), true);
   } else {
     const size_t n_inj = inj_index[inj_rows];
     R0_REQUIRE(n_inj == 0 || (inj_offsets && inj_values), "r0hip_prove_segment_trace: null injector arrays");
@@ -353,10 +353,9 @@ std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const 
     Span w("witgen");
     rv32im_witgen(s, mode, data.p, global.p, n, static_cast<const rvwg::PreflightCycle*>(pf->cycles),
                   static_cast<const rvwg::MemoryTxn*>(pf->txns), pf->txns_len, pf->bigint_bytes, pf->bigint_bytes_len,
-                  pf->table_split_cycle, uint32_t(n));
+                  pf->table_split_cycle, uint32_t(n), true);
   }
-  eltwise_zeroize(s, global.p, global.words);
-  eltwise_zeroize(s, data.p, data.words);
+  eltwise_zeroize(s, global.p, global.words);  // the data group was zeroized by the witgen merge
   HIP_OK(hipMemsetD32Async(accum.p, 0xFFFFFFFFu, accum.words, s));
   const AccumStep acc{accum.p, n, false, h_bigint, n_bigint};
   return prove_segment(*c, suite, po2, code.p, data.p, nullptr, global.p, true, 2, mix, nullptr, &acc);

@@ -107,6 +107,7 @@ enum ScratchSlot : int {
   kSlotRvwgTables = 79,
   kSlotRvwgKeys = 83,
   kSlotRvwgSortTemp = 84,
+  kSlotRvwgCompact = 85,
   // r0hip_prove_segment_trace (api.cpp): the injector's index, offsets and values
   kSlotRvInjIndex = 80,
   kSlotRvInjOffsets = 81,

@@ -12,6 +12,7 @@ namespace rvwg {
 constexpr uint32_t kThreads = 128;
 constexpr uint32_t kInvalid = 0xFFFFFFFFu;  // Fp::invalid()
 constexpr uint32_t kMajors = 13;            // Top's instruction mux (majorOnehot)
+constexpr uint32_t kDataCols = 211;         // the rv32im data group (REGCOUNT_DATA)
 
 // rv32im-sys/kernels/cxx/preflight.h:21-41 (RawPreflightCycle / RawMemoryTransaction)
 struct PreflightCycle {
@@ -94,10 +95,42 @@ __device__ __forceinline__ void st(const Args& A, const uint32_t* view, uint32_t
   A.data[i] = v;
 }
 
+// The arm kernels keep this cycle's own row values in a compact, slot-major buffer of their
+// bin (cb[slot * n + i], lane i = the cycle's place in the bin's list: one coalesced store per
+// column for a wavefront), pre-filled with INVALID; rv32im_witgen.hip's merge writes them into
+// the column-major data group afterwards, whole lines at a time. (Writing the data group from
+// the arm kernels directly cost ≈3.7 GB of partial-line writes per po2=20 segment: a line of a
+// column holds 32 consecutive cycles of every arm.)
+//
 // a store whose cell the generator knows to be INVALID (set by no injector and by no earlier
 // store of this cycle): the checked set cannot fail
-__device__ __forceinline__ void st_fresh(const Args& A, uint32_t col, uint32_t cycle, uint32_t v) {
-  A.data[uint64_t(col) * A.rows + cycle] = v;
+__device__ __forceinline__ void stc(uint32_t* cb, uint32_t n, uint32_t i, uint32_t slot, uint32_t v) {
+  cb[size_t(slot) * n + i] = v;
+}
+
+// the row's value of a column stored earlier on some path of this cycle: its slot (checked get)
+__device__ __forceinline__ uint32_t ldc(const Args& A, const uint32_t* cb, uint32_t n, uint32_t i, uint32_t slot,
+                                        uint32_t col, uint32_t cycle) {
+  const uint32_t v = cb[size_t(slot) * n + i];
+  if (v == kInvalid) fail(A, kErrUnset, cycle, col);
+  return v;
+}
+
+// checked set of an injected column: the old value is the injector's (data, read-only view)
+__device__ __forceinline__ void st_inj(const Args& A, const uint32_t* view, uint32_t* cb, uint32_t n, uint32_t i,
+                                       uint32_t slot, uint32_t col, uint32_t cycle, uint32_t v) {
+  const uint32_t old = view[uint64_t(col) * A.rows + cycle];
+  if (old != kInvalid && old != v) fail(A, kErrInconsistent, cycle, col);
+  cb[size_t(slot) * n + i] = v;
+}
+
+// checked set of a column some earlier path of this cycle may have stored
+__device__ __forceinline__ void st_maybe(const Args& A, uint32_t* cb, uint32_t n, uint32_t i, uint32_t slot, uint32_t col,
+                                         uint32_t cycle, uint32_t v) {
+  uint32_t* p = cb + size_t(slot) * n + i;
+  const uint32_t old = *p;
+  if (old != kInvalid && old != v) fail(A, kErrInconsistent, cycle, col);
+  *p = v;
 }
 
 __device__ __forceinline__ uint32_t gld(const Args& A, uint32_t idx, uint32_t cycle) {
@@ -264,17 +297,25 @@ __device__ __forceinline__ uint32_t bigint_byte(const Args& A, uint32_t cycle, u
 }  // namespace rvwg
 
 // the generated kernels: step_Top specialised to instruction arm `major` over a list of cycles
-void rv32im_witgen_major(uint32_t major, hipStream_t s, const rvwg::Args& A, const uint32_t* cycles, uint32_t n);
+void rv32im_witgen_major(uint32_t major, hipStream_t s, const rvwg::Args& A, const uint32_t* list, uint32_t n,
+                         uint32_t* cb);
+// each arm's compact slot of every data column ([13][211], -1: never stored) and slot counts
+const int16_t* rv32im_witgen_slot_table();
+uint32_t rv32im_witgen_nslots(uint32_t major);
 // EQZ messages of the generated code (steps.cpp locations), by index
 const char* rv32im_witgen_message(uint32_t k);
 // the driver (rv32im_witgen.hip): both phases over cycles [0, last_cycle) with the preflight
 // arrays resident on the device; synchronises, throws on a failed check
+// zeroize: the merge writes 0 for INVALID words (eltwise_zeroize fused, as hal_generate_witness
+// does right after stepExec, witgen/mod.rs:166-169)
 void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
                        const rvwg::PreflightCycle* d_cycles, const rvwg::MemoryTxn* d_txns, size_t n_txns,
-                       const uint8_t* d_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle);
+                       const uint8_t* d_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle,
+                       bool zeroize = false);
 // the same from host preflight arrays (uploaded first), as RawPreflightTrace hands them over
 void rv32im_witgen(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
                    const rvwg::PreflightCycle* h_cycles, const rvwg::MemoryTxn* h_txns, size_t n_txns,
-                   const uint8_t* h_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle);
+                   const uint8_t* h_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle,
+                   bool zeroize = false);
 
 }  // namespace r0

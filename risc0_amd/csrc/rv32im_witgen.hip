@@ -19,7 +19,6 @@
 // already resident (rv32im_witgen_dev). The cycles are bucketed on the device (counts, one
 // 27-word read-back for the launch sizes, fill). Checks that throw in the reference record an
 // error code and the cycle, raised after the kernels drain.
-#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -62,12 +61,13 @@ namespace {
 
 constexpr uint32_t kBins = 2 * rvwg::kMajors;  // (phase, major)
 constexpr uint32_t kBucketThreads = 256;
+constexpr uint32_t kMergeThreads = 256;
 
 // per (phase, instruction arm) cycle counts; a major outside the 13 arms is an error (the
-// reference's OneHot EQZ on majorOnehot fails for it). keys/vals (optional): each cycle's bin
-// and index, for the stable sort into cycle order within each bin.
+// reference's OneHot EQZ on majorOnehot fails for it). keys/vals: each cycle's bin and index,
+// for the stable sort into cycle order within each bin.
 __global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(rvwg::Args A, uint32_t split, uint32_t* counts,
-                                                                     uint8_t* keys, uint32_t* vals, bool by_minor) {
+                                                                     uint8_t* keys, uint32_t* vals) {
   __shared__ uint32_t h[kBins];
   if (threadIdx.x < kBins) h[threadIdx.x] = 0;
   __syncthreads();
@@ -79,32 +79,62 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(rvwg::Args
       rvwg::fail(A, rvwg::kErrMajor, c, m);
     else
       atomicAdd(&h[b], 1u);
-    if (keys) {
-      const uint32_t key = m >= rvwg::kMajors ? kBins : b;
-      keys[c] = uint8_t(by_minor ? key * 8u + (A.cycles[c].minor & 7u) : key);
-      vals[c] = c;
-    }
+    keys[c] = uint8_t(m >= rvwg::kMajors ? kBins : b);
+    vals[c] = c;
   }
   __syncthreads();
   if (threadIdx.x < kBins && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
 }
 
-// each cycle into its bucket (cursor = the bucket's next slot; the order within a bucket does
-// not matter: the cycles of a phase are independent)
-__global__ __launch_bounds__(kBucketThreads) void bucket_fill_kernel(rvwg::Args A, uint32_t split, uint32_t* cursor,
-                                                                    uint32_t* list) {
-  const uint32_t c = blockIdx.x * kBucketThreads + threadIdx.x;
-  if (c >= A.ncycles) return;
-  const uint32_t m = A.cycles[c].major;
-  if (m >= rvwg::kMajors) return;
-  list[atomicAdd(&cursor[(c >= split) * rvwg::kMajors + m], 1u)] = c;
+struct BinTable {
+  uint32_t off[kBins + 1];  // first list index of each bin
+  uint32_t cnt[kBins];
+  uint64_t cbase[kBins];    // each bin's compact values in the compact buffer (words)
+};
+
+// each cycle's place in its bin's list (the lane that ran it, its compact column index)
+__global__ __launch_bounds__(kBucketThreads) void bin_pos_kernel(const uint32_t* list, const uint8_t* sorted_keys,
+                                                                uint32_t n, BinTable T, uint32_t* pos) {
+  const uint32_t j = blockIdx.x * kBucketThreads + threadIdx.x;
+  if (j < n) pos[list[j]] = j - T.off[sorted_keys[j]];
+}
+
+// the data group from the arms' compact values, a column line at a time: word (col, row) is the
+// row's stored value if its arm stored one, else the data word as the injector left it (an
+// injected value or INVALID); zeroize: INVALID -> 0. Every word of rows [0, rows) is written,
+// so each line of a column goes out whole.
+__global__ __launch_bounds__(kMergeThreads) void merge_kernel(uint32_t* data, uint32_t rows, uint32_t ncycles,
+                                                             const uint32_t* cbuf, const uint8_t* keys,
+                                                             const uint32_t* pos, const int16_t* slot_of, BinTable T,
+                                                             bool zeroize) {
+  __shared__ int16_t slot[rvwg::kMajors * rvwg::kDataCols];
+  for (uint32_t t = threadIdx.x; t < rvwg::kMajors * rvwg::kDataCols; t += kMergeThreads) slot[t] = slot_of[t];
+  __syncthreads();
+  const uint32_t r = blockIdx.x * kMergeThreads + threadIdx.x;
+  if (r >= rows) return;
+  const bool stepped = r < ncycles;
+  const uint32_t b = stepped ? keys[r] : 0u;
+  const uint32_t arm = b % rvwg::kMajors;
+  const uint32_t n = stepped ? T.cnt[b] : 0u, i = stepped ? pos[r] : 0u;
+  const uint32_t* cb = cbuf + (stepped ? T.cbase[b] : 0u);
+  const int16_t* sl = slot + arm * rvwg::kDataCols;
+#pragma unroll 8
+  for (uint32_t col = 0; col < rvwg::kDataCols; col++) {
+    const int s = stepped ? sl[col] : -1;
+    uint32_t* p = data + uint64_t(col) * rows + r;
+    uint32_t v = s >= 0 ? cb[size_t(s) * n + i] : rvwg::kInvalid;
+    if (v == rvwg::kInvalid) v = *p;
+    if (zeroize && v == rvwg::kInvalid) v = 0u;
+    *p = v;
+  }
 }
 
 }  // namespace
 
 void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
                        const rvwg::PreflightCycle* d_cycles, const rvwg::MemoryTxn* d_txns, size_t n_txns,
-                       const uint8_t* d_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle) {
+                       const uint8_t* d_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle,
+                       bool zeroize) {
   using namespace rvwg;
   R0_REQUIRE(mode <= 2, "rv32im_witgen: mode must be 0 (parallel), 1 (forward) or 2 (reverse)");
   R0_REQUIRE(rows >= 4 && (rows & (rows - 1)) == 0 && rows <= (size_t(1) << 24),
@@ -113,11 +143,14 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
   R0_REQUIRE((last_cycle == 0 || d_cycles) && (n_txns == 0 || d_txns) && (n_bigint == 0 || d_bigint),
              "rv32im_witgen: null trace array with a nonzero count");
   R0_REQUIRE(n_txns < (size_t(1) << 32) && n_bigint < (size_t(1) << 32), "rv32im_witgen: trace too long");
-  if (last_cycle == 0) return;
-  // lookup tables, error record, bucket counts and cursors in one scratch block
-  auto* tab = static_cast<uint32_t*>(scratch((256 + 65536 + 4 + 2 * kBins) * 4, kSlotRvwgTables));
+  if (last_cycle == 0) {
+    if (zeroize) eltwise_zeroize(s, data, rows * kDataCols);
+    return;
+  }
+  // lookup tables, error record and bucket counts in one scratch block
+  auto* tab = static_cast<uint32_t*>(scratch((256 + 65536 + 4 + kBins) * 4, kSlotRvwgTables));
   auto* d_list = static_cast<uint32_t*>(scratch(size_t(last_cycle) * 4, kSlotRvwgLists));
-  HIP_OK(hipMemsetD32Async(tab, 0, 256 + 65536 + 4 + 2 * kBins, s));
+  HIP_OK(hipMemsetD32Async(tab, 0, 256 + 65536 + 4 + kBins, s));
   Args A{};
   A.data = data;
   A.global = global;
@@ -132,61 +165,66 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
   A.u16 = tab + 256;
   A.err = tab + 256 + 65536;
   uint32_t* counts = A.err + 4;
-  uint32_t* cursor = counts + kBins;
   const uint32_t g = (last_cycle + kBucketThreads - 1) / kBucketThreads;
   // the two phases' cycles bucketed by instruction arm: counts (one read-back for the launch
-  // sizes), then either a stable radix sort of (bin, cycle) — each bucket in cycle order, so a
-  // wave's lanes write nearby rows of each data column — or atomic cursors (R0_RVWG_SORT=0:
-  // arbitrary order within a bucket). R0_RVWG_SORT=2 sorts by (bin, minor, cycle): a wave's
-  // lanes then mostly share the arm's minor mux branch, at the cost of row locality.
-  static const int sort_mode = [] {
-    const char* e = std::getenv("R0_RVWG_SORT");
-    return e && (e[0] == '0' || e[0] == '2') ? e[0] - '0' : 1;
-  }();
-  const bool sorted = sort_mode != 0, by_minor = sort_mode == 2;
-  uint8_t* keys = nullptr;
-  uint32_t* vals = nullptr;
-  if (sorted) {
-    auto* kb = static_cast<uint8_t*>(scratch(size_t(last_cycle) * 6 + 64, kSlotRvwgKeys));
-    keys = kb;
-    vals = reinterpret_cast<uint32_t*>(kb + ((size_t(last_cycle) * 2 + 15) & ~size_t(15)));
-  }
+  // sizes), then a stable radix sort of (bin, cycle): each bucket in cycle order, so a wave's
+  // lanes read nearby transactions and injected rows
+  const size_t kb_bytes = (size_t(last_cycle) * 2 + 15) & ~size_t(15);
+  auto* kb = static_cast<uint8_t*>(scratch(kb_bytes + size_t(last_cycle) * 8 + 64, kSlotRvwgKeys));
+  uint8_t* keys = kb;
+  uint8_t* keys_out = kb + last_cycle;
+  uint32_t* vals = reinterpret_cast<uint32_t*>(kb + kb_bytes);
+  uint32_t* pos = vals + last_cycle;
   uint32_t h[4 + kBins];
   {
     KScope ks("rv32im_witgen_bucket", double(last_cycle) * 2 * sizeof(PreflightCycle));
-    hipLaunchKernelGGL(bucket_count_kernel, dim3(g), dim3(kBucketThreads), 0, s, A, table_split, counts, keys, vals,
-                       by_minor);
+    hipLaunchKernelGGL(bucket_count_kernel, dim3(g), dim3(kBucketThreads), 0, s, A, table_split, counts, keys, vals);
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(h, A.err, sizeof(h), hipMemcpyDeviceToHost, s));  // err[0..2], pad, counts
     HIP_OK(hipStreamSynchronize(s));
   }
   R0_REQUIRE(h[0] == 0, "rv32im witgen: " + witgen_error(h));
   const uint32_t* cnt = h + 4;  // counts start at A.err + 4
-  uint32_t off[kBins + 1];
-  off[0] = 0;
-  for (uint32_t b = 0; b < kBins; b++) off[b + 1] = off[b] + cnt[b];
-  R0_REQUIRE(off[kBins] == last_cycle, "rv32im witgen: bucket counts do not add up");
-  if (sorted) {
-    uint8_t* keys_out = keys + last_cycle;
-    size_t temp_bytes = 0;
-    const int end_bit = by_minor ? 8 : 5;
-    HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, keys_out, vals, d_list, int(last_cycle), 0,
-                                              end_bit, s));
-    void* temp = scratch(temp_bytes + 256, kSlotRvwgSortTemp);
-    HIP_OK(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys_out, vals, d_list, int(last_cycle), 0,
-                                              end_bit, s));
-  } else {
-    upload_async(cursor, off, kBins * 4);
-    hipLaunchKernelGGL(bucket_fill_kernel, dim3(g), dim3(kBucketThreads), 0, s, A, table_split, cursor, d_list);
-    HIP_OK(hipGetLastError());
+  BinTable T{};
+  T.off[0] = 0;
+  size_t cwords = 0;
+  for (uint32_t b = 0; b < kBins; b++) {
+    T.off[b + 1] = T.off[b] + cnt[b];
+    T.cnt[b] = cnt[b];
+    T.cbase[b] = cwords;
+    cwords += size_t(rv32im_witgen_nslots(b % kMajors)) * cnt[b];
   }
+  R0_REQUIRE(T.off[kBins] == last_cycle, "rv32im witgen: bucket counts do not add up");
+  size_t temp_bytes = 0;
+  HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, keys_out, vals, d_list, int(last_cycle), 0, 5, s));
+  void* temp = scratch(temp_bytes + 256, kSlotRvwgSortTemp);
+  HIP_OK(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys_out, vals, d_list, int(last_cycle), 0, 5, s));
+  hipLaunchKernelGGL(bin_pos_kernel, dim3(g), dim3(kBucketThreads), 0, s, d_list, keys_out, last_cycle, T, pos);
+  HIP_OK(hipGetLastError());
+  // the arms' compact values, INVALID until stored
+  auto* cbuf = static_cast<uint32_t*>(scratch(cwords * 4 + 16, kSlotRvwgCompact));
+  HIP_OK(hipMemsetD32Async(cbuf, 0xFFFFFFFFu, cwords, s));
   for (int p = 0; p < 2; p++) {
     KScope ks(p ? "rv32im_witgen_tables" : "rv32im_witgen_exec",
-              double(off[(p + 1) * kMajors] - off[p * kMajors]) * (4.0 * 211 + sizeof(PreflightCycle)));
+              double(T.off[(p + 1) * kMajors] - T.off[p * kMajors]) * (4.0 * 211 + sizeof(PreflightCycle)));
     for (uint32_t k = 0; k < kMajors; k++) {
       const uint32_t b = p * kMajors + k;
-      rv32im_witgen_major(k, s, A, d_list + off[b], off[b + 1] - off[b]);
+      rv32im_witgen_major(k, s, A, d_list + T.off[b], T.cnt[b], cbuf + T.cbase[b]);
     }
+  }
+  {
+    static const int16_t* d_slot = [] {
+      // the slot table, uploaded once per process (it is constant)
+      const size_t bytes = size_t(kMajors) * kDataCols * sizeof(int16_t);
+      void* p = nullptr;
+      HIP_OK(hipMalloc(&p, bytes));
+      HIP_OK(hipMemcpy(p, rv32im_witgen_slot_table(), bytes, hipMemcpyHostToDevice));
+      return static_cast<const int16_t*>(p);
+    }();
+    KScope ks("rv32im_witgen_merge", double(rows) * kDataCols * 8.0 + double(cwords) * 4.0);
+    hipLaunchKernelGGL(merge_kernel, dim3(uint32_t((rows + kMergeThreads - 1) / kMergeThreads)), dim3(kMergeThreads), 0,
+                       s, data, uint32_t(rows), last_cycle, cbuf, keys, pos, d_slot, T, zeroize);
+    HIP_OK(hipGetLastError());
   }
   uint32_t h_err[3] = {0, 0, 0};
   HIP_OK(hipMemcpyAsync(h_err, A.err, 12, hipMemcpyDeviceToHost, s));
@@ -196,7 +234,7 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
 
 void rv32im_witgen(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
                    const rvwg::PreflightCycle* h_cycles, const rvwg::MemoryTxn* h_txns, size_t n_txns,
-                   const uint8_t* h_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle) {
+                   const uint8_t* h_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle, bool zeroize) {
   using namespace rvwg;
   R0_REQUIRE(last_cycle <= rows && last_cycle <= (size_t(1) << 24), "rv32im_witgen: more cycles than rows");
   R0_REQUIRE((last_cycle == 0 || h_cycles) && (n_txns == 0 || h_txns) && (n_bigint == 0 || h_bigint),
@@ -208,7 +246,7 @@ void rv32im_witgen(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* globa
   upload_async(d_txns, h_txns, n_txns * sizeof(MemoryTxn));
   upload_async(d_bigint, h_bigint, n_bigint);
   rv32im_witgen_dev(s, mode, data, global, rows, d_cycles, n_txns ? d_txns : nullptr, n_txns,
-                    n_bigint ? d_bigint : nullptr, n_bigint, table_split, last_cycle);
+                    n_bigint ? d_bigint : nullptr, n_bigint, table_split, last_cycle, zeroize);
 }
 
 }  // namespace r0
