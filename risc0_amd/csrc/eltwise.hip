@@ -314,6 +314,7 @@ constexpr int kDivPer = 16;
 struct DivRow {
   uint32_t* p;     // row base (FpExt AoS)
   FpExt z;
+  uint32_t* rem;   // where the remainder goes (FpExt)
 };
 
 __global__ __launch_bounds__(kThreads) void div_local_kernel(const DivRow* rows, uint32_t nlanes, uint32_t* lanev) {
@@ -365,9 +366,9 @@ __global__ __launch_bounds__(kThreads) void div_block_kernel(const DivRow* rows,
   }
 }
 
-// blockv <- carry into the top lane of each block; rem[row] = cur_0.
-__global__ __launch_bounds__(kThreads) void div_top_kernel(uint32_t nblocks, uint32_t* blockv, const uint32_t* blockm,
-                                                          uint32_t* rem) {
+// blockv <- carry into the top lane of each block; the row's remainder = cur_0.
+__global__ __launch_bounds__(kThreads) void div_top_kernel(const DivRow* rows, uint32_t nblocks, uint32_t* blockv,
+                                                          const uint32_t* blockm) {
   __shared__ FpExt vals[kThreads + 1];
   __shared__ FpExt mul[kThreads + 1];
   const uint32_t row = blockIdx.x, tid = threadIdx.x;
@@ -401,7 +402,7 @@ __global__ __launch_bounds__(kThreads) void div_top_kernel(uint32_t nblocks, uin
     if (b < nblocks) st_fe(bv + uint64_t(b) * 4, cin);
     carry = total;
   }
-  if (tid == 0) st_fe(rem + 4 * row, carry);
+  if (tid == 0) st_fe(rows[row].rem, carry);
 }
 
 __global__ __launch_bounds__(kThreads) void div_apply_kernel(const DivRow* rows, uint32_t nlanes, const uint32_t* lanev,
@@ -422,7 +423,7 @@ __global__ __launch_bounds__(kThreads) void div_apply_kernel(const DivRow* rows,
 }
 
 // rows whose length is not a multiple of 16: one lane per row, serial
-__global__ void div_serial_kernel(const DivRow* rows, uint64_t n, uint32_t* rem, uint32_t nrows) {
+__global__ void div_serial_kernel(const DivRow* rows, uint64_t n, uint32_t nrows) {
   uint32_t row = blockIdx.x * kThreads + threadIdx.x;
   if (row >= nrows) return;
   const DivRow r = rows[row];
@@ -432,7 +433,7 @@ __global__ void div_serial_kernel(const DivRow* rows, uint64_t n, uint32_t* rem,
     st_fe(r.p + 4 * i, cur);
     cur = fe_add(fe_mul(r.z, cur), pi);
   }
-  st_fe(rem + 4 * row, cur);
+  st_fe(r.rem, cur);
 }
 
 // combos_prepare tail (hal/mod.rs:212-233): combos[r*cycles + i] -= deltas[r*width + i]
@@ -622,20 +623,15 @@ void poly_divide_rows(hipStream_t s, uint32_t* io, size_t n, const std::vector<s
   KScope ks("poly_divide", double(ndiv) * n * 32);
   // round k divides every row that has a k-th z (the rows' z lists run in order)
   for (size_t k = 0; k < maxz; k++) {
+    // each row's remainder goes straight to its place in rem_dev (row-major, maxz per row)
     std::vector<DivRow> rs;
-    std::vector<uint32_t> ids;
     for (size_t r = 0; r < rows; r++)
-      if (k < zs[r].size()) {
-        rs.push_back(DivRow{io + uint64_t(r) * n * 4, zs[r][k]});
-        ids.push_back(uint32_t(r));
-      }
+      if (k < zs[r].size()) rs.push_back(DivRow{io + uint64_t(r) * n * 4, zs[r][k], rem_dev + (uint64_t(r) * maxz + k) * 4});
     uint32_t nr = uint32_t(rs.size());
     DivRow* drows = static_cast<DivRow*>(scratch(rs.size() * sizeof(DivRow), k % 2 ? kSlotDivRowsAlt : kSlotDivRows));
     upload_async(drows, rs.data(), rs.size() * sizeof(DivRow));
-    uint32_t* rem = static_cast<uint32_t*>(scratch(size_t(nr) * 16, kSlotDivRem));
     if (n % kDivPer != 0) {
-      hipLaunchKernelGGL(div_serial_kernel, dim3(div_up(nr, kThreads)), dim3(kThreads), 0, s, drows, uint64_t(n),
-                         rem, nr);
+      hipLaunchKernelGGL(div_serial_kernel, dim3(div_up(nr, kThreads)), dim3(kThreads), 0, s, drows, uint64_t(n), nr);
       HIP_OK(hipGetLastError());
     } else {
       uint32_t nlanes = uint32_t(n / kDivPer);
@@ -649,14 +645,12 @@ void poly_divide_rows(hipStream_t s, uint32_t* io, size_t n, const std::vector<s
       hipLaunchKernelGGL(div_block_kernel, dim3(nblocks, nr), dim3(kThreads), 0, s, drows, nlanes, lanev, lanem,
                          blockv, blockm);
       HIP_OK(hipGetLastError());
-      hipLaunchKernelGGL(div_top_kernel, dim3(nr), dim3(kThreads), 0, s, nblocks, blockv, blockm, rem);
+      hipLaunchKernelGGL(div_top_kernel, dim3(nr), dim3(kThreads), 0, s, drows, nblocks, blockv, blockm);
       HIP_OK(hipGetLastError());
       hipLaunchKernelGGL(div_apply_kernel, dim3(nblocks, nr), dim3(kThreads), 0, s, drows, nlanes, lanev, lanem,
                          blockv);
       HIP_OK(hipGetLastError());
     }
-    for (uint32_t t = 0; t < nr; t++)
-      HIP_OK(hipMemcpyAsync(rem_dev + (uint64_t(ids[t]) * maxz + k) * 4, rem + 4 * t, 16, hipMemcpyDeviceToDevice, s));
   }
 }
 
