@@ -13,6 +13,7 @@ constexpr uint32_t kThreads = 128;
 constexpr uint32_t kInvalid = 0xFFFFFFFFu;  // Fp::invalid()
 constexpr uint32_t kMajors = 13;            // Top's instruction mux (majorOnehot)
 constexpr uint32_t kDataCols = 211;         // the rv32im data group (REGCOUNT_DATA)
+constexpr uint32_t kNoSlot = 0x3FFF, kInjectedCol = 0x4000;  // rv32im_witgen_slot_table() entries
 
 // rv32im-sys/kernels/cxx/preflight.h:21-41 (RawPreflightCycle / RawMemoryTransaction)
 struct PreflightCycle {
@@ -299,15 +300,18 @@ __device__ __forceinline__ uint32_t bigint_byte(const Args& A, uint32_t cycle, u
 // the generated kernels: step_Top specialised to instruction arm `major` over a list of cycles
 void rv32im_witgen_major(uint32_t major, hipStream_t s, const rvwg::Args& A, const uint32_t* list, uint32_t n,
                          uint32_t* cb);
-// each arm's compact slot of every data column ([13][211], -1: never stored) and slot counts
+// each arm's compact slot of every data column ([13][211]: low 14 bits the slot, kNoSlot if the
+// arm never stores the column; kInjectedCol if the injector sets it on the arm's rows) and the
+// arms' slot counts
 const int16_t* rv32im_witgen_slot_table();
 uint32_t rv32im_witgen_nslots(uint32_t major);
 // EQZ messages of the generated code (steps.cpp locations), by index
 const char* rv32im_witgen_message(uint32_t k);
 // the driver (rv32im_witgen.hip): both phases over cycles [0, last_cycle) with the preflight
 // arrays resident on the device; synchronises, throws on a failed check
-// zeroize: the merge writes 0 for INVALID words (eltwise_zeroize fused, as hal_generate_witness
-// does right after stepExec, witgen/mod.rs:166-169)
+// zeroize (the prover's path): the data group is the prover's own, all INVALID but the injector's
+// words, and the merge writes 0 for INVALID words (eltwise_zeroize fused, as
+// hal_generate_witness does right after stepExec, witgen/mod.rs:166-169)
 void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
                        const rvwg::PreflightCycle* d_cycles, const rvwg::MemoryTxn* d_txns, size_t n_txns,
                        const uint8_t* d_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle,

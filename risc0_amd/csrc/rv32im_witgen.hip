@@ -101,12 +101,13 @@ __global__ __launch_bounds__(kBucketThreads) void bin_pos_kernel(const uint32_t*
 
 // the data group from the arms' compact values, a column line at a time: word (col, row) is the
 // row's stored value if its arm stored one, else the data word as the injector left it (an
-// injected value or INVALID); zeroize: INVALID -> 0. Every word of rows [0, rows) is written,
-// so each line of a column goes out whole.
+// injected value or INVALID). Every word of rows [0, rows) is written, so each line of a column
+// goes out whole. prover: the data group is the prover's own (INVALID but where the injector
+// wrote), so only injected columns are read back, and INVALID becomes 0 (the zeroize).
 __global__ __launch_bounds__(kMergeThreads) void merge_kernel(uint32_t* data, uint32_t rows, uint32_t ncycles,
                                                              const uint32_t* cbuf, const uint8_t* keys,
                                                              const uint32_t* pos, const int16_t* slot_of, BinTable T,
-                                                             bool zeroize) {
+                                                             bool prover) {
   __shared__ int16_t slot[rvwg::kMajors * rvwg::kDataCols];
   for (uint32_t t = threadIdx.x; t < rvwg::kMajors * rvwg::kDataCols; t += kMergeThreads) slot[t] = slot_of[t];
   __syncthreads();
@@ -120,11 +121,12 @@ __global__ __launch_bounds__(kMergeThreads) void merge_kernel(uint32_t* data, ui
   const int16_t* sl = slot + arm * rvwg::kDataCols;
 #pragma unroll 8
   for (uint32_t col = 0; col < rvwg::kDataCols; col++) {
-    const int s = stepped ? sl[col] : -1;
+    const uint32_t e = stepped ? uint32_t(sl[col]) : uint32_t(rvwg::kNoSlot | rvwg::kInjectedCol);
+    const uint32_t slot = e & rvwg::kNoSlot;
     uint32_t* p = data + uint64_t(col) * rows + r;
-    uint32_t v = s >= 0 ? cb[size_t(s) * n + i] : rvwg::kInvalid;
-    if (v == rvwg::kInvalid) v = *p;
-    if (zeroize && v == rvwg::kInvalid) v = 0u;
+    uint32_t v = slot != rvwg::kNoSlot ? cb[size_t(slot) * n + i] : rvwg::kInvalid;
+    if (v == rvwg::kInvalid && (!prover || (e & rvwg::kInjectedCol))) v = *p;
+    if (prover && v == rvwg::kInvalid) v = 0u;
     *p = v;
   }
 }
