@@ -490,8 +490,22 @@ def end_to_end_trace(r, hal, args, trace, k):
     starts in host memory and k threads each call r0hip_prove_segment_trace, which stages it
     through the thread's pinned arena onto its own stream while the other threads' proofs run.
     Reported beside `value`, never as it."""
-    cyc, tx = trace.arrays()
-    idx, off, val = trace.injector_arrays()
+    import ctypes
+    lib = r.lib()
+    hosts = []
+
+    def pinned(a):
+        """a copy of `a` in page-locked memory (r0hip_host_alloc), as a producer would hand the
+        trace over: the library then copies it to the device directly, without staging"""
+        a = np.ascontiguousarray(a)
+        p = ctypes.c_void_p()
+        r.check(lib.r0hip_host_alloc(ctypes.byref(p), max(1, a.nbytes)))
+        hosts.append(p.value)
+        v = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(a.nbytes,)).view(a.dtype)
+        v[:] = a.reshape(-1)
+        return v.reshape(a.shape)
+    cyc, tx = (pinned(a) for a in trace.arrays())
+    idx, off, val = (pinned(a) for a in trace.injector_arrays())
     glob = trace.global_words()
     bi = trace.bigint_array()
     bi = bi if len(bi) else None
@@ -510,20 +524,25 @@ def end_to_end_trace(r, hal, args, trace, k):
         for t_ in ts:
             t_.join()
 
-    run(k)  # warm every thread's stream, arena and pool
-    one()  # and this thread's (its staging arena grows to the trace's size once)
-    t0 = time.perf_counter()
-    one()
-    t_one = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    run(args.e2e_steps)
-    t = time.perf_counter() - t0
+    try:
+        run(k)  # warm every thread's stream, arena and pool
+        one()  # and this thread's
+        t0 = time.perf_counter()
+        one()
+        t_one = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        run(args.e2e_steps)
+        t = time.perf_counter() - t0
+    finally:
+        for hp in hosts:
+            r.check(lib.r0hip_host_free(hp))
     return {"value": round(args.e2e_steps * (1 << args.po2) / t, 1), "unit": "cycles/s",
             "ms_per_step": round(1000.0 * t / args.e2e_steps, 3), "steps": args.e2e_steps,
             "segments_in_flight_per_gpu": k, "h2d_bytes_per_segment": int(h2d),
             "ms_one_segment_unpipelined": round(1000.0 * t_one, 1),
-            "note": "the headline's prove_core from a preflight trace, with the trace in host memory (uploaded "
-                    "through each prover thread's pinned staging arena, r0hip_prove_segment_trace)"}
+            "note": "the headline's prove_core from a preflight trace, with the trace in page-locked host memory "
+                    "(r0hip_host_alloc) copied to the device by r0hip_prove_segment_trace on each prover thread's "
+                    "stream"}
 
 
 def pmc_traffic(family, calls, args):

@@ -225,9 +225,18 @@ void* scratch(size_t bytes, int slot) {
 }
 
 // ---- pinned staging for async uploads (per thread) ---------------------------
+bool host_pinned(const void* p, size_t bytes);
+
 void upload_async(void* d_dst, const void* h_src, size_t bytes) {
   if (!bytes) return;
   ensure_init();
+  // source inside a live r0hip_host_alloc block: already page-locked, copy it directly (the
+  // callers keep their sources alive until the stream has drained: every entry point that
+  // takes host arrays returns only after its work is done)
+  if (bytes >= (size_t(64) << 10) && host_pinned(h_src, bytes)) {
+    HIP_OK(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, t_ctx.stream));
+    return;
+  }
   Stage& st = t_ctx.stage;
   size_t need = (bytes + 255) & ~size_t(255);
   if (st.used + need > st.cap) {
@@ -406,6 +415,17 @@ void* host_alloc(size_t bytes) {
   std::lock_guard<std::mutex> lk(g_host_mu);
   g_host_size[p] = bytes;
   return p;
+}
+
+// [p, p + bytes) lies inside one live (not freed) r0hip_host_alloc block
+bool host_pinned(const void* p, size_t bytes) {
+  std::lock_guard<std::mutex> lk(g_host_mu);
+  auto it = g_host_size.upper_bound(const_cast<void*>(p));
+  if (it == g_host_size.begin()) return false;
+  --it;
+  const auto* base = static_cast<const uint8_t*>(it->first);
+  const auto* q = static_cast<const uint8_t*>(p);
+  return q >= base && q + bytes <= base + it->second && !g_host_idle.count(it->first);
 }
 
 void host_free(void* p) {
