@@ -80,20 +80,25 @@ __device__ __forceinline__ void fail(const Args& A, uint32_t code, uint32_t cycl
   }
 }
 
-// Buffer::get / Buffer::set with checked = true. `view` is A.data, or for the injected
-// columns a read-only alias the generated kernels declare __restrict__ (see
-// tools/gen_rv32im_witgen.py, Path)
-__device__ __forceinline__ uint32_t ld(const Args& A, const uint32_t* view, uint32_t col, uint32_t row, uint32_t cycle) {
-  const uint32_t v = view[uint64_t(col) * A.rows + row];
-  if (v == kInvalid) fail(A, kErrUnset, cycle, col);
-  return v;
+// A lane's first failed check, in program order, kept in two registers without a branch;
+// the kernel reports it once, at its end (fail). The reference throws at the first failure;
+// later values of a failed cycle are garbage here, but the call fails with that first error.
+struct Err {
+  uint32_t code, detail;
+};
+__device__ __forceinline__ void note(Err& e, bool bad, uint32_t code, uint32_t detail = 0u) {
+  const bool first = bad && e.code == 0u;
+  e.code = first ? code : e.code;
+  e.detail = first ? detail : e.detail;
 }
 
-__device__ __forceinline__ void st(const Args& A, const uint32_t* view, uint32_t col, uint32_t cycle, uint32_t v) {
-  const uint64_t i = uint64_t(col) * A.rows + cycle;
-  const uint32_t old = view[i];
-  if (old != kInvalid && old != v) fail(A, kErrInconsistent, cycle, col);
-  A.data[i] = v;
+// Buffer::get with checked = true. `view` is A.data, or for the injected columns a read-only
+// alias the generated kernels declare __restrict__ (see tools/gen_rv32im_witgen.py, Path)
+__device__ __forceinline__ uint32_t ld(const Args& A, Err& err, const uint32_t* view, uint32_t col, uint32_t row,
+                                       uint32_t cycle) {
+  const uint32_t v = view[uint64_t(col) * A.rows + row];
+  note(err, v == kInvalid, kErrUnset, col);
+  return v;
 }
 
 // The arm kernels keep this cycle's own row values in a compact, slot-major buffer of their
@@ -110,53 +115,54 @@ __device__ __forceinline__ void stc(uint32_t* cb, uint32_t n, uint32_t i, uint32
 }
 
 // the row's value of a column stored earlier on some path of this cycle: its slot (checked get)
-__device__ __forceinline__ uint32_t ldc(const Args& A, const uint32_t* cb, uint32_t n, uint32_t i, uint32_t slot,
-                                        uint32_t col, uint32_t cycle) {
+__device__ __forceinline__ uint32_t ldc(const Args& A, Err& err, const uint32_t* cb, uint32_t n, uint32_t i,
+                                        uint32_t slot, uint32_t col, uint32_t cycle) {
   const uint32_t v = cb[size_t(slot) * n + i];
-  if (v == kInvalid) fail(A, kErrUnset, cycle, col);
+  note(err, v == kInvalid, kErrUnset, col);
   return v;
 }
 
 // checked set of an injected column: the old value is the injector's (data, read-only view)
-__device__ __forceinline__ void st_inj(const Args& A, const uint32_t* view, uint32_t* cb, uint32_t n, uint32_t i,
-                                       uint32_t slot, uint32_t col, uint32_t cycle, uint32_t v) {
+__device__ __forceinline__ void st_inj(const Args& A, Err& err, const uint32_t* view, uint32_t* cb, uint32_t n,
+                                       uint32_t i, uint32_t slot, uint32_t col, uint32_t cycle, uint32_t v) {
   const uint32_t old = view[uint64_t(col) * A.rows + cycle];
-  if (old != kInvalid && old != v) fail(A, kErrInconsistent, cycle, col);
+  note(err, old != kInvalid && old != v, kErrInconsistent, col);
   cb[size_t(slot) * n + i] = v;
 }
 
 // checked set of a column some earlier path of this cycle may have stored
-__device__ __forceinline__ void st_maybe(const Args& A, uint32_t* cb, uint32_t n, uint32_t i, uint32_t slot, uint32_t col,
-                                         uint32_t cycle, uint32_t v) {
+__device__ __forceinline__ void st_maybe(const Args& A, Err& err, uint32_t* cb, uint32_t n, uint32_t i, uint32_t slot,
+                                         uint32_t col, uint32_t cycle, uint32_t v) {
   uint32_t* p = cb + size_t(slot) * n + i;
   const uint32_t old = *p;
-  if (old != kInvalid && old != v) fail(A, kErrInconsistent, cycle, col);
+  note(err, old != kInvalid && old != v, kErrInconsistent, col);
   *p = v;
 }
 
-__device__ __forceinline__ uint32_t gld(const Args& A, uint32_t idx, uint32_t cycle) {
+__device__ __forceinline__ uint32_t gld(const Args& A, Err& err, uint32_t idx, uint32_t cycle) {
   const uint32_t v = A.global[idx];
-  if (v == kInvalid) fail(A, kErrUnset, cycle, 0x10000u + idx);
+  note(err, v == kInvalid, kErrUnset, 0x10000u + idx);
   return v;
 }
 
-__device__ __forceinline__ void gst(const Args& A, uint32_t idx, uint32_t cycle, uint32_t v) {
+__device__ __forceinline__ void gst(const Args& A, Err& err, uint32_t idx, uint32_t cycle, uint32_t v) {
   const uint32_t old = A.global[idx];
-  if (old != kInvalid && old != v) fail(A, kErrInconsistent, cycle, 0x10000u + idx);
+  note(err, old != kInvalid && old != v, kErrInconsistent, 0x10000u + idx);
   A.global[idx] = v;
 }
 
-// extern_getMemoryTxn (ffi.cpp:84-113): the cycle's next transaction
-__device__ __forceinline__ void txn(const Args& A, const MemoryTxn* txs, uint32_t cycle, uint32_t& cur, uint32_t addr_w,
-                                    uint32_t& prev_cycle, uint32_t& prev_lo, uint32_t& prev_hi, uint32_t& lo, uint32_t& hi) {
-  if (cur >= A.n_txns) {
-    fail(A, kErrTxnRange, cycle, cur);
-    prev_cycle = prev_lo = prev_hi = lo = hi = 0u;
-    return;
-  }
-  const MemoryTxn t = txs[cur++];
-  if (t.cycle / 2 != cycle) fail(A, kErrTxnCycle, cycle, t.cycle);
-  if (t.addr != to_u32(addr_w)) fail(A, kErrTxnAddr, cycle, t.addr);
+// extern_getMemoryTxn (ffi.cpp:84-113): the cycle's next transaction. A.txns always holds at
+// least one record (rv32im_witgen_dev points it at a zero record when the trace has none), so
+// a cursor past the end reads record 0 and reports the overrun.
+__device__ __forceinline__ void txn(const Args& A, Err& err, const MemoryTxn* txs, uint32_t cycle, uint32_t& cur,
+                                    uint32_t addr_w, uint32_t& prev_cycle, uint32_t& prev_lo, uint32_t& prev_hi,
+                                    uint32_t& lo, uint32_t& hi) {
+  const bool oob = cur >= A.n_txns;
+  note(err, oob, kErrTxnRange, cur);
+  const MemoryTxn t = txs[oob ? 0u : cur];
+  cur++;
+  note(err, t.cycle / 2 != cycle, kErrTxnCycle, t.cycle);
+  note(err, t.addr != to_u32(addr_w), kErrTxnAddr, t.addr);
   prev_cycle = from_u32(t.prev_cycle);
   prev_lo = from_u32(t.prev_word & 0xFFFFu);
   prev_hi = from_u32(t.prev_word >> 16);
@@ -166,12 +172,11 @@ __device__ __forceinline__ void txn(const Args& A, const MemoryTxn* txs, uint32_
 
 // extern_hostReadPrepare / extern_hostWrite (ffi.cpp:201-212): the word of the cycle's next
 // transaction, without advancing
-__device__ __forceinline__ uint32_t host_word(const Args& A, const MemoryTxn* txs, uint32_t cycle, uint32_t cur) {
-  if (cur >= A.n_txns) {
-    fail(A, kErrTxnRange, cycle, cur);
-    return 0u;
-  }
-  return from_u32(txs[cur].word);
+__device__ __forceinline__ uint32_t host_word(const Args& A, Err& err, const MemoryTxn* txs, uint32_t cycle,
+                                              uint32_t cur) {
+  const bool oob = cur >= A.n_txns;
+  note(err, oob, kErrTxnRange, cur);
+  return from_u32(txs[oob ? 0u : cur].word);
 }
 
 // The workgroup's lookup counts in LDS, added to the device tables once at the kernel's end:
@@ -219,18 +224,15 @@ __device__ __forceinline__ void u16_count(const Args& A, const LdsTables& T, uin
 }
 
 // LookupTables::lookupDelta (tables.h:33-53; the count argument is not used there either)
-__device__ __forceinline__ void lookup_delta(const Args& A, uint32_t cycle, uint32_t table_w, uint32_t index_w,
-                                             const LdsTables& T) {
+__device__ __forceinline__ void lookup_delta(const Args& A, Err& err, uint32_t cycle, uint32_t table_w,
+                                             uint32_t index_w, const LdsTables& T) {
   const uint32_t table = to_u32(table_w), index = to_u32(index_w);
   if (table == 0u) return;
-  if (table != 8u && table != 16u) {
-    fail(A, kErrLookupTable, cycle, table);
-    return;
-  }
-  if (index >= (1u << table)) {
-    fail(A, kErrLookupIndex, cycle, index);
-    return;
-  }
+  const bool bad_t = table != 8u && table != 16u;
+  const bool bad_i = !bad_t && index >= (1u << table);
+  note(err, bad_t, kErrLookupTable, table);
+  note(err, bad_i, kErrLookupIndex, index);
+  if (bad_t || bad_i) return;
   if (table == 8u)
     atomicAdd(T.h8 + index, 1u);
   else
@@ -238,23 +240,23 @@ __device__ __forceinline__ void lookup_delta(const Args& A, uint32_t cycle, uint
 }
 
 // LookupTables::lookupCurrent (tables.h:55-66)
-__device__ __forceinline__ uint32_t lookup_current(const Args& A, uint32_t cycle, uint32_t table_w, uint32_t index_w) {
+__device__ __forceinline__ uint32_t lookup_current(const Args& A, Err& err, uint32_t cycle, uint32_t table_w,
+                                                   uint32_t index_w) {
   const uint32_t table = to_u32(table_w), index = to_u32(index_w);
-  if ((table != 8u && table != 16u) || index >= (1u << table)) {
-    fail(A, table != 8u && table != 16u ? kErrLookupTable : kErrLookupIndex, cycle, index);
-    return 0u;
-  }
-  return from_u32(__hip_atomic_load((table == 8u ? A.u8 : A.u16) + index, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const bool bad_t = table != 8u && table != 16u;
+  const bool bad_i = !bad_t && index >= (1u << table);
+  note(err, bad_t, kErrLookupTable, index);
+  note(err, bad_i, kErrLookupIndex, index);
+  const uint32_t* tab = table == 8u ? A.u8 : A.u16;
+  return from_u32(__hip_atomic_load(tab + (bad_t || bad_i ? 0u : index), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
 // extern_getDiffCount (ffi.cpp:141-145)
-__device__ __forceinline__ uint32_t diff_count(const Args& A, uint32_t cycle, uint32_t c_w) {
+__device__ __forceinline__ uint32_t diff_count(const Args& A, Err& err, uint32_t cycle, uint32_t c_w) {
   const uint32_t c = to_u32(c_w);
-  if (c / 2 >= A.ncycles) {
-    fail(A, kErrDiffCount, cycle, c);
-    return 0u;
-  }
-  return from_u32(A.cycles[c / 2].diff_count[c % 2]);
+  const bool bad = c / 2 >= A.ncycles;
+  note(err, bad, kErrDiffCount, c);
+  return from_u32(A.cycles[bad ? 0u : c / 2].diff_count[c % 2]);
 }
 
 // divide_rv32im + extern_divide (ffi.cpp:54-82, 177-188)
@@ -285,14 +287,12 @@ __device__ __forceinline__ void divide(uint32_t nl, uint32_t nh, uint32_t dl, ui
   r1 = from_u32(rem >> 16);
 }
 
-// extern_bigIntExtern (ffi.cpp:221-228)
-__device__ __forceinline__ uint32_t bigint_byte(const Args& A, uint32_t cycle, uint32_t i) {
+// extern_bigIntExtern (ffi.cpp:221-228); A.bigint always holds at least one byte (as A.txns)
+__device__ __forceinline__ uint32_t bigint_byte(const Args& A, Err& err, uint32_t cycle, uint32_t i) {
   const uint32_t k = A.cycles[cycle].bigint_idx + i;
-  if (k >= A.n_bigint) {
-    fail(A, kErrBigint, cycle, k);
-    return 0u;
-  }
-  return from_u32(A.bigint[k]);
+  const bool bad = k >= A.n_bigint;
+  note(err, bad, kErrBigint, k);
+  return from_u32(A.bigint[bad ? 0u : k]);
 }
 
 }  // namespace rvwg

@@ -149,19 +149,22 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
     if (zeroize) eltwise_zeroize(s, data, rows * kDataCols);
     return;
   }
-  // lookup tables, error record and bucket counts in one scratch block
-  auto* tab = static_cast<uint32_t*>(scratch((256 + 65536 + 4 + kBins) * 4, kSlotRvwgTables));
+  // lookup tables, error record, bucket counts and a zero transaction record / bigint byte (what
+  // an empty trace's pointers show the kernels) in one scratch block
+  constexpr size_t kTabWords = 256 + 65536 + 4 + kBins + 8;
+  auto* tab = static_cast<uint32_t*>(scratch(kTabWords * 4, kSlotRvwgTables));
   auto* d_list = static_cast<uint32_t*>(scratch(size_t(last_cycle) * 4, kSlotRvwgLists));
-  HIP_OK(hipMemsetD32Async(tab, 0, 256 + 65536 + 4 + kBins, s));
+  HIP_OK(hipMemsetD32Async(tab, 0, kTabWords, s));
+  const uint32_t* zero_rec = tab + 256 + 65536 + 4 + kBins;
   Args A{};
   A.data = data;
   A.global = global;
   A.rows = uint32_t(rows);
   A.ncycles = last_cycle;
   A.cycles = d_cycles;
-  A.txns = d_txns;
+  A.txns = n_txns ? d_txns : reinterpret_cast<const MemoryTxn*>(zero_rec);
   A.n_txns = uint32_t(n_txns);
-  A.bigint = d_bigint;
+  A.bigint = n_bigint ? d_bigint : reinterpret_cast<const uint8_t*>(zero_rec);
   A.n_bigint = uint32_t(n_bigint);
   A.u8 = tab;
   A.u16 = tab + 256;
