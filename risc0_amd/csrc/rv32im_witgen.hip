@@ -19,6 +19,7 @@
 // already resident (rv32im_witgen_dev). The cycles are bucketed on the device (counts, one
 // 27-word read-back for the launch sizes, fill). Checks that throw in the reference record an
 // error code and the cycle, raised after the kernels drain.
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -67,7 +68,7 @@ constexpr uint32_t kMergeThreads = 256;
 // reference's OneHot EQZ on majorOnehot fails for it). keys/vals: each cycle's bin and index,
 // for the stable sort into cycle order within each bin.
 __global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(rvwg::Args A, uint32_t split, uint32_t* counts,
-                                                                     uint8_t* keys, uint32_t* vals) {
+                                                                     uint8_t* keys, uint32_t* vals, uint32_t minor_bits) {
   __shared__ uint32_t h[kBins];
   if (threadIdx.x < kBins) h[threadIdx.x] = 0;
   __syncthreads();
@@ -79,7 +80,9 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(rvwg::Args
       rvwg::fail(A, rvwg::kErrMajor, c, m);
     else
       atomicAdd(&h[b], 1u);
-    keys[c] = uint8_t(m >= rvwg::kMajors ? kBins : b);
+    // the sort key: the bin, and with minor_bits = 3 the minor below it (a bin's cycles then
+    // run minor by minor: fewer divergent minor arms per wavefront, rows further apart)
+    keys[c] = uint8_t(((m >= rvwg::kMajors ? kBins : b) << minor_bits) | (A.cycles[c].minor & ((1u << minor_bits) - 1u)));
     vals[c] = c;
   }
   __syncthreads();
@@ -87,6 +90,7 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(rvwg::Args
 }
 
 struct BinTable {
+  uint32_t minor_bits;      // sort keys are bin << minor_bits | minor
   uint32_t off[kBins + 1];  // first list index of each bin
   uint32_t cnt[kBins];
   uint64_t cbase[kBins];    // each bin's compact values in the compact buffer (words)
@@ -96,7 +100,7 @@ struct BinTable {
 __global__ __launch_bounds__(kBucketThreads) void bin_pos_kernel(const uint32_t* list, const uint8_t* sorted_keys,
                                                                 uint32_t n, BinTable T, uint32_t* pos) {
   const uint32_t j = blockIdx.x * kBucketThreads + threadIdx.x;
-  if (j < n) pos[list[j]] = j - T.off[sorted_keys[j]];
+  if (j < n) pos[list[j]] = j - T.off[sorted_keys[j] >> T.minor_bits];
 }
 
 // the data group from the arms' compact values, a column line at a time: word (col, row) is the
@@ -114,7 +118,7 @@ __global__ __launch_bounds__(kMergeThreads) void merge_kernel(uint32_t* data, ui
   const uint32_t r = blockIdx.x * kMergeThreads + threadIdx.x;
   if (r >= rows) return;
   const bool stepped = r < ncycles;
-  const uint32_t b = stepped ? keys[r] : 0u;
+  const uint32_t b = stepped ? uint32_t(keys[r]) >> T.minor_bits : 0u;
   const uint32_t arm = b % rvwg::kMajors;
   const uint32_t n = stepped ? T.cnt[b] : 0u, i = stepped ? pos[r] : 0u;
   const uint32_t* cb = cbuf + (stepped ? T.cbase[b] : 0u);
@@ -180,10 +184,17 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
   uint8_t* keys_out = kb + last_cycle;
   uint32_t* vals = reinterpret_cast<uint32_t*>(kb + kb_bytes);
   uint32_t* pos = vals + last_cycle;
+  // R0_RVWG_MINOR=1: order each bin's cycles by minor too (an A/B switch; the default keeps
+  // cycle order, measured faster)
+  static const uint32_t minor_bits = [] {
+    const char* e = std::getenv("R0_RVWG_MINOR");
+    return e && e[0] == '1' ? 3u : 0u;
+  }();
   uint32_t h[4 + kBins];
   {
     KScope ks("rv32im_witgen_bucket", double(last_cycle) * 2 * sizeof(PreflightCycle));
-    hipLaunchKernelGGL(bucket_count_kernel, dim3(g), dim3(kBucketThreads), 0, s, A, table_split, counts, keys, vals);
+    hipLaunchKernelGGL(bucket_count_kernel, dim3(g), dim3(kBucketThreads), 0, s, A, table_split, counts, keys, vals,
+                       minor_bits);
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(h, A.err, sizeof(h), hipMemcpyDeviceToHost, s));  // err[0..2], pad, counts
     HIP_OK(hipStreamSynchronize(s));
@@ -191,6 +202,7 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
   R0_REQUIRE(h[0] == 0, "rv32im witgen: " + witgen_error(h));
   const uint32_t* cnt = h + 4;  // counts start at A.err + 4
   BinTable T{};
+  T.minor_bits = minor_bits;
   T.off[0] = 0;
   size_t cwords = 0;
   for (uint32_t b = 0; b < kBins; b++) {
@@ -201,9 +213,12 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
   }
   R0_REQUIRE(T.off[kBins] == last_cycle, "rv32im witgen: bucket counts do not add up");
   size_t temp_bytes = 0;
-  HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, keys_out, vals, d_list, int(last_cycle), 0, 5, s));
+  const int end_bit = 5 + int(minor_bits);
+  HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, temp_bytes, keys, keys_out, vals, d_list, int(last_cycle), 0,
+                                            end_bit, s));
   void* temp = scratch(temp_bytes + 256, kSlotRvwgSortTemp);
-  HIP_OK(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys_out, vals, d_list, int(last_cycle), 0, 5, s));
+  HIP_OK(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys, keys_out, vals, d_list, int(last_cycle), 0,
+                                            end_bit, s));
   hipLaunchKernelGGL(bin_pos_kernel, dim3(g), dim3(kBucketThreads), 0, s, d_list, keys_out, last_cycle, T, pos);
   HIP_OK(hipGetLastError());
   // the arms' compact values, INVALID until stored
