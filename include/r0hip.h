@@ -233,6 +233,8 @@ const char* r0hip_rv32im_witgen(uint32_t mode, const r0hip_raw_exec_buffers* buf
  * r0hip_prove_segment_accum takes them. Runs: data INVALID, scatter, stepExec (both phases),
  * zeroize, then the prove_core sequence with the version word 2 (RV32IM_SEAL_VERSION) and the
  * accumulation on the device. Seal and mix out as r0hip_prove_segment. */
+/* Host arrays of 64 KiB or more that lie inside r0hip_host_alloc blocks are copied to the
+ * device directly; others are staged through the calling thread's page-locked arena. */
 const char* r0hip_prove_segment_trace(int suite, uint32_t po2, uint32_t mode, const uint32_t* h_global,
                                       const uint32_t* h_inj_index, size_t inj_rows, const uint32_t* h_inj_offsets,
                                       const uint32_t* h_inj_values, const r0hip_raw_preflight_trace* preflight,
