@@ -184,11 +184,12 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
   uint8_t* keys_out = kb + last_cycle;
   uint32_t* vals = reinterpret_cast<uint32_t*>(kb + kb_bytes);
   uint32_t* pos = vals + last_cycle;
-  // R0_RVWG_MINOR=1: order each bin's cycles by minor too (an A/B switch; the default keeps
-  // cycle order, measured faster)
+  // each bin's cycles ordered by minor, then cycle: a wavefront's lanes mostly share the arm's
+  // minor mux branch (phase 1 at po2=20: 1.27 -> 0.85 ms, the merge's gathers 0.57 -> 0.73 ms;
+  // `profiles/r4l_*`). R0_RVWG_MINOR=0 keeps plain cycle order.
   static const uint32_t minor_bits = [] {
     const char* e = std::getenv("R0_RVWG_MINOR");
-    return e && e[0] == '1' ? 3u : 0u;
+    return e && e[0] == '0' ? 0u : 3u;
   }();
   uint32_t h[4 + kBins];
   {
