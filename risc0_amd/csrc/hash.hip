@@ -406,11 +406,19 @@ void merkle_tree(hipStream_t s, int suite, uint32_t* nodes, const uint32_t* matr
   merkle_layers(s, suite, nodes, rows);
 }
 
+// Poseidon2 tree tops start at this many nodes (R0_P2_TOP_NODES, a power of two <= 512): the
+// layers above it are separate multi-CU launches, the ones from it to the root one workgroup
+static size_t p2_top_nodes() {
+  static const size_t v = env_size("R0_P2_TOP_NODES", 512);
+  return v;
+}
+
 void merkle_layers(hipStream_t s, int suite, uint32_t* nodes, size_t rows) {
   static const char* names[3] = {"merkle_fold_poseidon2", "merkle_fold_sha256", "merkle_fold_poseidon254"};
   KScope ks(names[suite], double(rows) * 32 * 1.5, suite == 0 ? double(rows - 1) * kP2Modmuls : 0);
   size_t layer = rows / 2;
-  for (; layer > 512; layer /= 2) hash_fold(s, suite, nodes, 2 * layer, layer);
+  const size_t top = suite == 0 ? std::min<size_t>(512, p2_top_nodes()) : 512;
+  for (; layer > top; layer /= 2) hash_fold(s, suite, nodes, 2 * layer, layer);
   if (layer >= 1) {
     const dim3 grid(1), block(kThreads);
     if (suite == 0) hipLaunchKernelGGL(p2_fold_top_kernel, grid, dim3(kTopThreads), 0, s, nodes, uint32_t(layer),
