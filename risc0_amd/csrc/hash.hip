@@ -407,9 +407,11 @@ void merkle_tree(hipStream_t s, int suite, uint32_t* nodes, const uint32_t* matr
 }
 
 // Poseidon2 tree tops start at this many nodes (R0_P2_TOP_NODES, a power of two <= 512): the
-// layers above it are separate multi-CU launches, the ones from it to the root one workgroup
+// layers above it are separate multi-CU launches (quad kernels, ~11 us each), the ones from it
+// to the root one workgroup of quads. The one-workgroup top took 114 us from 512 nodes (the 512-
+// and 256-node layers one lane per node, two waves per SIMD), 63 us from 64 (`profiles/r4m_*`).
 static size_t p2_top_nodes() {
-  static const size_t v = env_size("R0_P2_TOP_NODES", 512);
+  static const size_t v = env_size("R0_P2_TOP_NODES", 64);
   return v;
 }
 
