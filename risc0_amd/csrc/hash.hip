@@ -106,42 +106,6 @@ __global__ __launch_bounds__(kThreads) void p2_fold_quad_kernel(uint32_t* io, ui
   dst[4 + q] = c[1];
 }
 
-// The small layers and the root in one launch, as a dataflow: a quad hashes its node of the
-// first layer (n nodes: [n, 2n)), publishes it and counts its arrival at the parent; the
-// second child to arrive hashes the parent, and so on up to the root (node 1), while first
-// arrivers stop. No layer barrier and no launch per layer: the longest chain is log2(n) + 1
-// dependent permutations. Publication is a device-scope release (the node's words written
-// back past this XCD's L2) before the counter's atomic, and the climbing quad acquires (its
-// L2 copy invalidated) before reading the sibling: siblings share a cache line and may have
-// been written by another XCD. Every quad exits after at most log2(n) + 1 permutations.
-__global__ __launch_bounds__(kThreads) void p2_fold_tree_kernel(uint32_t* io, uint64_t n, uint32_t* arrivals) {
-  const uint64_t t = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
-  const uint64_t i = t >> 2;
-  if (i >= n) return;  // whole quads: n * 4 lanes
-  const uint32_t q = threadIdx.x & 3;
-  uint64_t node = n + i;
-  for (;;) {
-    const uint32_t* src = io + 2 * node * 8;
-    uint32_t c[6];
-#pragma unroll
-    for (int j = 0; j < 4; j++) c[j] = src[4 * j + q];
-    c[4] = c[5] = 0;
-    poseidon2_mix_quad(c);
-    uint32_t* dst = io + node * 8;
-    dst[q] = c[0];
-    dst[4 + q] = c[1];
-    if (node == 1) break;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    uint32_t prior = 0;
-    if (q == 0)
-      prior = __hip_atomic_fetch_add(arrivals + (node >> 1), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    prior = __shfl(prior, 0, 4);
-    if (prior == 0) break;  // the sibling hashes the parent
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    node >>= 1;
-  }
-}
-
 // ---- Poseidon254 (BN254 Fr, poseidon_254/mod.rs) ---------------------------------
 // One lane per row as above; the 3-cell state is 27 VGPRs of 29-bit limbs. Row values are
 // decoded from Montgomery to canonical (Elem::as_u32) and packed 8 per cell.
@@ -446,14 +410,12 @@ void merkle_tree(hipStream_t s, int suite, uint32_t* nodes, const uint32_t* matr
 // layers above it are separate multi-CU launches (quad kernels, ~11 us each), the ones from it
 // to the root one workgroup of quads. The one-workgroup top took 114 us from 512 nodes (the 512-
 // and 256-node layers one lane per node, two waves per SIMD), 63 us from 64 (`profiles/r4m_*`).
+// Measured and rejected: every layer of <= 32768 nodes plus the root in one dataflow launch
+// (the second child to arrive hashes the parent, agent-scope release/acquire around a per-
+// parent counter): 419 us per tree against 140 us, the L2 write-back and invalidate of each
+// release/acquire costing more than the launches they save (`profiles/r4n_merkle_tree_ab.txt`).
 static size_t p2_top_nodes() {
   static const size_t v = env_size("R0_P2_TOP_NODES", 64);
-  return v;
-}
-
-// R0_P2_TREE=0: the per-layer launches and the one-workgroup top instead of the dataflow kernel
-static bool p2_tree_fold() {
-  static const bool v = env_size("R0_P2_TREE", 1) != 0;
   return v;
 }
 
@@ -461,19 +423,6 @@ void merkle_layers(hipStream_t s, int suite, uint32_t* nodes, size_t rows) {
   static const char* names[3] = {"merkle_fold_poseidon2", "merkle_fold_sha256", "merkle_fold_poseidon254"};
   KScope ks(names[suite], double(rows) * 32 * 1.5, suite == 0 ? double(rows - 1) * kP2Modmuls : 0);
   size_t layer = rows / 2;
-  if (suite == 0 && p2_tree_fold()) {
-    // the large layers one launch each, then every layer of <= quad_fold_max() nodes and the
-    // root in one dataflow launch
-    for (; layer > quad_fold_max(); layer /= 2) hash_fold(s, suite, nodes, 2 * layer, layer);
-    if (layer >= 1) {
-      auto* arrivals = static_cast<uint32_t*>(scratch(layer * 4 + 16, kSlotMerkleArrivals));
-      HIP_OK(hipMemsetD32Async(arrivals, 0, layer, s));
-      hipLaunchKernelGGL(p2_fold_tree_kernel, dim3(div_up(4 * layer, kThreads)), dim3(kThreads), 0, s, nodes,
-                         uint64_t(layer), arrivals);
-      HIP_OK(hipGetLastError());
-    }
-    return;
-  }
   const size_t top = suite == 0 ? std::min<size_t>(512, p2_top_nodes()) : 512;
   for (; layer > top; layer /= 2) hash_fold(s, suite, nodes, 2 * layer, layer);
   if (layer >= 1) {

@@ -108,8 +108,6 @@ enum ScratchSlot : int {
   kSlotRvwgKeys = 83,
   kSlotRvwgSortTemp = 84,
   kSlotRvwgCompact = 85,
-  // Merkle tree dataflow fold (hash.hip): per-parent arrival counters
-  kSlotMerkleArrivals = 86,
   // r0hip_prove_segment_trace (api.cpp): the injector's index, offsets and values
   kSlotRvInjIndex = 80,
   kSlotRvInjOffsets = 81,
