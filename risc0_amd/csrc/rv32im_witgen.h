@@ -103,40 +103,47 @@ __device__ __forceinline__ uint32_t ld(const Args& A, Err& err, const uint32_t* 
 
 // The arm kernels keep this cycle's own row values in a compact, slot-major buffer of their
 // bin (cb[slot * n + i], lane i = the cycle's place in the bin's list: one coalesced store per
-// column for a wavefront), pre-filled with INVALID; rv32im_witgen.hip's merge writes them into
-// the column-major data group afterwards, whole lines at a time. (Writing the data group from
-// the arm kernels directly cost ≈3.7 GB of partial-line writes per po2=20 segment: a line of a
-// column holds 32 consecutive cycles of every arm.)
+// column for a wavefront), with a bit per slot in the lane's mask words sm0.. (stored after the
+// slots, cb[(nslots + w) * n + i]): a slot is read only if its bit is set, so the buffer needs
+// no INVALID fill. rv32im_witgen.hip's merge writes the values into the column-major data
+// group afterwards, whole lines at a time. (Writing the data group from the arm kernels
+// directly cost ≈3.7 GB of partial-line writes per po2=20 segment: a line of a column holds
+// 32 consecutive cycles of every arm.)
 //
 // a store whose cell the generator knows to be INVALID (set by no injector and by no earlier
 // store of this cycle): the checked set cannot fail
-__device__ __forceinline__ void stc(uint32_t* cb, uint32_t n, uint32_t i, uint32_t slot, uint32_t v) {
+__device__ __forceinline__ void stc(uint32_t* cb, uint32_t n, uint32_t i, uint32_t slot, uint32_t v, uint32_t& smw,
+                                    uint32_t bit) {
   cb[size_t(slot) * n + i] = v;
+  smw |= bit;
 }
 
 // the row's value of a column stored earlier on some path of this cycle: its slot (checked get)
 __device__ __forceinline__ uint32_t ldc(const Args& A, Err& err, const uint32_t* cb, uint32_t n, uint32_t i,
-                                        uint32_t slot, uint32_t col, uint32_t cycle) {
-  const uint32_t v = cb[size_t(slot) * n + i];
+                                        uint32_t slot, uint32_t col, uint32_t cycle, uint32_t smw, uint32_t bit) {
+  const uint32_t v = (smw & bit) ? cb[size_t(slot) * n + i] : kInvalid;
   note(err, v == kInvalid, kErrUnset, col);
   return v;
 }
 
 // checked set of an injected column: the old value is the injector's (data, read-only view)
 __device__ __forceinline__ void st_inj(const Args& A, Err& err, const uint32_t* view, uint32_t* cb, uint32_t n,
-                                       uint32_t i, uint32_t slot, uint32_t col, uint32_t cycle, uint32_t v) {
+                                       uint32_t i, uint32_t slot, uint32_t col, uint32_t cycle, uint32_t v,
+                                       uint32_t& smw, uint32_t bit) {
   const uint32_t old = view[uint64_t(col) * A.rows + cycle];
   note(err, old != kInvalid && old != v, kErrInconsistent, col);
   cb[size_t(slot) * n + i] = v;
+  smw |= bit;
 }
 
 // checked set of a column some earlier path of this cycle may have stored
 __device__ __forceinline__ void st_maybe(const Args& A, Err& err, uint32_t* cb, uint32_t n, uint32_t i, uint32_t slot,
-                                         uint32_t col, uint32_t cycle, uint32_t v) {
+                                         uint32_t col, uint32_t cycle, uint32_t v, uint32_t& smw, uint32_t bit) {
   uint32_t* p = cb + size_t(slot) * n + i;
-  const uint32_t old = *p;
+  const uint32_t old = (smw & bit) ? *p : kInvalid;
   note(err, old != kInvalid && old != v, kErrInconsistent, col);
   *p = v;
+  smw |= bit;
 }
 
 __device__ __forceinline__ uint32_t gld(const Args& A, Err& err, uint32_t idx, uint32_t cycle) {

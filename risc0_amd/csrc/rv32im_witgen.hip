@@ -91,6 +91,7 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(rvwg::Args
 
 struct BinTable {
   uint32_t minor_bits;      // sort keys are bin << minor_bits | minor
+  uint32_t nslots[rvwg::kMajors];  // each arm's slots; its mask words follow them
   uint32_t off[kBins + 1];  // first list index of each bin
   uint32_t cnt[kBins];
   uint64_t cbase[kBins];    // each bin's compact values in the compact buffer (words)
@@ -112,23 +113,29 @@ __global__ __launch_bounds__(kMergeThreads) void merge_kernel(uint32_t* data, ui
                                                              const uint32_t* cbuf, const uint8_t* keys,
                                                              const uint32_t* pos, const int16_t* slot_of, BinTable T,
                                                              bool prover) {
+  constexpr uint32_t kMaskWords = (rvwg::kDataCols + 31) / 32;
   __shared__ int16_t slot[rvwg::kMajors * rvwg::kDataCols];
+  __shared__ uint32_t msk[kMaskWords][kMergeThreads];  // this thread's row: its arm's stored-slot bits
   for (uint32_t t = threadIdx.x; t < rvwg::kMajors * rvwg::kDataCols; t += kMergeThreads) slot[t] = slot_of[t];
-  __syncthreads();
   const uint32_t r = blockIdx.x * kMergeThreads + threadIdx.x;
-  if (r >= rows) return;
   const bool stepped = r < ncycles;
   const uint32_t b = stepped ? uint32_t(keys[r]) >> T.minor_bits : 0u;
   const uint32_t arm = b % rvwg::kMajors;
   const uint32_t n = stepped ? T.cnt[b] : 0u, i = stepped ? pos[r] : 0u;
   const uint32_t* cb = cbuf + (stepped ? T.cbase[b] : 0u);
+  const uint32_t ns = T.nslots[arm];
+  for (uint32_t w = 0; w < kMaskWords; w++)
+    msk[w][threadIdx.x] = stepped && 32 * w < ns ? cb[size_t(ns + w) * n + i] : 0u;
+  __syncthreads();
+  if (r >= rows) return;
   const int16_t* sl = slot + arm * rvwg::kDataCols;
 #pragma unroll 8
   for (uint32_t col = 0; col < rvwg::kDataCols; col++) {
     const uint32_t e = stepped ? uint32_t(sl[col]) : uint32_t(rvwg::kNoSlot | rvwg::kInjectedCol);
     const uint32_t slot = e & rvwg::kNoSlot;
     uint32_t* p = data + uint64_t(col) * rows + r;
-    uint32_t v = slot != rvwg::kNoSlot ? cb[size_t(slot) * n + i] : rvwg::kInvalid;
+    const bool stored = slot != rvwg::kNoSlot && ((msk[slot >> 5][threadIdx.x] >> (slot & 31)) & 1u);
+    uint32_t v = stored ? cb[size_t(slot) * n + i] : rvwg::kInvalid;
     if (v == rvwg::kInvalid && (!prover || (e & rvwg::kInjectedCol))) v = *p;
     if (prover && v == rvwg::kInvalid) v = 0u;
     *p = v;
@@ -206,11 +213,13 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
   T.minor_bits = minor_bits;
   T.off[0] = 0;
   size_t cwords = 0;
+  for (uint32_t k = 0; k < kMajors; k++) T.nslots[k] = rv32im_witgen_nslots(k);
   for (uint32_t b = 0; b < kBins; b++) {
     T.off[b + 1] = T.off[b] + cnt[b];
     T.cnt[b] = cnt[b];
     T.cbase[b] = cwords;
-    cwords += size_t(rv32im_witgen_nslots(b % kMajors)) * cnt[b];
+    const uint32_t ns = T.nslots[b % kMajors];
+    cwords += size_t(ns + (ns + 31) / 32) * cnt[b];  // the slots, then the lanes' mask words
   }
   R0_REQUIRE(T.off[kBins] == last_cycle, "rv32im witgen: bucket counts do not add up");
   size_t temp_bytes = 0;
@@ -222,9 +231,8 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
                                             end_bit, s));
   hipLaunchKernelGGL(bin_pos_kernel, dim3(g), dim3(kBucketThreads), 0, s, d_list, keys_out, last_cycle, T, pos);
   HIP_OK(hipGetLastError());
-  // the arms' compact values, INVALID until stored
+  // the arms' compact values (read only where a lane's mask says stored: no fill)
   auto* cbuf = static_cast<uint32_t*>(scratch(cwords * 4 + 16, kSlotRvwgCompact));
-  HIP_OK(hipMemsetD32Async(cbuf, 0xFFFFFFFFu, cwords, s));
   for (int p = 0; p < 2; p++) {
     KScope ks(p ? "rv32im_witgen_tables" : "rv32im_witgen_exec",
               double(T.off[(p + 1) * kMajors] - T.off[p * kMajors]) * (4.0 * 211 + sizeof(PreflightCycle)));
