@@ -1401,14 +1401,15 @@ def bigint_mul_add_nondet(tr, mode):
     return {wc: c[:16], wc + 4: c[16:], wc + 8: d}
 
 
-def ecall_trace(po2, seed=1, n_user=60, data_base=0x00100000, terminate=True, sha=True, bigint=False):
+def ecall_trace(po2, seed=1, n_user=60, data_base=0x00100000, terminate=True, sha=True, bigint=False, reps=1):
     """user code that traps into a machine-mode kernel twice through `ecall` (Poseidon2 buffer
     registers as byte addresses). The first entry
     runs a Poseidon2 ecall with state (is_elem 0, two blocks), one without state on field
     elements, a host write and an unaligned host read, then `mret`s back; the second entry
     terminates (or, terminate=False, `mret`s again and the program runs off its end). sha: the
     first entry also runs a two-block SHA-256 ecall. bigint: the first entry also runs a
-    BigInt ecall (bigint_mul_add_program, mode 0)."""
+    BigInt ecall (bigint_mul_add_program, mode 0). reps: the first entry runs its ecalls that
+    many times (a loop on s0), for traces whose ecall arms fill many wavefronts."""
     rng = np.random.default_rng(seed)
     user = random_program(rng, n_user, data_base) + [asm("ecall")] + random_program(rng, n_user, data_base)[1:] + \
         [asm("lui", 31, data_base >> 12), asm("ecall")] + random_program(rng, 20, data_base)[1:]
@@ -1438,6 +1439,8 @@ def ecall_trace(po2, seed=1, n_user=60, data_base=0x00100000, terminate=True, sh
         body += [asm("addi", 9, 5, 0), asm("addi", 5, 0, 0)] + li(10, B + BIGINT_BLOB) + li(6, B + BIGINT_NONDET) + \
             li(7, B + BIGINT_VERIFY) + li(28, B + BIGINT_CONSTS) + li(11, B + BIGINT_A) + li(12, B + BIGINT_B) + \
             li(13, B + BIGINT_C) + [asm("addi", 17, 0, 5), asm("ecall"), asm("addi", 5, 9, 0)]
+    if reps > 1:  # s0 counts the passes: body; s0 -= 1; bne s0, x0, body
+        body = li(8, reps) + body + [asm("addi", 8, 8, -1), asm("bne", 8, 0, -4 * (len(body) + 1))]
     body += [asm("mret")]
     second = [asm("addi", 17, 0, 0), asm("ecall")] if terminate else [asm("mret")]
     k += [asm("bge", 5, 6, 4 * (len(body) + 1))] + body + second
@@ -1462,5 +1465,6 @@ def ecall_trace(po2, seed=1, n_user=60, data_base=0x00100000, terminate=True, sh
     regs = {r: int(rng.integers(0, 1 << 32)) for r in range(1, 31)}
     mregs = {5: 0}
     return Trace(po2, user, data=data, regs=regs, seed=seed, kernel=k, machine_regs=mregs,
-                 read_record=[bytes(int(x) for x in rng.integers(0, 256, 23))], write_record=[0, 8, 0],
+                 read_record=[bytes(int(x) for x in rng.integers(0, 256, 23)) for _ in range(reps)],
+                 write_record=[0] + [8] * reps + [0],
                  bigint_nondet=bigint_mul_add_nondet if bigint else None)

@@ -56,6 +56,28 @@ def test_rv32im_witgen_ecalls_match_reference(hal, terminate, bigint):
             gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle, bigint=bi[:56])
 
 
+def test_rv32im_witgen_ecall_heavy_matches_reference(hal, oracle):
+    """30 passes of the machine-mode ecalls (Poseidon2, SHA-256, BigInt, host I/O) at po2=16:
+    the ecall arms fill many wavefronts per bin (SHA-256 4230 rows, Poseidon2 5881, BigInt
+    540), across the minor-ordered bins and their stored-slot masks. Data and global groups
+    equal the reference's; the proof from the trace equals the CPU path's and is valid."""
+    import risc0_amd as r
+    t = T.ecall_trace(16, seed=5, bigint=True, reps=30)
+    data, glob, cyc, tx = W.inputs(t)
+    bi = t.bigint_array()
+    ref_d, ref_g = W.run(data, glob, cyc, tx, t.table_split_cycle, 1 << 16, W.MODE_PARALLEL, bigint=bi)
+    d, g = gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle, bigint=bi)
+    bad = np.flatnonzero(d != ref_d)
+    assert bad.size == 0, f"{bad.size} words differ; first (col, row): {[(int(i) >> 16, int(i) & 0xFFFF) for i in bad[:8]]}"
+    assert np.array_equal(g, ref_g)
+    ref_seal, ref_mix, _, _, _ = W.prove_from_trace(t, oracle.POSEIDON2, oracle)
+    idx, off, val = W.injector_arrays(t)
+    seal, mix = r.prove_segment_trace(hal, 16, W.global_words(t), idx, off, val, cyc, tx, t.table_split_cycle,
+                                      bigint=bi, bigint_records=t.bigint_records())
+    assert np.array_equal(mix, ref_mix) and np.array_equal(seal, ref_seal)
+    assert r.verify_seal("rv32im", hal.suite, seal, check_validity=True) == 16
+
+
 def test_rv32im_witgen_modes(hal):
     """every mode runs the same schedule and gives the reference's forward-mode words"""
     t = T.random_trace(13, 500, seed=9)
