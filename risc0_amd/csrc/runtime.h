@@ -108,6 +108,7 @@ enum ScratchSlot : int {
   kSlotRvwgKeys = 83,
   kSlotRvwgSortTemp = 84,
   kSlotRvwgCompact = 85,
+  kSlotRvwgSlotTable = 86,
   // r0hip_prove_segment_trace (api.cpp): the injector's index, offsets and values
   kSlotRvInjIndex = 80,
   kSlotRvInjOffsets = 81,

@@ -242,14 +242,10 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
     }
   }
   {
-    static const int16_t* d_slot = [] {
-      // the slot table, uploaded once per process (it is constant)
-      const size_t bytes = size_t(kMajors) * kDataCols * sizeof(int16_t);
-      void* p = nullptr;
-      HIP_OK(hipMalloc(&p, bytes));
-      HIP_OK(hipMemcpy(p, rv32im_witgen_slot_table(), bytes, hipMemcpyHostToDevice));
-      return static_cast<const int16_t*>(p);
-    }();
+    // the slot table (constant, 5.5 KB) into this thread's scratch
+    const size_t slot_bytes = size_t(kMajors) * kDataCols * sizeof(int16_t);
+    auto* d_slot = static_cast<int16_t*>(scratch(slot_bytes, kSlotRvwgSlotTable));
+    upload_async(d_slot, rv32im_witgen_slot_table(), slot_bytes);
     KScope ks("rv32im_witgen_merge", double(rows) * kDataCols * 8.0 + double(cwords) * 4.0);
     hipLaunchKernelGGL(merge_kernel, dim3(uint32_t((rows + kMergeThreads - 1) / kMergeThreads)), dim3(kMergeThreads), 0,
                        s, data, uint32_t(rows), last_cycle, cbuf, keys, pos, d_slot, T, zeroize);
