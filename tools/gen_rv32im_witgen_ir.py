@@ -31,8 +31,10 @@ IR (one statement per line; buffers: data (col, back) and global (index)):
   mod ID A B | inr ID LO MID HI
   m ID                     phi register, 0 until assigned
   a ID SRC                 phi ID = SRC
-  if ID [major K] / else / end     branch on xID != 0; `major K` tags the arms of Top's
-                                   instruction mux (majorOnehot)
+  if ID [major K | minor M] / else / end
+                                   branch on xID != 0; `major K` tags the arms of Top's
+                                   instruction mux (majorOnehot), `minor M` those of an arm's
+                                   minor mux (minorOnehot)
   w COL ID                 data store at this cycle (checked set)
   gw IDX ID                global store (checked set)
   eqz ID K                 error unless xID == 0 (message K)
@@ -270,6 +272,7 @@ class Ev(A.Ev):
         x = self.x
         arms = []
         has_else = False
+        k0 = k
         while True:
             assert t[k] == "if" and t[k + 1] == "("
             sel, k = self.expr(t, k + 2, env)
@@ -288,6 +291,9 @@ class Ev(A.Ev):
                 k = self.skip_block(t, k + 2)
             break
         tag = self.fn_stack and self.fn_stack[-1] == "exec_Top" and len(arms) == 13
+        # an arm's minor mux (`if (to_size_t(....minorOnehot._super[0]._super))` ...): tagged so
+        # the kernel generator can specialise it as it does Top's major mux
+        minor = not tag and "minorOnehot" in t[k0:k0 + 12]
         outer = dict(env)
         start_pos = len(x.ir.ops)
         phis = {}     # name -> phi structure
@@ -296,7 +302,7 @@ class Ev(A.Ev):
         for ai, (sel, start) in enumerate(arms):
             if ai:
                 x.ir.emit("else")
-            x.ir.emit(*(("if", sel, "major", ai) if tag else ("if", sel)))
+            x.ir.emit(*(("if", sel, "major", ai) if tag else ("if", sel, "minor", ai) if minor else ("if", sel)))
             depth += 1
             x.push()
             arm_env = dict(outer)
