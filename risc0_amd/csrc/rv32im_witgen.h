@@ -85,11 +85,18 @@ __device__ __forceinline__ void fail(const Args& A, uint32_t code, uint32_t cycl
 // later values of a failed cycle are garbage here, but the call fails with that first error.
 struct Err {
   uint32_t code, detail;
+  bool pin;  // a per-kernel constant (see note)
 };
 __device__ __forceinline__ void note(Err& e, bool bad, uint32_t code, uint32_t detail = 0u) {
   const bool first = bad && e.code == 0u;
   e.code = first ? code : e.code;
   e.detail = first ? detail : e.detail;
+  // pin: both selects stay at this point. Unpinned, the scheduler sinks every `detail` select
+  // to the kernel's end (nothing reads it earlier) and keeps each check's 64-bit lane mask live
+  // until then: SGPR spills into VGPR lanes, 188 instead of 76 VGPRs for arm 4, 2.5 KB of
+  // scratch per lane for the SHA-256 arm. Pinned, the other arms lose their freedom to hoist
+  // loads and run slower (tools/gen_rv32im_witgen.py PIN_NOTES, profiles/r4s_*).
+  if (e.pin) asm volatile("" : "+v"(e.code), "+v"(e.detail));
 }
 
 // Buffer::get with checked = true. `view` is A.data, or for the injected columns a read-only
