@@ -108,6 +108,13 @@ __device__ __forceinline__ uint32_t ld(const Args& A, Err& err, const uint32_t* 
   return v;
 }
 
+// A load of an injected cell again, near a far use of its first (checked) load: the opaque row
+// keeps the compiler from merging the two, so the value need not stay live in between
+__device__ __forceinline__ uint32_t reld(const Args& A, const uint32_t* view, uint32_t col, uint32_t row) {
+  asm volatile("" : "+v"(row));
+  return view[uint64_t(col) * A.rows + row];
+}
+
 // The arm kernels keep this cycle's own row values in a compact, slot-major buffer of their
 // bin (cb[slot * n + i], lane i = the cycle's place in the bin's list: one coalesced store per
 // column for a wavefront), with a bit per slot in the lane's mask words sm0.. (stored after the
