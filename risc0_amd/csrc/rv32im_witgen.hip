@@ -112,12 +112,20 @@ __global__ __launch_bounds__(kBucketThreads) void bin_pos_kernel(const uint32_t*
 __global__ __launch_bounds__(kMergeThreads) void merge_kernel(uint32_t* data, uint32_t rows, uint32_t ncycles,
                                                              const uint32_t* cbuf, const uint8_t* keys,
                                                              const uint32_t* pos, const int16_t* slot_of, BinTable T,
-                                                             bool prover) {
+                                                             bool prover, bool xcd_tiles) {
   constexpr uint32_t kMaskWords = (rvwg::kDataCols + 31) / 32;
   __shared__ int16_t slot[rvwg::kMajors * rvwg::kDataCols];
   __shared__ uint32_t msk[kMaskWords][kMergeThreads];  // this thread's row: its arm's stored-slot bits
   for (uint32_t t = threadIdx.x; t < rvwg::kMajors * rvwg::kDataCols; t += kMergeThreads) slot[t] = slot_of[t];
-  const uint32_t r = blockIdx.x * kMergeThreads + threadIdx.x;
+  // xcd_tiles: consecutive workgroups go to the 8 XCDs in turn; renumbered, each XCD takes one
+  // contiguous run of rows, so the compact lines that neighbouring row tiles share stay in its L2
+  // (po2 20 loop guest: 0.71 -> 0.68 ms, profiles/r4v_witgen_merge_ab.txt)
+  uint32_t tile = blockIdx.x;
+  if (xcd_tiles) {
+    const uint32_t per = gridDim.x / 8, rem = gridDim.x % 8, x = blockIdx.x % 8, q = blockIdx.x / 8;
+    tile = x < rem ? x * (per + 1) + q : rem * (per + 1) + (x - rem) * per + q;
+  }
+  const uint32_t r = tile * kMergeThreads + threadIdx.x;
   const bool stepped = r < ncycles;
   const uint32_t b = stepped ? uint32_t(keys[r]) >> T.minor_bits : 0u;
   const uint32_t arm = b % rvwg::kMajors;
@@ -198,6 +206,10 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
     const char* e = std::getenv("R0_RVWG_MINOR");
     return e && e[0] == '0' ? 0u : 3u;
   }();
+  static const bool merge_xcd = [] {
+    const char* e = std::getenv("R0_RVWG_MERGE_XCD");
+    return !(e && e[0] == '0');
+  }();
   uint32_t h[4 + kBins];
   {
     KScope ks("rv32im_witgen_bucket", double(last_cycle) * 2 * sizeof(PreflightCycle));
@@ -248,7 +260,7 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
     upload_async(d_slot, rv32im_witgen_slot_table(), slot_bytes);
     KScope ks("rv32im_witgen_merge", double(rows) * kDataCols * 8.0 + double(cwords) * 4.0);
     hipLaunchKernelGGL(merge_kernel, dim3(uint32_t((rows + kMergeThreads - 1) / kMergeThreads)), dim3(kMergeThreads), 0,
-                       s, data, uint32_t(rows), last_cycle, cbuf, keys, pos, d_slot, T, zeroize);
+                       s, data, uint32_t(rows), last_cycle, cbuf, keys, pos, d_slot, T, zeroize, merge_xcd);
     HIP_OK(hipGetLastError());
   }
   uint32_t h_err[3] = {0, 0, 0};
