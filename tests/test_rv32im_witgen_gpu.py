@@ -116,6 +116,38 @@ def test_rv32im_witgen_failures(hal):
     assert np.array_equal(d, ref[0]) and np.array_equal(g, ref[1])
 
 
+@pytest.mark.parametrize("trace", ["random", "ecalls"])
+def test_rv32im_witgen_first_failure_matches_reference(hal, trace):
+    """one row of every instruction arm with its minor moved to the next one: the call fails
+    with the reference's message for its first failed check, word for word for an EQZ (its
+    zirgen source location and the cycle), in each arm kernel: the checks kept in program
+    order (arms 4 and 11) and the rest, and the arms that reload injected cells (10, 11)"""
+    import risc0_amd as r
+    t = T.random_trace(13, 400, seed=4) if trace == "random" else T.ecall_trace(14, seed=3, bigint=True)
+    data, glob, cyc, tx = W.inputs(t)
+    rows = 1 << (13 if trace == "random" else 14)
+    bi = t.bigint_array()
+    arms = 0
+    for arm in range(13):
+        cand = [i for i in range(t.table_split_cycle) if cyc["major"][i] == arm]
+        if not cand:
+            continue
+        row = cand[len(cand) // 2]
+        c2 = cyc.copy()
+        c2["minor"][row] = (int(c2["minor"][row]) + 1) % 8
+        with pytest.raises(RuntimeError) as ref:
+            W.run(data, glob, c2, tx, t.table_split_cycle, rows, bigint=bi)
+        with pytest.raises(r.R0HipError) as got:
+            gpu_witgen(hal, data, glob, c2, tx, t.table_split_cycle, bigint=bi)
+        want = str(ref.value)
+        if "eqz failure" in want:
+            assert want in str(got.value), (arm, want, str(got.value))
+        else:
+            assert want.split(":")[0] in str(got.value), (arm, want, str(got.value))
+        arms += 1
+    assert arms == (10 if trace == "random" else 13)
+
+
 @pytest.mark.parametrize("po2,n,suite,seed", [(13, 250, "poseidon2", 21), (14, 2500, "poseidon2", 3),
                                               (14, 2000, "sha-256", 8), (14, 0, "poseidon2", 4)])
 def test_prove_segment_trace_matches_oracle(po2, n, suite, seed, oracle):
