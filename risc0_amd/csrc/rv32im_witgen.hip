@@ -5,10 +5,12 @@
 //
 // stepExec runs step_Top (generated from steps.cpp, gen/rvwitgen/witgen_k*.hip) once per
 // cycle in two phases, as par_stepExec does: cycles [0, tableSplitCycle) first — their
-// lookupDelta calls count the u8/u16 lookup tables with device atomics — then the table and
-// done rows [tableSplitCycle, lastCycle), whose lookupCurrent reads those counts. Within a
-// phase the cycles are bucketed by their preflight major, and one kernel per instruction arm
-// runs step_Top specialised to that arm over its bucket: a wavefront's lanes share the arm.
+// lookupDelta calls count the u8/u16 lookup tables (summed per workgroup in LDS, flushed once
+// with device atomics) — then the table and done rows [tableSplitCycle, lastCycle), whose
+// lookupCurrent reads those counts. Within a phase the cycles are bucketed by their preflight
+// major (then minor), and one kernel per instruction arm runs step_Top specialised to that arm
+// over its bucket: a wavefront's lanes share the arm. The arms store into compact per-bin
+// buffers; merge_kernel writes the data group from them.
 // Every phase is a set of independent cycles: the rows a step reads at back > 0 are the
 // injected ones (cycle, next pc/state/mode, the Poseidon2/SHA/BigInt states), exactly what
 // makes the reference's parallel mode well defined. The reference's forward and reverse
@@ -17,8 +19,8 @@
 //
 // The preflight trace comes from the host, as RawPreflightTrace does (host pointers), or is
 // already resident (rv32im_witgen_dev). The cycles are bucketed on the device (counts, one
-// 27-word read-back for the launch sizes, fill). Checks that throw in the reference record an
-// error code and the cycle, raised after the kernels drain.
+// 27-word read-back for the launch sizes, a radix sort). Checks that throw in the reference
+// record the lane's first failure, raised after the kernels drain.
 #include <cstdlib>
 #include <string>
 #include <vector>
