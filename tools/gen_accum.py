@@ -563,6 +563,9 @@ def block(L, ind, items, extra, avail, defs, order, inv_batch, load_ahead, bools
     return set(avail) | {d for ins in pre for d in ([o for o, _ in ins[1]] if ins[0] == "ib" else defined(ins))}
 
 
+ACC_WAVES = {}
+
+
 def emit_sorted(nodes, defs, order, inv_batch, load_ahead, bools, tile=256):
     """One arm-sorted kernel over whole units (arm_chunks): each cycle's key is the first of
     the kernel's arm guards it satisfies; the 256 cycles of a workgroup are counting-sorted
@@ -757,6 +760,11 @@ def main():
     inv_batch = int(sys.argv[4]) if len(sys.argv) > 4 else 8
     load_ahead = int(sys.argv[5]) if len(sys.argv) > 5 else 64
     fuse = int(sys.argv[6]) if len(sys.argv) > 6 else 1
+    # R0_ACC_WAVES="3" (every kernel) or "0:3,2:3" (kernel:waves): an occupancy target per
+    # kernel (amdgpu_waves_per_eu); unset, the compiler picks the register budget
+    global ACC_WAVES
+    ACC_WAVES = {(-1 if ":" not in e else int(e.split(":")[0])): int(e.split(":")[-1])
+                 for e in os.environ.get("R0_ACC_WAVES", "").split(",") if e}
     pack = int(sys.argv[7]) if len(sys.argv) > 7 else 20000
     sort = int(sys.argv[8]) if len(sys.argv) > 8 else 256
     ns, names, prefix = CIRCUITS[circuit]
@@ -774,7 +782,9 @@ def main():
         launch[name] = []
         for L, own in emit_fn(name, fns[name], limit, k, inv_batch, load_ahead, pack, sort):
             wg = sort if own else 256
-            src = [HEAD, f"__global__ __launch_bounds__({wg}) void k{k}(AccArgs A) {{"]
+            wv = ACC_WAVES.get(k, ACC_WAVES.get(-1, 0))
+            occ = f" __attribute__((amdgpu_waves_per_eu({wv}, {wv})))" if wv else ""
+            src = [HEAD, f"__global__ __launch_bounds__({wg}){occ} void k{k}(AccArgs A) {{"]
             if not own:
                 src += ["  const uint32_t cycle = blockIdx.x * 256u + threadIdx.x;",
                         "  if (cycle >= A.steps) return;",
