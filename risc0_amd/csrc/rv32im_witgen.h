@@ -9,7 +9,7 @@
 namespace r0 {
 namespace rvwg {
 
-constexpr uint32_t kThreads = 128;
+constexpr uint32_t kThreads = 256;  // po2 20 loop guest: 0.78 -> 0.64 ms vs 128 (profiles/r4thr_witgen_threads_ab.txt)
 constexpr uint32_t kInvalid = 0xFFFFFFFFu;  // Fp::invalid()
 constexpr uint32_t kMajors = 13;            // Top's instruction mux (majorOnehot)
 constexpr uint32_t kDataCols = 211;         // the rv32im data group (REGCOUNT_DATA)
