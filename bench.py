@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
 """Benchmark: RISC-V cycles proved per second at segment po2=20 (BASELINE.json metric).
 
-A step proves one rv32im segment of 2^po2 cycles on one GPU: from the witness
-groups already resident in HBM (code 1 / data 211 / accum 103 columns, synthetic,
-seeded per segment) to the seal (Vec<u32>) on the host, through the whole STARK
-prover (commit code/data/accum, eval_check, DEEP-ALI, FRI, query openings).
+A step proves one rv32im segment of 2^po2 cycles on one GPU the way the reference's
+prove_core does (circuit/rv32im/src/prove/hal/mod.rs:143-224), from the segment's
+preflight trace: the trace (the datasheet's loop guest, restated preflight) starts in
+page-locked host memory, and the native segment pipeline (r0hip_prove_segments trace jobs)
+uploads it, generates the witness, accumulates and proves to the seal (Vec<u32>) on the
+host, with in_flight segments on the GPU and the next trace uploading, as r0vm's GPU worker
+queue runs segments. --witness times the prove core alone on a resident synthetic witness.
 Multi-GPU: one process per GPU, whole segments sharded per rank, no data-path
 collective (gloo only for the barriers, the max-time reduce and the host-side gather of
 seal digests). The ranks come from torch.distributed.run, or — when `--gpus N` is given
@@ -42,8 +45,19 @@ def parse():
     ap.add_argument("--witness", action="store_true",
                     help="rv32im: time the prove core on a resident synthetic witness instead of the default "
                          "trace -> witness generation -> accumulation -> seal unit")
+    ap.add_argument("--guest", default="loop_s", choices=["loop_s", "random_loop"],
+                    help="trace mode: loop_s = the datasheet's benchmark guest (risc0/zkvm/examples/loop.s under the "
+                         "v1compat kernel, datasheet.rs iteration counts); random_loop = a random 32-instruction "
+                         "RV32IM body repeated until the segment suspends")
+    ap.add_argument("--traces", type=int, default=None,
+                    help="trace mode: distinct preflight traces per rank, cycled over the timed segments "
+                         "(default 4 up to po2=22, 1 above)")
+    ap.add_argument("--resident-steps", type=int, default=None,
+                    help="trace mode: segments of the side leg that proves trace 0 from device memory "
+                         "(r0hip_prove_segment_trace_resident; the round-4 headline); default --steps, 0 = skip")
     ap.add_argument("--e2e-steps", type=int, default=6,
-                    help="segments of the end-to-end (pinned host witness -> H2D -> seal) leg; 0 = skip")
+                    help="segments of the witness end-to-end (pinned host witness groups -> H2D -> seal) leg; "
+                         "0 = skip")
     ap.add_argument("--accum-steps", type=int, default=8,
                     help="segments of the leg that runs the rv32im accumulation inside the prover on the "
                          "resident witness (r0hip_prove_segment_accum), as the reference's prove_core does; "
@@ -125,29 +139,48 @@ def main():
     # per-thread globals buffer: prove_segment zeroizes it in place; the witness
     # groups are only read and are shared
     globs = [dg] + [hal.copy_from_elem("global", glob) for _ in range(k - 1)]
-    trace_mode = args.circuit == "rv32im" and args.po2 <= 22 and not args.witness
+    trace_mode = args.circuit == "rv32im" and not args.witness
 
     def prove_witness(slot):
         return r.prove_segment(hal, args.circuit, args.po2, dc, dd, da, globs[slot], version=version)
 
     rt = trace = None
+    traces, tjobs = [], []
     if trace_mode:
         # the headline unit is the reference's prove_core (prove/hal/mod.rs:143-224): a
-        # preflight trace -> witness generation -> accumulation -> seal. The trace (a loop
-        # guest, restated preflight: tests/rv32im_trace.py) is built and uploaded once, before
-        # the timed region.
+        # preflight trace in host memory -> upload -> witness generation -> accumulation ->
+        # seal, through the native segment pipeline as r0vm's GPU worker runs it. Each rank
+        # builds --traces distinct traces (restated preflight: tests/rv32im_trace.py) into
+        # page-locked memory before the timed region, and the timed segments cycle through them.
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import rv32im_trace as T  # the input generator: a restated preflight (test infrastructure, no oracle)
+        ntr = args.traces if args.traces is not None else (4 if args.po2 <= 22 else 1)
         t0 = time.perf_counter()
-        trace = T.loop_trace(args.po2, body_len=32, seed=0x5249534330 + rank)
+        for i in range(max(1, ntr)):
+            seed = 0x5249534330 + 64 * rank + i
+            if args.guest == "loop_s":
+                # the datasheet's iteration count, shortened by a few iterations per trace so the
+                # traces differ in their rows as well as in their seeds
+                t_ = T.loop_s_trace(args.po2, T.loop_s_iterations(args.po2) - 37 * i, seed=seed)
+            else:
+                t_ = T.loop_trace(args.po2, body_len=32, seed=seed)
+            cyc, tx = t_.arrays()
+            idx, off, val = t_.injector_arrays()
+            tjobs.append(r.TraceJob(*(r.pinned_copy(a) for a in (t_.global_words(), idx, off, val, cyc, tx)),
+                                    t_.table_split_cycle, bigint=t_.bigint_array(),
+                                    bigint_records=t_.bigint_records()))
+            traces.append(t_)
+        trace = traces[0]
         cyc, tx = trace.arrays()
         idx, off, val = trace.injector_arrays()
         bi = trace.bigint_array()
         rt = r.ResidentTrace(hal, args.po2, trace.global_words(), idx, off, val, cyc, tx, trace.table_split_cycle,
                              bigint=bi if len(bi) else None)
         bigint_records = trace.bigint_records() or None
-        print(f"rank {rank}: trace built in {time.perf_counter() - t0:.1f} s ({trace.table_split_cycle} rows before "
-              f"the tables, {len(tx)} memory transactions)", file=sys.stderr)
+        del cyc, tx, idx, off, val
+        print(f"rank {rank}: {len(traces)} {args.guest} traces built in {time.perf_counter() - t0:.1f} s (trace 0: "
+              f"{trace.table_split_cycle} rows before the tables, {len(trace.arrays()[1])} memory transactions, "
+              f"{tjobs[0].h2d_bytes() / 1e6:.0f} MB to upload)", file=sys.stderr)
 
     def timed_leg(prove_one, label):
         phase_tot, last = {}, {}
@@ -180,9 +213,29 @@ def main():
             print(json.dumps({label + "_phases_ms": phases, "seal_words": int(last["seal"].size)}), file=sys.stderr)
         return t, last["seal"], last["mix"]
 
+    resident = None
     if trace_mode:
-        t, seal, mix = timed_leg(lambda slot: r.prove_segment_trace_resident(hal, rt, bigint_records=bigint_records),
-                                 "trace")
+        batch = [tjobs[i % len(tjobs)] for i in range(args.steps)]
+        out = {}
+
+        def pipeline(jobs_):
+            out["res"] = r.prove_trace_segments(hal, args.po2, jobs_, in_flight=k)
+        pipeline([tjobs[i % len(tjobs)] for i in range(max(args.warmup, k + 1))])  # warm every set, thread, pool
+        _t, t = timed_segments(pipeline, [batch], 0, hal.synchronize, dist)
+        seal, mix = out["res"][0]  # job 0 proved trace 0
+        seals_distinct = len({sl.tobytes() for sl, _ in out["res"]})
+        t0 = time.perf_counter()
+        pipeline([tjobs[0]])
+        t_one = time.perf_counter() - t0
+        rsteps = args.steps if args.resident_steps is None else args.resident_steps
+        if rsteps > 0:
+            t_r, seal_r, _ = timed_leg(lambda slot: r.prove_segment_trace_resident(hal, rt, bigint_records=bigint_records),
+                                       "resident_trace")
+            assert np.array_equal(seal_r, seal), "the resident trace's seal differs from the pipeline's"
+            resident = {"value": round(world * args.steps * (1 << args.po2) / t_r, 1), "unit": "cycles/s",
+                        "ms_per_step": round(1000.0 * t_r / args.steps, 3), "segments_in_flight_per_gpu": k,
+                        "note": "trace 0 resident in HBM before the timed region (r0hip_prove_segment_trace_resident "
+                                "from k host threads): the round-4 headline, no H2D"}
         if not args.no_prove_only:
             t_w, seal_w, _ = timed_leg(prove_witness, "prove_only")
     else:
@@ -208,7 +261,6 @@ def main():
     roofline = None
     cpu = None
     e2e = None
-    e2e_trace = None
     acc_leg = None
     if rank == 0:
         prove_timed = ((lambda: r.prove_segment_trace_resident(hal, rt, bigint_records=bigint_records)) if trace_mode
@@ -219,8 +271,6 @@ def main():
         kl = k if args.inflight is not None else min(k, 2)
         if args.e2e_steps > 0 and host_witness is not None:
             e2e = end_to_end(r, hal, args, host_witness, kl, version)
-        if args.e2e_steps > 0 and trace_mode:
-            e2e_trace = end_to_end_trace(r, hal, args, trace, k)
         if args.accum_steps > 0 and args.circuit == "rv32im" and host_witness is not None:
             acc_leg = with_accumulation(r, hal, args, host_witness, kl, version)
         if not args.no_cpu_baseline and world == 1:
@@ -228,13 +278,22 @@ def main():
     del host_witness
 
     if rank == 0:
-        workload = (f"{args.circuit} segment po2={args.po2}, {args.hashfn} hashfn, preflight trace resident in HBM "
-                    "-> witness generation -> accumulation -> seal on host (the reference's prove_core)"
+        workload = (f"{args.circuit} segment po2={args.po2}, {args.hashfn} hashfn, from its preflight trace in page-locked "
+                    "host memory: upload -> witness generation -> accumulation -> seal on host (the reference's "
+                    "prove_core), through the native segment pipeline (r0hip_prove_segments trace jobs)"
                     if trace_mode else
                     f"{args.circuit} segment po2={args.po2}, {args.hashfn} hashfn, witness resident in HBM -> seal on host")
-        data = ("synthetic (a loop guest: random 32-instruction RV32IM body, repeated until the segment suspends; "
-                "preflight restated from the reference executor, tests/rv32im_trace.py; seeded per rank)"
-                if trace_mode else "synthetic (uniform BabyBear witness, seeded per segment)")
+        if trace_mode and args.guest == "loop_s":
+            data = (f"synthetic: the datasheet's loop guest (risc0/zkvm/examples/loop.s under a restated v1compat kernel; "
+                    f"{T.loop_s_iterations(args.po2)} iterations less 37 per trace, datasheet.rs:42-58), preflight restated "
+                    f"from the reference executor (tests/rv32im_trace.py); {len(traces)} distinct seeded traces per rank, "
+                    "cycled over the segments")
+        elif trace_mode:
+            data = (f"synthetic (a loop guest: random 32-instruction RV32IM body, repeated until the segment suspends; "
+                    f"preflight restated from the reference executor, tests/rv32im_trace.py; {len(traces)} distinct "
+                    "seeded traces per rank)")
+        else:
+            data = "synthetic (uniform BabyBear witness, seeded per segment)"
         line = {
             "metric": f"RISC-V cycles proved/sec at segment po2={args.po2}",
             "value": round(value, 1),
@@ -253,6 +312,10 @@ def main():
                        "segments_per_gpu": args.steps, "segments_in_flight_per_gpu": k,
                        "parallelism": f"segment-per-gpu x{world}",
                        "seal_sha256_by_rank": [digests[i] for i in range(world)],
+                       **({"guest": args.guest, "distinct_traces_per_rank": len(traces),
+                           "distinct_seals_rank0": seals_distinct,
+                           "h2d_bytes_per_segment": int(tjobs[0].h2d_bytes()),
+                           "ms_one_segment_unpipelined": round(1000.0 * t_one, 1)} if trace_mode else {}),
                        "ranks_share_devices": any(shared[i] for i in range(world))},
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -263,8 +326,8 @@ def main():
             line["prove_only"] = prove_only
         if e2e:
             line["end_to_end"] = e2e
-        if e2e_trace:
-            line["end_to_end_from_trace"] = e2e_trace
+        if resident:
+            line["resident_trace"] = resident
         if acc_leg:
             line["with_accumulation"] = acc_leg
         print(json.dumps(line))
@@ -484,67 +547,6 @@ def end_to_end(r, hal, args, witness, k, version):
             **({"with_device_accumulation": dev_acc} if dev_acc else {})}
 
 
-def end_to_end_trace(r, hal, args, trace, k):
-    """PCIe-inclusive form of the headline: each segment's preflight trace (cycles, memory
-    transactions, injector, global vector; 0.17 GB at po2=20 against 1.32 GB of witness groups)
-    starts in host memory and k threads each call r0hip_prove_segment_trace, which stages it
-    through the thread's pinned arena onto its own stream while the other threads' proofs run.
-    Reported beside `value`, never as it."""
-    import ctypes
-    lib = r.lib()
-    hosts = []
-
-    def pinned(a):
-        """a copy of `a` in page-locked memory (r0hip_host_alloc), as a producer would hand the
-        trace over: the library then copies it to the device directly, without staging"""
-        a = np.ascontiguousarray(a)
-        p = ctypes.c_void_p()
-        r.check(lib.r0hip_host_alloc(ctypes.byref(p), max(1, a.nbytes)))
-        hosts.append(p.value)
-        v = np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(ctypes.c_uint8)), shape=(a.nbytes,)).view(a.dtype)
-        v[:] = a.reshape(-1)
-        return v.reshape(a.shape)
-    cyc, tx = (pinned(a) for a in trace.arrays())
-    idx, off, val = (pinned(a) for a in trace.injector_arrays())
-    glob = trace.global_words()
-    bi = trace.bigint_array()
-    bi = bi if len(bi) else None
-    recs = trace.bigint_records() or None
-    h2d = sum(a.nbytes for a in (cyc, tx, idx, off, val, glob)) + (0 if bi is None else bi.nbytes)
-
-    def one():
-        r.prove_segment_trace(hal, args.po2, glob, idx, off, val, cyc, tx, trace.table_split_cycle, bigint=bi,
-                              bigint_records=recs)
-
-    def run(n):
-        share = [n // k + (1 if i < n % k else 0) for i in range(k)]
-        ts = [threading.Thread(target=lambda c=c: [one() for _ in range(c)]) for c in share if c]
-        for t_ in ts:
-            t_.start()
-        for t_ in ts:
-            t_.join()
-
-    try:
-        run(k)  # warm every thread's stream, arena and pool
-        one()  # and this thread's
-        t0 = time.perf_counter()
-        one()
-        t_one = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        run(args.e2e_steps)
-        t = time.perf_counter() - t0
-    finally:
-        for hp in hosts:
-            r.check(lib.r0hip_host_free(hp))
-    return {"value": round(args.e2e_steps * (1 << args.po2) / t, 1), "unit": "cycles/s",
-            "ms_per_step": round(1000.0 * t / args.e2e_steps, 3), "steps": args.e2e_steps,
-            "segments_in_flight_per_gpu": k, "h2d_bytes_per_segment": int(h2d),
-            "ms_one_segment_unpipelined": round(1000.0 * t_one, 1),
-            "note": "the headline's prove_core from a preflight trace, with the trace in page-locked host memory "
-                    "(r0hip_host_alloc) copied to the device by r0hip_prove_segment_trace on each prover thread's "
-                    "stream"}
-
-
 def pmc_traffic(family, calls, args):
     """HBM bytes per launch of `family` from the newest committed rocprofv3 PMC summary
     (profiles/r*_pmc_traffic.json, FETCH_SIZE/WRITE_SIZE passes of this same bench
@@ -604,6 +606,11 @@ def cpu_baseline_trace(args, trace, gpu_seal, gpu_mix):
         import rv32im_witgen_ref as W
         if oracle.ref_lib() is None or not RA.available():
             return None
+        compare = trace.po2 <= 20
+        if not compare:  # a po2 > 20 segment would take the CPU path most of an hour: time the po2=20 guest
+            import rv32im_trace as T
+            trace = T.loop_s_trace(20, seed=0x5249534330) if args.guest == "loop_s" else \
+                T.loop_trace(20, body_len=32, seed=0x5249534330)
         import hashlib
         suite = {"poseidon2": oracle.POSEIDON2, "sha-256": oracle.SHA256, "poseidon_254": oracle.POSEIDON254}[args.hashfn]
         rows = 1 << trace.po2
@@ -640,10 +647,12 @@ def cpu_baseline_trace(args, trace, gpu_seal, gpu_mix):
                           f"{t:.1f} s wall: the reference's compiled witgen and accumulation (oracle/_ref) and the "
                           "oracle prover with the reference's compiled poly_fp",
                 "seconds_by_hal_op": ops,
-                "seal_equal": bool(np.array_equal(cseal, gpu_seal)), "mix_equal": bool(np.array_equal(cmix, gpu_mix)),
+                "seal_equal": bool(np.array_equal(cseal, gpu_seal)) if compare else None,
+                "mix_equal": bool(np.array_equal(cmix, gpu_mix)) if compare else None,
                 "oracle_seal_sha256": dig(cseal), "gpu_seal_sha256": dig(gpu_seal),
                 "oracle_mix_sha256": dig(cmix), "gpu_mix_sha256": dig(gpu_mix),
-                "parity_note": "CPU prove_core of rank 0's own trace against the last timed GPU seal of that trace"}
+                "parity_note": ("CPU prove_core of rank 0's trace 0 against the GPU seal the timed pipeline proved from "
+                                "that trace" if compare else "po2=20 sample; no parity at the bench's size")}
     except Exception as e:  # the baseline is reported, never required
         print(f"cpu baseline failed: {e}", file=sys.stderr)
         return None

@@ -292,15 +292,35 @@ const char* r0hip_prove_recursion(int suite, uint32_t po2, const uint32_t* d_ctr
 
 /* ---- segment pipeline (r0vm's per-GPU worker queue, r0vm/src/actors/worker.rs:75-76, over the
  * zkvm's per-segment prove loop, zkvm/src/host/server/prove/prover_impl.rs:84-94) ----
- * Proves njobs segments of one (circuit, suite, po2) from HOST witness buffers: an uploader
- * thread copies each job's groups, in 48-column chunks, into one of in_flight+1 device buffer
- * sets while in_flight prover threads run r0hip_prove_segment's core on their own streams; a
- * prover starts a job at once and commits each group chunk by chunk as it lands (Poseidon2
- * and SHA-256; Poseidon254 waits for whole groups). Seals equal r0hip_prove_segment's. Host
- * buffers must stay valid until the call returns and should be page-locked
- * (r0hip_host_alloc) for full PCIe rate. Per job: seal into
- * h_seal (seal_cap words), its length in seal_len, mix values into h_mix_out (optional),
- * and error = NULL or a malloc'd message (free() it). Returns NULL when every job succeeded. */
+ * Proves njobs segments of one (circuit, suite, po2) from HOST inputs: an uploader thread copies
+ * each job's inputs into one of in_flight+1 device buffer sets while in_flight prover threads
+ * prove on their own streams. Host buffers must stay valid until the call returns and should be
+ * page-locked (r0hip_host_alloc) for full PCIe rate. Per job: seal into h_seal (seal_cap words),
+ * its length in seal_len, mix values into h_mix_out (optional), and error = NULL or a malloc'd
+ * message (free() it). Returns NULL when every job succeeded.
+ * Two job forms, one per call (all jobs of a call take the same form):
+ *  - witness jobs (trace == NULL): the witness groups, copied in 48-column chunks; a prover
+ *    starts a job at once and commits each group chunk by chunk as it lands (Poseidon2 and
+ *    SHA-256; Poseidon254 waits for whole groups). Seals equal r0hip_prove_segment's.
+ *  - trace jobs (trace != NULL, rv32im only, write_version = 1 and version = 2): the job is
+ *    SegmentProverImpl::prove_core from a preflight trace (circuit/rv32im/src/prove/hal/mod.rs:
+ *    143-224), the unit r0vm's GPU worker runs from the executor's segments
+ *    (r0vm/src/actors/worker.rs:186-260, job/proof.rs:238-323), with the CUDA prove_core's trace
+ *    upload (circuit/rv32im/src/prove/witgen/mod.rs:135-176) done by the uploader: the trace, the
+ *    injector and the global vector go into one of in_flight+1 device trace sets while the
+ *    provers run witness generation, accumulation and the proof from the others. The injector is
+ *    checked on the host as r0hip_prove_segment_trace checks it. h_bigint/n_bigint are the
+ *    trace's BigInt backs; h_code/h_data/h_accum/h_global are unused. Seals equal
+ *    r0hip_prove_segment_trace's. */
+typedef struct r0hip_trace_input {
+  uint32_t mode;                      /* as r0hip_rv32im_witgen */
+  const uint32_t* h_global;           /* build_global_vec's 90 Montgomery words */
+  const uint32_t* h_inj_index;        /* inj_rows + 1 entries */
+  size_t inj_rows;
+  const uint32_t* h_inj_offsets;      /* h_inj_index[inj_rows] entries each */
+  const uint32_t* h_inj_values;
+  r0hip_raw_preflight_trace preflight; /* host pointers; 2^po2 cycle records */
+} r0hip_trace_input;
 typedef struct r0hip_segment_job {
   const uint32_t* h_code;
   const uint32_t* h_data;
@@ -314,6 +334,7 @@ typedef struct r0hip_segment_job {
   size_t seal_len;
   uint32_t* h_mix_out;
   const char* error;
+  const r0hip_trace_input* trace;    /* non-NULL: a trace job (see above) */
 } r0hip_segment_job;
 const char* r0hip_prove_segments(const char* circuit, int suite, uint32_t po2, int write_version, uint32_t version,
                                  r0hip_segment_job* jobs, size_t njobs, uint32_t in_flight);

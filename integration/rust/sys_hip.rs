@@ -35,7 +35,21 @@ pub struct R0HipBigIntBack {
     pub bytes: [u8; 16],
 }
 
-/// One job of r0hip_prove_segments (host witness in, seal out).
+/// A preflight trace as a trace job of r0hip_prove_segments takes it (struct r0hip_trace_input):
+/// host pointers; `preflight` has the repr(C) layout of risc0_circuit_rv32im_sys::RawPreflightTrace.
+#[repr(C)]
+pub struct R0HipTraceInput {
+    pub mode: u32,
+    pub h_global: *const u32,
+    pub h_inj_index: *const u32,
+    pub inj_rows: usize,
+    pub h_inj_offsets: *const u32,
+    pub h_inj_values: *const u32,
+    pub preflight: risc0_circuit_rv32im_sys::RawPreflightTrace,
+}
+
+/// One job of r0hip_prove_segments: host witness groups in (trace NULL), or a preflight trace
+/// (trace non-NULL, rv32im prove_core); seal out.
 #[repr(C)]
 pub struct R0HipSegmentJob {
     pub h_code: *const u32,
@@ -49,6 +63,7 @@ pub struct R0HipSegmentJob {
     pub seal_len: usize,
     pub h_mix_out: *mut u32,
     pub error: *const c_char,
+    pub trace: *const R0HipTraceInput,
 }
 
 #[link(name = "r0hip")]

@@ -8,6 +8,7 @@
 #include <cstdlib>
 #include <algorithm>
 #include <cstring>
+#include <functional>
 #include <stdexcept>
 #include <vector>
 
@@ -293,6 +294,10 @@ const char* r0hip_rv32im_witgen(uint32_t mode, const r0hip_raw_exec_buffers* buf
                    buffers->global.rows == 1,
                "r0hip_rv32im_witgen: buffers are not the rv32im data group and global vector");
     R0_REQUIRE(cycles == buffers->data.rows, "r0hip_rv32im_witgen: cycles must equal the data group's rows");
+    // the reference's witness generator takes Buffer<checked = true> (witgen/mod.rs:150) and
+    // these kernels always run the checked stores and reads
+    R0_REQUIRE(buffers->data.checked && buffers->global.checked,
+               "r0hip_rv32im_witgen: unchecked buffers are not supported (the reference passes checked = true)");
     stage_reset();
     rv32im_witgen(stream(), mode, buffers->data.buf, buffers->global.buf, buffers->data.rows,
                   static_cast<const rvwg::PreflightCycle*>(preflight->cycles),
@@ -303,18 +308,23 @@ const char* r0hip_rv32im_witgen(uint32_t mode, const r0hip_raw_exec_buffers* buf
 
 }  // extern "C"
 
-namespace {
+namespace r0 {
+
+void check_injector(const uint32_t* index, size_t rows, const uint32_t* offsets, const uint32_t* values,
+                    size_t limit);
 
 // SegmentProverImpl::prove_core from a preflight (circuit/rv32im/src/prove/hal/mod.rs:143-224):
 // WitnessGenerator::hal_generate_witness (witgen/mod.rs:135-176: globals, code and data
 // INVALID, the injector scattered into data, stepExec, zeroize), then the prove core with the
 // version word 2 and WitnessGenerator::accum on the device. `resident`: the global vector,
 // the injector and the preflight arrays are device pointers; otherwise host pointers.
+// inputs_ready (resident only): called with the stream after the INVALID fills and before the
+// first read of the inputs (the segment pipeline makes the stream wait for their upload there).
 std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const uint32_t* global_in,
                                   const uint32_t* inj_index, size_t inj_rows, const uint32_t* inj_offsets,
                                   const uint32_t* inj_values, const r0hip_raw_preflight_trace* pf,
                                   const r0hip_bigint_back* h_bigint, size_t n_bigint, bool resident,
-                                  std::vector<uint32_t>* mix) {
+                                  std::vector<uint32_t>* mix, const std::function<void(hipStream_t)>& inputs_ready) {
   const CircuitDef* c = find_circuit("rv32im");
   R0_REQUIRE(global_in && inj_index && pf && pf->cycles, "r0hip_prove_segment_trace: null argument");
   R0_REQUIRE(po2 >= 2 && po2 <= 24, "r0hip_prove_segment_trace: po2 out of range");
@@ -329,6 +339,7 @@ std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const 
   HIP_OK(hipMemsetD32Async(code.p, 0u, code.words, s));  // INVALID, zeroized: nothing writes code
   HIP_OK(hipMemsetD32Async(data.p, 0xFFFFFFFFu, data.words, s));
   if (resident) {
+    if (inputs_ready) inputs_ready(s);
     HIP_OK(hipMemcpyAsync(global.p, global_in, global.words * 4, hipMemcpyDeviceToDevice, s));
     scatter(s, data.p, inj_index, inj_offsets, inj_values, inj_rows, data.words);
     Span w("witgen");
@@ -336,10 +347,8 @@ std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const 
                       static_cast<const rvwg::MemoryTxn*>(pf->txns), pf->txns_len, pf->bigint_bytes,
                       pf->bigint_bytes_len, pf->table_split_cycle, uint32_t(n), true);
   } else {
+    check_injector(inj_index, inj_rows, inj_offsets, inj_values, data_cols * n);
     const size_t n_inj = inj_index[inj_rows];
-    R0_REQUIRE(n_inj == 0 || (inj_offsets && inj_values), "r0hip_prove_segment_trace: null injector arrays");
-    for (size_t i = 0; i < n_inj; i++)
-      R0_REQUIRE(inj_offsets[i] < data_cols * n, "r0hip_prove_segment_trace: injector offset outside the data group");
     upload_async(global.p, global_in, global.words * 4);
     if (n_inj) {
       auto* idx = static_cast<uint32_t*>(scratch((inj_rows + 1) * 4, kSlotRvInjIndex));
@@ -360,6 +369,24 @@ std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const 
   const AccumStep acc{accum.p, n, false, h_bigint, n_bigint};
   return prove_segment(*c, suite, po2, code.p, data.p, nullptr, global.p, true, 2, mix, nullptr, &acc);
 }
+
+// The host injector (Injector, witgen/mod.rs:329-378) before it is uploaded: a CSR index that
+// never decreases (entries of row c are [index[c], index[c + 1])) and offsets inside the data
+// group. O(rows + entries); the resident path's scatter bounds its reads and writes instead.
+void check_injector(const uint32_t* index, size_t rows, const uint32_t* offsets, const uint32_t* values,
+                    size_t limit) {
+  for (size_t c = 0; c < rows; c++)
+    R0_REQUIRE(index[c] <= index[c + 1], "r0hip_prove_segment_trace: injector index decreases at row " +
+                                             std::to_string(c));
+  const size_t n_inj = index[rows];
+  R0_REQUIRE(n_inj == 0 || (offsets && values), "r0hip_prove_segment_trace: null injector arrays");
+  for (size_t i = 0; i < n_inj; i++)
+    R0_REQUIRE(offsets[i] < limit, "r0hip_prove_segment_trace: injector offset outside the data group");
+}
+
+}  // namespace r0
+
+namespace {
 
 void seal_out(const std::vector<uint32_t>& seal, const std::vector<uint32_t>& mix, uint32_t* h_seal, size_t seal_cap,
               size_t* seal_len, uint32_t* h_mix_out) {
@@ -383,7 +410,7 @@ const char* r0hip_prove_segment_trace(int suite, uint32_t po2, uint32_t mode, co
   return wrap([&] {
     std::vector<uint32_t> mix;
     auto seal = prove_trace(suite, po2, mode, h_global, h_inj_index, inj_rows, h_inj_offsets, h_inj_values, preflight,
-                            h_bigint, n_bigint, false, &mix);
+                            h_bigint, n_bigint, false, &mix, {});
     seal_out(seal, mix, h_seal, seal_cap, seal_len, h_mix_out);
   });
 }
@@ -397,7 +424,7 @@ const char* r0hip_prove_segment_trace_resident(int suite, uint32_t po2, uint32_t
   return wrap([&] {
     std::vector<uint32_t> mix;
     auto seal = prove_trace(suite, po2, mode, d_global, d_inj_index, inj_rows, d_inj_offsets, d_inj_values,
-                            d_preflight, h_bigint, n_bigint, true, &mix);
+                            d_preflight, h_bigint, n_bigint, true, &mix, {});
     seal_out(seal, mix, h_seal, seal_cap, seal_len, h_mix_out);
   });
 }

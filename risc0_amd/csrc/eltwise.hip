@@ -77,13 +77,15 @@ __global__ void gather_kernel(uint32_t* dst, const uint32_t* src, uint64_t idx, 
   if (g < size) dst[g] = src[g * stride + idx];
 }
 // cpu.rs:598-615: one lane per cycle walks its CSR slice
-// offsets at or past `limit` (the buffer's words) are skipped: a resident injector the host
-// has not checked cannot write outside the buffer
+// offsets at or past `limit` (the buffer's words) are skipped, and no row reads entries past
+// index[cycles] (the arrays' length): a resident injector the host has not checked can neither
+// write outside the buffer nor read past its own arrays
 __global__ void scatter_kernel(uint32_t* into, const uint32_t* index, const uint32_t* offsets,
                                const uint32_t* values, uint64_t cycles, uint64_t limit) {
   uint64_t c = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (c >= cycles) return;
-  for (uint32_t i = index[c]; i < index[c + 1]; i++)
+  const uint32_t end = min(index[c + 1], index[cycles]);
+  for (uint32_t i = index[c]; i < end; i++)
     if (offsets[i] < limit) into[offsets[i]] = values[i];
 }
 // cpu.rs:617-635

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <algorithm>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -32,6 +33,14 @@ std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2
                                     const uint32_t* data, const uint32_t* accum, uint32_t* global,
                                     bool write_version, uint32_t version, std::vector<uint32_t>* mix_out,
                                     const UploadGate* uploads, const AccumStep* acc = nullptr);
+// api.cpp: rv32im prove_core from a preflight trace, and the host check of an injector
+std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const uint32_t* global_in,
+                                  const uint32_t* inj_index, size_t inj_rows, const uint32_t* inj_offsets,
+                                  const uint32_t* inj_values, const r0hip_raw_preflight_trace* pf,
+                                  const r0hip_bigint_back* h_bigint, size_t n_bigint, bool resident,
+                                  std::vector<uint32_t>* mix, const std::function<void(hipStream_t)>& inputs_ready);
+void check_injector(const uint32_t* index, size_t rows, const uint32_t* offsets, const uint32_t* values,
+                    size_t limit);
 
 namespace {
 
@@ -108,6 +117,161 @@ char* dup_msg(const char* m) {
   return p;
 }
 
+// A device trace set: one job's preflight trace, injector and global vector, and the event
+// that marks their upload on the uploader's stream. `landed`: the uploader has queued every
+// copy and recorded the event, or failed (the job then carries the error).
+struct TraceSet {
+  DevBuf glob, index, offsets, values, cycles, txns, bigint;
+  hipEvent_t ev = nullptr;
+  size_t job = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  bool landed = false;
+  void mark() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      landed = true;
+    }
+    cv.notify_all();
+  }
+  void wait_landed() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return landed; });
+  }
+};
+
+// Trace jobs: the uploader copies job i's trace into a free trace set and hands the set to a
+// prover at once; the prover allocates and INVALID-fills its witness groups, then its stream
+// waits for the set's event before the scatter (prove_trace's inputs_ready), so the copies of
+// one segment overlap the proofs of the others. k + 1 sets, sized once for the largest job.
+const char* prove_trace_jobs(int suite, uint32_t po2, r0hip_segment_job* jobs, size_t njobs, size_t k) {
+  constexpr size_t kCycleWords = 9, kTxnWords = 5, kGlobalWords = 90;  // RawPreflightCycle 36 B, txn 20 B
+  const size_t n = size_t(1) << po2;
+  const size_t data_words = size_t(211) * n;
+  size_t cap_inj = 1, cap_txn = 1, cap_big = 4;
+  for (size_t i = 0; i < njobs; i++) {
+    const r0hip_trace_input* t = jobs[i].trace;
+    R0_REQUIRE(t, "r0hip_prove_segments: a call mixes trace jobs and witness jobs");
+    if (t->h_inj_index && t->inj_rows <= n) cap_inj = std::max<size_t>(cap_inj, t->h_inj_index[t->inj_rows]);
+    cap_txn = std::max<size_t>(cap_txn, t->preflight.txns_len);
+    cap_big = std::max<size_t>(cap_big, t->preflight.bigint_bytes_len);
+  }
+  std::vector<TraceSet> sets(k + 1);
+  struct Events {
+    std::vector<TraceSet>& sets;
+    ~Events() {
+      for (auto& s : sets)
+        if (s.ev) (void)hipEventDestroy(s.ev);
+    }
+  } events{sets};
+  for (auto& s : sets) {
+    s.glob = DevBuf(kGlobalWords);
+    s.index = DevBuf(n + 1);
+    s.offsets = DevBuf(cap_inj);
+    s.values = DevBuf(cap_inj);
+    s.cycles = DevBuf(n * kCycleWords);
+    s.txns = DevBuf(cap_txn * kTxnWords);
+    s.bigint = DevBuf((cap_big + 3) / 4);
+    HIP_OK(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+  }
+  HIP_OK(hipDeviceSynchronize());  // allocations complete before other streams use them
+  Queue free_q, ready_q;
+  for (size_t s = 0; s < sets.size(); s++) free_q.put(long(s));
+
+  std::thread uploader([&] {
+    for (size_t i = 0; i < njobs; i++) {
+      long s = free_q.get();
+      TraceSet& b = sets[s];
+      {
+        std::lock_guard<std::mutex> lk(b.mu);
+        b.job = i;
+        b.landed = false;
+      }
+      ready_q.put(s);  // the prover fills its groups while the trace uploads
+      try {
+        ensure_init();
+        const r0hip_trace_input& t = *jobs[i].trace;
+        const r0hip_raw_preflight_trace& pf = t.preflight;
+        R0_REQUIRE(t.h_global && t.h_inj_index && pf.cycles, "trace job: null argument");
+        R0_REQUIRE(t.inj_rows <= n, "trace job: injector longer than the segment");
+        R0_REQUIRE((pf.txns_len == 0 || pf.txns) && (pf.bigint_bytes_len == 0 || pf.bigint_bytes),
+                   "trace job: null trace array with a nonzero count");
+        R0_REQUIRE(jobs[i].n_bigint == 0 || jobs[i].h_bigint, "trace job: h_bigint is NULL with n_bigint > 0");
+        check_injector(t.h_inj_index, t.inj_rows, t.h_inj_offsets, t.h_inj_values, data_words);
+        const size_t n_inj = t.h_inj_index[t.inj_rows];
+        stage_reset();  // the previous job's staged copies have landed: the arena is free
+        upload_async(b.glob.p, t.h_global, kGlobalWords * 4);
+        upload_async(b.index.p, t.h_inj_index, (t.inj_rows + 1) * 4);
+        upload_async(b.offsets.p, t.h_inj_offsets, n_inj * 4);
+        upload_async(b.values.p, t.h_inj_values, n_inj * 4);
+        upload_async(b.cycles.p, pf.cycles, n * kCycleWords * 4);
+        upload_async(b.txns.p, pf.txns, size_t(pf.txns_len) * kTxnWords * 4);
+        upload_async(b.bigint.p, pf.bigint_bytes, pf.bigint_bytes_len);
+        HIP_OK(hipEventRecord(b.ev, stream()));
+      } catch (const std::exception& e) {
+        {
+          std::lock_guard<std::mutex> lk(b.mu);
+          if (!jobs[i].error) jobs[i].error = dup_msg(e.what());
+        }
+        drain_after_error();
+      }
+      b.mark();
+    }
+    // every copy done before the call returns: the caller may free its host buffers then
+    drain_after_error();
+    for (size_t t = 0; t < k; t++) ready_q.put(-1);
+  });
+
+  std::vector<std::thread> provers;
+  for (size_t t = 0; t < k; t++) {
+    provers.emplace_back([&] {
+      for (;;) {
+        long s = ready_q.get();
+        if (s < 0) return;
+        TraceSet& b = sets[s];
+        r0hip_segment_job& j = jobs[b.job];
+        const r0hip_trace_input& tr = *j.trace;
+        try {
+          ensure_init();
+          r0hip_raw_preflight_trace pf = tr.preflight;  // the set's device copies
+          pf.cycles = b.cycles.p;
+          pf.txns = pf.txns_len ? b.txns.p : nullptr;
+          pf.bigint_bytes = pf.bigint_bytes_len ? reinterpret_cast<const uint8_t*>(b.bigint.p) : nullptr;
+          std::vector<uint32_t> mix;
+          std::vector<uint32_t> seal = prove_trace(
+              suite, po2, tr.mode, b.glob.p, b.index.p, tr.inj_rows, b.offsets.p, b.values.p, &pf, j.h_bigint,
+              j.n_bigint, true, &mix, [&](hipStream_t st) {
+                b.wait_landed();
+                {
+                  std::lock_guard<std::mutex> lk(b.mu);
+                  if (j.error) throw std::runtime_error(j.error);
+                }
+                HIP_OK(hipStreamWaitEvent(st, b.ev, 0));
+              });
+          HIP_OK(hipStreamSynchronize(stream()));
+          j.seal_len = seal.size();
+          if (j.h_mix_out) memcpy(j.h_mix_out, mix.data(), mix.size() * 4);
+          R0_REQUIRE(!j.h_seal || seal.size() <= j.seal_cap, "seal buffer too small");
+          if (j.h_seal) memcpy(j.h_seal, seal.data(), seal.size() * 4);
+        } catch (const std::exception& e) {
+          {
+            std::lock_guard<std::mutex> lk(b.mu);
+            if (!j.error) j.error = dup_msg(e.what());
+          }
+          drain_after_error();  // kernels queued before the throw may still read this set
+        }
+        b.wait_landed();  // the uploader is done with this job before the set is refilled
+        free_q.put(s);
+      }
+    });
+  }
+  uploader.join();
+  for (auto& t : provers) t.join();
+  for (size_t i = 0; i < njobs; i++)
+    if (jobs[i].error) return dup_msg((std::string("segment ") + std::to_string(i) + ": " + jobs[i].error).c_str());
+  return nullptr;
+}
+
 }  // namespace
 }  // namespace r0
 
@@ -125,6 +289,16 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
     ensure_init();
     if (njobs == 0) return nullptr;
     const size_t k = std::max<size_t>(1, std::min<size_t>(in_flight ? in_flight : 2, njobs));
+    for (size_t i = 0; i < njobs; i++) {
+      jobs[i].error = nullptr;
+      jobs[i].seal_len = 0;
+    }
+    if (jobs[0].trace) {
+      R0_REQUIRE(std::string(c->name) == "rv32im", "trace jobs are rv32im segments");
+      R0_REQUIRE(write_version && version == 2, "trace jobs write the rv32im seal version word 2");
+      return prove_trace_jobs(suite, po2, jobs, njobs, k);
+    }
+    for (size_t i = 0; i < njobs; i++) R0_REQUIRE(!jobs[i].trace, "a call mixes witness jobs and trace jobs");
     const bool device_accum_ok = std::string(c->name) == "rv32im";
     const size_t n = size_t(1) << po2;
     // group_sizes: accum 0, code 1, data 2 (the reference's register-group order)

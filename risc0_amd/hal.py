@@ -551,11 +551,98 @@ def prove_segment_trace_resident(hal, t, mode=0, bigint_records=None, seal_cap=1
     return seal[: n.value].copy(), mix
 
 
+class TraceInput(C.Structure):
+    """struct r0hip_trace_input (include/r0hip.h): one preflight trace, host pointers"""
+    _fields_ = [("mode", C.c_uint32), ("h_global", C.c_void_p), ("h_inj_index", C.c_void_p), ("inj_rows", C.c_size_t),
+                ("h_inj_offsets", C.c_void_p), ("h_inj_values", C.c_void_p), ("preflight", RawPreflightTrace)]
+
+
 class SegmentJob(C.Structure):
     """struct r0hip_segment_job (include/r0hip.h)"""
     _fields_ = [("h_code", C.c_void_p), ("h_data", C.c_void_p), ("h_accum", C.c_void_p), ("h_global", C.c_void_p),
                 ("h_bigint", C.c_void_p), ("n_bigint", C.c_size_t), ("h_seal", C.c_void_p),
-                ("seal_cap", C.c_size_t), ("seal_len", C.c_size_t), ("h_mix_out", C.c_void_p), ("error", C.c_void_p)]
+                ("seal_cap", C.c_size_t), ("seal_len", C.c_size_t), ("h_mix_out", C.c_void_p), ("error", C.c_void_p),
+                ("trace", C.c_void_p)]
+
+
+class TraceJob:
+    """one rv32im segment's preflight trace as the segment pipeline takes it (r0hip_trace_input):
+    the global vector, the injector (index / offsets / Montgomery values), the cycle and
+    transaction records, the BigInt bytes and backs. The arrays are kept as given (page-locked
+    views from host_array() copy at full PCIe rate; others are staged)."""
+
+    def __init__(self, glob, inj_index, inj_offsets, inj_values, cycles, txns, table_split, bigint=None,
+                 bigint_records=None, mode=0):
+        u = lambda a: a if isinstance(a, np.ndarray) and a.dtype == np.uint32 and a.flags.c_contiguous \
+            else np.ascontiguousarray(a, dtype=np.uint32)
+        self.glob, self.index, self.offsets, self.values = u(glob), u(inj_index), u(inj_offsets), u(inj_values)
+        self.cycles, self.txns = np.ascontiguousarray(cycles), np.ascontiguousarray(txns)
+        self.bigint = None if bigint is None or not len(bigint) else np.ascontiguousarray(bigint, dtype=np.uint8)
+        self.backs = bigint_backs(bigint_records)
+        pf = RawPreflightTrace(self.cycles.ctypes.data, self.txns.ctypes.data if self.txns.nbytes else None,
+                               None if self.bigint is None else self.bigint.ctypes.data, self.txns.nbytes // 20,
+                               0 if self.bigint is None else self.bigint.size, table_split)
+        self.struct = TraceInput(mode, self.glob.ctypes.data, self.index.ctypes.data, self.index.size - 1,
+                                 self.offsets.ctypes.data if self.offsets.size else None,
+                                 self.values.ctypes.data if self.values.size else None, pf)
+
+    def h2d_bytes(self):
+        return sum(a.nbytes for a in (self.glob, self.index, self.offsets, self.values, self.cycles, self.txns)) + \
+            (0 if self.bigint is None else self.bigint.nbytes)
+
+
+def host_array(shape, dtype):
+    """a numpy array over page-locked host memory (r0hip_host_alloc); the block goes back with
+    r0hip_host_free when the last view of it is gone"""
+    dtype = np.dtype(dtype)
+    count = int(np.prod(shape))
+    nbytes = max(1, count * dtype.itemsize)
+    p = C.c_void_p()
+    check(lib().r0hip_host_alloc(C.byref(p), nbytes))
+    block = (C.c_uint8 * nbytes).from_address(p.value)
+    block._owner = _HostBlock(p.value)  # the ctypes array is every view's base
+    return np.frombuffer(block, dtype=dtype, count=count).reshape(shape)
+
+
+def pinned_copy(a):
+    """a copy of `a` in page-locked host memory (host_array)"""
+    a = np.ascontiguousarray(a)
+    out = host_array(a.shape, a.dtype)
+    out[...] = a
+    return out
+
+
+class _HostBlock:
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    def __del__(self):
+        if self.ptr:
+            lib().r0hip_host_free(C.c_void_p(self.ptr))
+            self.ptr = None
+
+
+def prove_trace_segments(hal, po2, traces, in_flight=2, seal_cap=1 << 22):
+    """The native segment pipeline with trace jobs (r0hip_prove_segments, job.trace): each
+    TraceJob is one rv32im prove_core from its preflight trace; an uploader copies the traces
+    into in_flight + 1 device trace sets while in_flight provers run. Returns [(seal, mix)] in
+    job order."""
+    jobs = (SegmentJob * len(traces))()
+    seals, mixes, keep = [], [], []
+    for j, t in zip(jobs, traces):
+        keep.append(t)
+        j.trace = C.cast(C.pointer(t.struct), C.c_void_p).value
+        if t.backs is not None:
+            j.h_bigint, j.n_bigint = C.cast(t.backs, C.c_void_p).value, len(t.backs)
+        seals.append(np.zeros(seal_cap, dtype=np.uint32))
+        mixes.append(np.zeros(36, dtype=np.uint32))
+        j.h_seal, j.seal_cap, j.h_mix_out = seals[-1].ctypes.data, seal_cap, mixes[-1].ctypes.data
+    err = lib().r0hip_prove_segments(b"rv32im", hal.suite, po2, 1, 2, C.cast(jobs, C.c_void_p), len(traces), in_flight)
+    for j in jobs:
+        if j.error:
+            libc_free(j.error)
+    check(err)
+    return [(seal[: j.seal_len].copy(), mix) for j, seal, mix in zip(jobs, seals, mixes)]
 
 
 def prove_segments(hal, circuit, po2, witnesses, version=None, in_flight=2, seal_cap=1 << 24):

@@ -45,6 +45,7 @@ KERNEL_START = 0xC0000000
 KERNEL_END = 0xFF000000
 SAFE_WRITE_WADDR = 0xFFFF0100 // 4
 MEPC_WADDR = 0xFFFF0200 // 4
+USER_START_WADDR = 0x00010000 // 4  # binfmt image.rs:49
 ECALL_DISPATCH_WADDR = 0xFFFF1000 // 4
 MAX_IO_BYTES, MAX_IO_WORDS = 1024, 4
 PFLAG_IS_ELEM, PFLAG_CHECK_OUT = 0x80000000, 0x40000000
@@ -445,15 +446,24 @@ class Trace:
 
     def __init__(self, po2, program, *, base_pc=0x10000, data=None, regs=None, seed=1, max_user_cycles=None,
                  read_nodes=True, discover_cycles=None, kernel=None, kernel_pc=KERNEL_START, machine_regs=None,
-                 read_record=(), write_record=(), bigint_nondet=None):
+                 read_record=(), write_record=(), bigint_nondet=None, boot_kernel=False, zero_digests=False,
+                 fast_loop=None):
         """program: user code at base_pc. kernel: machine-mode code at kernel_pc, entered by a
         user `ecall` through ECALL_DISPATCH_ADDR (r0vm.rs:342-352); it leaves with `mret` or
         a machine ecall (terminate, host read/write, Poseidon2). read_record / write_record:
         the segment's host-read payloads (bytes) and host-write return values. bigint_nondet:
         the BigInt ecall's nondeterministic witness, f(trace, mode) -> {word address: 16 bytes},
-        standing in for the bibc nondet program's evaluation (execute/bigint.rs:190-194)."""
+        standing in for the bibc nondet program's evaluation (execute/bigint.rs:190-194).
+        boot_kernel: the image MemoryImage::with_kernel builds (binfmt/src/image.rs:178-184): the
+        segment resumes in machine mode at kernel_pc, the user entry sits at USER_START_ADDR and
+        the kernel installs its own ecall dispatch. zero_digests: input, output and PoVW nonce
+        digests start zero (a first segment) instead of seeded words. fast_loop: (head_pc,
+        iterations_left(trace)) — a user loop whose iterations produce the same rows and
+        transactions up to an affine change per iteration; once three iterations agree, the
+        rest (bar the last two) are emitted as numpy blocks (_bulk_loop) instead of stepped."""
         self.po2 = po2
         self.bigint_nondet = bigint_nondet
+        self.fast_loop = fast_loop
         self.rng = np.random.default_rng(seed)
         # image: code, data, registers, suspend state, input/output digests
         mem = {}
@@ -461,7 +471,7 @@ class Trace:
             mem[base_pc // 4 + i] = w
         for i, w in enumerate(kernel or ()):
             mem[kernel_pc // 4 + i] = w
-        if kernel:
+        if kernel and not boot_kernel:
             mem[ECALL_DISPATCH_WADDR] = kernel_pc
         for a, w in (data or {}).items():
             mem[a // 4] = w
@@ -472,12 +482,21 @@ class Trace:
             mem[MACHINE_REGS_WADDR + r] = v
         self.read_record = [list(x) for x in read_record]
         self.write_record = list(write_record)
-        mem[SUSPEND_PC_WADDR] = base_pc
-        mem[SUSPEND_MODE_WADDR] = 0
+        if boot_kernel:
+            mem[USER_START_WADDR] = base_pc
+            mem[SUSPEND_PC_WADDR] = kernel_pc
+            mem[SUSPEND_MODE_WADDR] = 1
+        else:
+            mem[SUSPEND_PC_WADDR] = base_pc
+            mem[SUSPEND_MODE_WADDR] = 0
         self.input_words = [int(x) for x in self.rng.integers(0, 1 << 32, 8, dtype=np.uint64)]
         for i in range(8):
             mem[GLOBAL_OUTPUT_WADDR + i] = int(self.rng.integers(0, 1 << 32))
         self.nonce = [int(x) for x in self.rng.integers(0, 1 << 32, 8, dtype=np.uint64)]
+        if zero_digests:
+            self.input_words, self.nonce = [0] * 8, [0] * 8
+            for i in range(8):
+                del mem[GLOBAL_OUTPUT_WADDR + i]
         self.rand_z = [int(x) for x in self.rng.integers(0, P, 4)]
         self.program_end = base_pc + 4 * len(program)
         # pass 1 (the executor's run that fixes the segment's partial image): the pages the
@@ -518,9 +537,15 @@ class Trace:
         self.build()
 
     def reset(self, mem, page_memory):
+        # rows and transactions: Python lists while stepping; numpy blocks (_flush, bulk loop
+        # iterations, padding) before them. Row and transaction numbers are global.
         self.cycles = []
-        self.backs = []
         self.txns = []
+        self._cyc_chunks, self._tx_chunks = [], []
+        self._row0 = self._tx0 = 0
+        self.backs = {}                   # row -> Back (the rows the injector adds columns to)
+        self.last_txn = {}                # address -> index of its last transaction
+        self.diff_inc = []                # extra diffCount increments (2 * row + k)
         self.pc = 0
         self.machine_mode = 0
         self.user_cycle = 0
@@ -537,10 +562,30 @@ class Trace:
         self.bigint_bytes = []
         self.bigint_idx = 0
 
+    def nrows(self):
+        return self._row0 + len(self.cycles)
+
+    def ntxns(self):
+        return self._tx0 + len(self.txns)
+
+    def _flush(self):
+        """move the stepped rows and transactions into numpy blocks"""
+        if self.cycles:
+            self._cyc_chunks.append(np.array(self.cycles, dtype=np.int64).reshape(-1, 11))
+            self._row0 += len(self.cycles)
+            self.cycles = []
+        if self.txns:
+            self._tx_chunks.append(np.array(self.txns, dtype=np.int64).reshape(-1, 5))
+            self._tx0 += len(self.txns)
+            self.txns = []
+
+    def last_row_mode(self):
+        return self.cycles[-1][4] if self.cycles else int(self._cyc_chunks[-1][-1, 4])
+
     # ---- memory (preflight.rs:571-634)
     def load_u32(self, addr, record=True):
         """LoadOp::Record (record=False: LoadOp::Load, the page is loaded but no txn is kept)"""
-        cycle = 2 * len(self.cycles)
+        cycle = 2 * self.nrows()
         if addr >= MERKLE_TREE_START_WADDR:
             if addr < MERKLE_TREE_END_WADDR:
                 word = self.page_memory[addr]
@@ -555,11 +600,12 @@ class Trace:
         self.orig_words.setdefault(addr, word)
         prev = self.prev_cycle.get(addr, U32_MAX)
         self.prev_cycle[addr] = cycle
+        self.last_txn[addr] = self.ntxns()
         self.txns.append((addr, cycle, word, prev, word))
         return word
 
     def store_u32(self, addr, word):
-        cycle = 2 * len(self.cycles) + 1
+        cycle = 2 * self.nrows() + 1
         if addr >= MEMORY_END_WADDR:
             prev_word = self.page_memory[addr]
             self.page_memory[addr] = word
@@ -571,14 +617,16 @@ class Trace:
                 self.dirty.add(addr // 256)
         prev = self.prev_cycle.get(addr, U32_MAX)
         self.prev_cycle[addr] = cycle
+        self.last_txn[addr] = self.ntxns()
         self.txns.append((addr, cycle, word, prev, prev_word))
 
     # ---- cycles (preflight.rs:373-469)
     def add_cycle(self, state, pc, major, minor, paging_idx=0, back=None):
+        if back is not None:
+            self.backs[self.nrows()] = back
         self.cycles.append([state, pc, major, minor, self.machine_mode, self.user_cycle, self.txn_idx, paging_idx,
                             self.bigint_idx, 0, 0])
-        self.backs.append(back)
-        self.txn_idx = len(self.txns)
+        self.txn_idx = self.ntxns()
         self.bigint_idx = len(self.bigint_bytes)
 
     def add_cycle_special(self, cur, nxt, pc, paging_idx=0, back=None):
@@ -740,7 +788,7 @@ class Trace:
             self.add_cycle(DECODE, self.pc, 7, 2)  # CONTROL0 / FENCE
         elif kind == "eany":
             # switched on the machine mode entering the EANY: the last row's
-            if self.cycles[-1][4] != 0:
+            if self.last_row_mode() != 0:
                 self.add_cycle(DECODE, self.pc, 8, 0)  # ECALL0 / MACHINE_ECALL
             else:
                 self.add_cycle(DECODE, self.pc, 7, 2)  # CONTROL0 / USER_ECALL
@@ -1029,8 +1077,8 @@ class Trace:
             self.load_u32(digest_waddr(1) + i)
         self.add_cycle_special(STORE_ROOT, CONTROL_TABLE, 0)
         # generate_tables / fini (preflight.rs:205-326)
-        self.table_split_cycle = len(self.cycles)
-        start = len(self.cycles)
+        self.table_split_cycle = self.nrows()
+        start = self.nrows()
         for i in range(16, 256, 16):
             self.add_cycle_special(CONTROL_TABLE, CONTROL_TABLE, i)
         self.machine_mode = 1
@@ -1039,45 +1087,68 @@ class Trace:
         self.machine_mode = 0
         self.add_cycle_special(CONTROL_TABLE, CONTROL_DONE, 0)
         # a segment that does not terminate: the shutdown threshold is this cycle count
-        self.segment_threshold = len(self.cycles)
+        self.segment_threshold = self.nrows()
         if not self.terminated:
-            diff = len(self.cycles) - self.segment_threshold
-            self.cycles[diff // 2][9 + diff % 2] += 1
+            self.diff_inc.append(self.nrows() - self.segment_threshold)
         self.machine_mode = 1
         self.add_cycle_special(CONTROL_DONE, CONTROL_DONE, 0)
-        assert len(self.cycles) - start == RESERVED_CYCLES
+        assert self.nrows() - start == RESERVED_CYCLES
         total = 1 << self.po2
-        assert len(self.cycles) <= total, "program too long for the segment"
-        while len(self.cycles) < total:
-            self.add_cycle_special(CONTROL_DONE, CONTROL_DONE, 0)
-        # wrap_memory_txns (preflight.rs:212-232)
-        txns = []
-        for (addr, cycle, word, prev, prev_word) in self.txns:
-            if prev == U32_MAX:
-                prev = self.prev_cycle[addr]
-            else:
-                assert cycle != prev
-                diff = cycle - 1 - prev
-                self.cycles[diff // 2][9 + diff % 2] += 1
-            if cycle == self.prev_cycle[addr]:
-                word = self.orig_words.get(addr, 0)
-            txns.append((addr, cycle, word, prev, prev_word))
-        self.txns = txns
+        assert self.nrows() <= total, "program too long for the segment"
+        # the padding rows: CONTROL_DONE repeated (no transactions, no backs)
+        pad = total - self.nrows()
+        self._flush()
+        if pad:
+            row = [CONTROL_DONE, 0, 7 + CONTROL_DONE // 8, CONTROL_DONE % 8, self.machine_mode, self.user_cycle,
+                   self.txn_idx, 0, self.bigint_idx, 0, 0]
+            self._cyc_chunks.append(np.tile(np.array(row, np.int64), (pad, 1)))
+            self._row0 += pad
+        cyc = np.concatenate(self._cyc_chunks) if self._cyc_chunks else np.zeros((0, 11), np.int64)
+        tx = np.concatenate(self._tx_chunks) if self._tx_chunks else np.zeros((0, 5), np.int64)
+        self._cyc_chunks = self._tx_chunks = None
+        # wrap_memory_txns (preflight.rs:212-232): an address's first transaction takes its last
+        # cycle as prevCycle; every other one counts cycle - 1 - prevCycle in diffCount; an
+        # address's last transaction carries its original word
+        prev = tx[:, 3]
+        first = np.flatnonzero(prev == U32_MAX)
+        if first.size:
+            prev[first] = [self.prev_cycle[int(a)] for a in tx[first, 0]]
+        rest = np.ones(len(tx), bool)
+        rest[first] = False
+        assert not np.any(tx[rest, 1] == prev[rest])
+        diffs = np.concatenate([tx[rest, 1] - 1 - prev[rest], np.array(self.diff_inc, np.int64)])
+        counts = np.bincount(diffs, minlength=2 * total)
+        assert counts.size == 2 * total, "diffCount past the segment"
+        cyc[:, 9] += counts[0::2]
+        cyc[:, 10] += counts[1::2]
+        for a, i in self.last_txn.items():
+            assert tx[i, 1] == self.prev_cycle[a]
+            tx[i, 2] = self.orig_words.get(a, 0)
+        self.cyc = np.zeros(total, CYCLE_DTYPE)
+        for j, f in enumerate(("state", "pc", "major", "minor", "machineMode", "userCycle", "txnIdx", "pagingIdx",
+                               "bigintIdx")):
+            self.cyc[f] = cyc[:, j]
+        self.cyc["diffCount"] = cyc[:, 9:11]
+        del cyc
+        self.tx = np.zeros(len(tx), TXN_DTYPE)
+        for j, f in enumerate(TXN_DTYPE.names):
+            self.tx[f] = tx[:, j]
+        del tx
         # update_p2_zcheck (preflight.rs:234-263)
         powers = [[1, 0, 0, 0]]
         for _ in range(16):
             powers.append(ext_mul(powers[-1], self.rand_z))
         z = [0, 0, 0, 0]
-        for row, back in enumerate(self.backs):
-            if back is None or back[0] != "p2":
+        C, X = self.cyc, self.tx
+        for row, back in self.backs.items():
+            if back[0] != "p2":
                 continue
             p2 = back[1]
-            cyc, nxt = self.cycles[row], self.cycles[row + 1]
-            state = (cyc[2] - 7) * 8 + cyc[3]
+            state = (int(C["major"][row]) - 7) * 8 + int(C["minor"][row])
             if state == POSEIDON_LOAD_IN:
                 z = ext_mul(z, powers[16])
-                for i, t in enumerate(range(cyc[6], nxt[6])):
-                    addr, cycle, word, prev, prev_word = self.txns[t]
+                for i, t in enumerate(range(int(C["txnIdx"][row]), int(C["txnIdx"][row + 1]))):
+                    cycle, word, prev, prev_word = (int(X[f][t]) for f in ("cycle", "word", "prevCycle", "prevWord"))
                     kind = p2.f["load_tx_type"]
                     if kind == TX_READ:
                         c0, c1 = 0, 1
@@ -1103,9 +1174,15 @@ class Trace:
         # the executor's segment ends at its suspend cycle (preflight.rs:174-176); a program
         # ends at a terminate ecall or (user code) past its last instruction
         self.user_cycles = 0
+        marks = [] if self.fast_loop else None
         while not self.terminated and (self.machine_mode or self.pc < self.program_end):
             if self.max_user_cycles is not None and self.user_cycles >= self.max_user_cycles:
                 break
+            if marks is not None and self.pc == self.fast_loop[0] and not self.machine_mode:
+                marks.append((self.nrows(), self.ntxns(), self.user_cycle, self.user_cycles))
+                if len(marks) == 5:
+                    self._bulk_loop(marks)
+                    marks = None
             self.step()
         # suspend (r0vm.rs:316-321, preflight.rs:528-543)
         self.store_u32(SUSPEND_PC_WADDR, self.pc)
@@ -1117,28 +1194,67 @@ class Trace:
         self.machine_mode = 3
         self.add_cycle_special(SUSPEND, POSEIDON_ENTRY, 0)
 
+    def _bulk_loop(self, marks):
+        """fast_loop: marks are (rows, txns, user_cycle, user_cycles) at the loop head before
+        iterations 0-4. Iterations 1-3 stepped in Python must differ by one constant delta in
+        every row and transaction field (words, cycles and prevCycles included); then the next K
+        iterations are that affine sequence, written as numpy blocks, and the machine state
+        (memory words, prevCycle, last transactions, cycle counters) is advanced as if they had
+        been stepped. The loop's last two iterations are left to Python (the exit branch)."""
+        (r1, t1, u1, v1), (r2, t2, u2, v2), (r3, t3, u3, v3), (r4, t4, u4, v4) = marks[1:]
+        R, T_ = r3 - r2, t3 - t2
+        assert r2 - r1 == R == r4 - r3 and t2 - t1 == T_ == t4 - t3, "loop iterations differ in shape"
+        assert self.backs.keys().isdisjoint(range(r1, r4)), "loop rows with backs"
+        rows = lambda a, b: np.array(self.cycles[a - self._row0:b - self._row0], np.int64).reshape(-1, 11)
+        txns = lambda a, b: np.array(self.txns[a - self._tx0:b - self._tx0], np.int64).reshape(-1, 5)
+        A, B, C = rows(r1, r2), rows(r2, r3), rows(r3, r4)
+        tA, tB, tC = txns(t1, t2), txns(t2, t3), txns(t3, t4)
+        dr, dt = C - B, tC - tB
+        if not (np.array_equal(B - A, dr) and np.array_equal(tB - tA, dt) and u3 - u2 == u4 - u3 == u2 - u1
+                and v3 - v2 == v4 - v3 == v2 - v1):
+            return  # not affine: keep stepping
+        assert not C[:, 9:].any() and not (tC[:, 3] == U32_MAX).any()
+        k = int(self.fast_loop[1](self)) - 2
+        if self.max_user_cycles is not None:
+            k = min(k, (self.max_user_cycles - self.user_cycles) // max(1, v4 - v3) - 2)
+        if k <= 0:
+            return
+        emit = not self.discover
+        j = np.arange(1, k + 1, dtype=np.int64)
+        last_rows = C + k * dr
+        last_tx = tC + k * dt
+        assert last_tx[:, 2].max() < (1 << 32) and last_tx[:, 4].max() < (1 << 32) and last_tx[:, 2].min() >= 0
+        if emit:
+            self._flush()
+            self._cyc_chunks.append((C[None] + j[:, None, None] * dr[None]).reshape(-1, 11))
+            self._tx_chunks.append((tC[None] + j[:, None, None] * dt[None]).reshape(-1, 5))
+            self._row0 += k * R
+            self._tx0 += k * T_
+        else:  # the discovery pass needs only the machine state
+            self._row0 += k * R
+            self._tx0 += k * T_
+        base = self.ntxns() - T_
+        for i, (addr, cycle, word, _, _) in enumerate(last_tx.tolist()):
+            self.prev_cycle[addr] = cycle
+            self.last_txn[addr] = base + i
+            if cycle & 1:  # a store
+                self.mem[addr] = word
+        self.user_cycle += k * (u4 - u3)
+        self.user_cycles += k * (v4 - v3)
+        self.txn_idx = self.ntxns()
+
     # ---- outputs
     def arrays(self):
-        """(cycles, txns) as the reference's RawPreflightCycle / RawMemoryTransaction arrays"""
-        cyc = np.zeros(len(self.cycles), CYCLE_DTYPE)
-        c = np.array(self.cycles, dtype=np.uint64)
-        for j, f in enumerate(("state", "pc", "major", "minor", "machineMode", "userCycle", "txnIdx", "pagingIdx",
-                               "bigintIdx")):
-            cyc[f] = c[:, j]
-        cyc["diffCount"] = c[:, 9:11]
-        tx = np.zeros(len(self.txns), TXN_DTYPE)
-        if self.txns:
-            t = np.array(self.txns, dtype=np.uint64)
-            for j, f in enumerate(TXN_DTYPE.names):
-                tx[f] = t[:, j]
-        return cyc, tx
+        """(cycles, txns) as the reference's RawPreflightCycle / RawMemoryTransaction arrays
+        (the trace's own arrays: copy before changing them)"""
+        return self.cyc, self.tx
 
     def injector_arrays(self, lay=None):
         """the Injector (witgen/mod.rs:329-378) as hal.scatter takes it: index (rows + 1),
         offsets (col * rows + row), Montgomery values"""
         rows = 1 << self.po2
         r, c, v = self.injector(lay or layout())
-        index = np.zeros(rows + 1, np.uint32)
+        index = np.zeros(rows + 1, np.int64)
         np.add.at(index, r.astype(np.int64) + 1, 1)
         index = np.cumsum(index).astype(np.uint32)
         assert np.all(np.diff(r.astype(np.int64)) >= 0)  # pushed row by row
@@ -1156,26 +1272,26 @@ class Trace:
     def bigint_records(self):
         """the Back::BigInt rows as the accumulation's records [(row, poly_op, coeff, bytes)]
         (witgen/mod.rs:187-199)"""
-        return [(row, b[1]["poly_op"], b[1]["coeff"], list(b[1]["bytes"])) for row, b in enumerate(self.backs)
-                if b is not None and b[0] == "bigint"]
+        return [(row, b[1]["poly_op"], b[1]["coeff"], list(b[1]["bytes"])) for row, b in self.backs.items()
+                if b[0] == "bigint"]
 
     def injector(self, lay):
-        """(rows, cols, plain values) of build_injector (witgen/mod.rs:226-270), in push order"""
-        rows, cols, vals = [], [], []
+        """(rows, cols, plain values) of build_injector (witgen/mod.rs:226-270), in push order:
+        per row its Back's columns, then cycle, next pc (low, high), next state, next mode"""
+        br, bc, bv = [], [], []  # the backs' entries
 
         def put(r, c, v):
-            rows.append(r)
-            cols.append(c)
-            vals.append(v)
-        for row, back in enumerate(self.backs):
-            cyc = self.cycles[row]
-            if back is not None and back[0] == "p2":
+            br.append(r)
+            bc.append(c)
+            bv.append(v)
+        for row, back in self.backs.items():
+            if back[0] == "p2":
                 for col, v in zip(lay["poseidon2_state"], back[1].as_array()):
                     put(row, col, v)
-            elif back is not None and back[0] == "ecall":
+            elif back[0] == "ecall":
                 for col, v in zip(lay["ecall_s"], back[1]):
                     put(row, col, v)
-            elif back is not None and back[0] == "sha2":  # fp_array, then u32 bits (witgen/mod.rs:253-260)
+            elif back[0] == "sha2":  # fp_array, then u32 bits (witgen/mod.rs:253-260)
                 st = back[1]
                 for col, v in zip(lay["sha2_fp"], (st["state_in_addr"], st["state_out_addr"], st["data_addr"],
                                                    st["count"], st["k_addr"], st["round"], st["next_state"])):
@@ -1183,18 +1299,36 @@ class Trace:
                 for col, v in zip(lay["sha2_u32"], (st["a"], st["e"], st["w"])):
                     for b in range(32):
                         put(row, col + b, (v >> b) & 1)
-            elif back is not None and back[0] == "bigint":  # BigIntState::as_array (witgen/bigint.rs:213-238)
+            elif back[0] == "bigint":  # BigIntState::as_array (witgen/bigint.rs:213-238)
                 st = back[1]
                 arr = [st["is_ecall"], st["mode"], st["pc"], st["poly_op"], st["coeff"]] + st["bytes"] + \
                     [st["next_state"]]
                 for col, v in zip(lay["bigint_state"], arr):
                     put(row, col, v)
-            put(row, lay["cycle"], row)
-            put(row, lay["next_pc_low"], cyc[1] & 0xFFFF)
-            put(row, lay["next_pc_high"], cyc[1] >> 16)
-            put(row, lay["next_state_0"], cyc[0])
-            put(row, lay["next_machine_mode"], cyc[4])
-        return np.array(rows, np.uint32), np.array(cols, np.uint32), np.array(vals, np.uint64)
+        n = len(self.cyc)
+        br = np.array(br, np.int64)
+        nb = np.bincount(br, minlength=n) if br.size else np.zeros(n, np.int64)
+        start = np.zeros(n + 1, np.int64)
+        np.cumsum(nb + 5, out=start[1:])
+        total = int(start[-1])
+        rows = np.empty(total, np.uint32)
+        cols = np.empty(total, np.uint32)
+        vals = np.empty(total, np.uint64)
+        if br.size:  # the k-th entry of a row's Back goes to start[row] + k (entries are in row order)
+            k = np.arange(br.size) - np.repeat(np.cumsum(nb) - nb, nb)
+            at = start[br] + k
+            rows[at], cols[at], vals[at] = br, bc, bv
+        pc = self.cyc["pc"].astype(np.uint64)
+        std = ((lay["cycle"], np.arange(n, dtype=np.uint64)), (lay["next_pc_low"], pc & 0xFFFF),
+               (lay["next_pc_high"], pc >> 16), (lay["next_state_0"], self.cyc["state"].astype(np.uint64)),
+               (lay["next_machine_mode"], self.cyc["machineMode"].astype(np.uint64)))
+        base = start[:-1] + nb
+        ar = np.arange(n, dtype=np.uint32)
+        for j, (col, v) in enumerate(std):
+            rows[base + j] = ar
+            cols[base + j] = col
+            vals[base + j] = v
+        return rows, cols, vals
 
     def global_values(self, lay):
         """build_global_vec (witgen/mod.rs:272-327): plain values, None = Val::INVALID"""
@@ -1468,3 +1602,245 @@ def ecall_trace(po2, seed=1, n_user=60, data_base=0x00100000, terminate=True, sh
                  read_record=[bytes(int(x) for x in rng.integers(0, 256, 23)) for _ in range(reps)],
                  write_record=[0] + [8] * reps + [0],
                  bigint_nondet=bigint_mul_add_nondet if bigint else None)
+
+
+# ------------------------------------------------------------------ the reference's benchmark guest
+class Asm:
+    """a two-pass assembler over asm(): labels, and the pseudo-instructions gas expands with a
+    fixed size (li, la = auipc + addi, lw from a symbol = auipc + lw, call = jal ra, j, jr,
+    mv, ret, unimp)"""
+
+    def __init__(self, base):
+        self.base, self.items, self.labels = base, [], {}
+
+    def pc(self):
+        return self.base + 4 * len(self.items)
+
+    def label(self, name):
+        self.labels[name] = self.pc()
+
+    def __call__(self, op, *a):
+        self.items.append((op, a, self.pc()))
+
+    def li(self, rd, v):
+        v &= U32_MAX
+        if v < 0x800 or v >= 0xFFFFF800:  # fits a 12-bit immediate
+            self("addi", rd, 0, s32(v))
+            return
+        for w in li(rd, v):
+            self.items.append(("word", (w,), self.pc()))
+        if self.items[-1][1][0] == asm("addi", rd, rd, 0):  # gas drops a zero low part
+            self.items.pop()
+
+    def la(self, rd, sym, op="addi"):
+        self("auipc_hi", rd, sym)
+        self(op + "_lo", rd, sym)
+
+    def words(self):
+        out = []
+        L = self.labels
+        for op, a, pc in self.items:
+            if op == "word":
+                out.append(a[0])
+            elif op == "auipc_hi":
+                off = (L[a[1]] - pc) & U32_MAX
+                out.append(asm("auipc", a[0], ((off + 0x800) >> 12) & 0xFFFFF))
+            elif op in ("addi_lo", "lw_lo"):
+                off = (L[a[1]] - (pc - 4)) & U32_MAX
+                lo = s32(off & 0xFFF) if off & 0x800 == 0 else (off & 0xFFF) - 0x1000
+                out.append(asm(op[:-3], a[0], a[0], lo))
+            elif op in B_OPS:
+                out.append(asm(op, a[0], a[1], L[a[2]] - pc))
+            elif op == "jal":
+                out.append(asm("jal", a[0], L[a[1]] - pc))
+            elif op == "unimp":
+                out.append(0xC0001073)  # csrrw x0, cycle, x0: the illegal instruction gas emits
+            else:
+                out.append(asm(op, *a))
+        return out
+
+
+# loop.s's symbols (a layout a riscv32 gcc -nostdlib link gives it: _start after the ELF and
+# program headers, .rodata after .text in the text segment, .data on the next page)
+LOOP_S_TEXT = 0x00010074
+SYS_READ_NAME = b"risc0_zkvm_platform::syscall::nr::SYS_READ\0"
+NULL_DIGEST = [0x5c176f83, 0x53f3c062, 0x42651683, 0x340b8b7e, 0x19d2d1f6, 0xae4d7602, 0xb8c606b4, 0xb075b53d]
+REG_SP, REG_RA, REG_GP, REG_TP, REG_T6 = 2, 1, 3, 4, 31
+REG_A4, REG_A5, REG_S0, REG_S1, REG_S2 = 14, 15, 8, 9, 10 + 8
+REG_S3, REG_S4, REG_S5 = 19, 20, 21
+# datasheet.rs:42-58: loop iterations per segment po2, and the full po2=20 segment
+CYCLES_PO2_ITERS = {15: 1024 * 8, 16: 1024 * 16, 17: 1024 * 32, 18: 1024 * 96, 19: 1024 * 128, 20: 1024 * 256,
+                    21: 1024 * 256 * 3, 22: 1024 * 256 * 7, 23: 1024 * 256 * 15, 24: 1024 * 256 * 31}
+ITERATIONS_FULL_PO2_20_SEGMENT = 1024 * 494 + 817
+
+
+def loop_s_program():
+    """risc0/zkvm/examples/loop.s:20-47: read `count` from stdin through the v1 SYS_READ
+    software ecall, count a4 up to it (addi + bltu), halt with the null output digest.
+    Returns (code words, {byte address: word} of .rodata/.data, the loop head, &count)."""
+    a = Asm(LOOP_S_TEXT)
+    T0, T6, A0, A1, A2, A3, A4, A5 = REG_T0, REG_T6, REG_A0, REG_A1, REG_A2, REG_A3, REG_A4, REG_A5
+    a.li(T0, 2)             # ecall::SOFTWARE
+    a.li(T6, 12)            # Syscall::Read
+    a.la(A0, "count")
+    a.li(A1, 4)
+    a.la(A2, "sys_read")
+    a.li(A3, 0)             # STDIN_FILENO
+    a.li(A4, 4)
+    a("ecall")
+    a.li(A4, 0)
+    a.la(A5, "count", "lw")  # lw a5, count
+    a.label("loop")
+    a("addi", A4, A4, 1)
+    a("bltu", A4, A5, "loop")
+    a.li(T0, 0)             # ecall::HALT
+    a.li(A0, 0)             # halt::TERMINATE, exit code 0
+    a.la(A1, "digest")
+    a("ecall")
+    end = a.pc()
+    digest = (end + 15) & ~15  # .rodata, .align 4
+    name = (digest + 32 + 15) & ~15
+    count = 0x00011000 + (((name + len(SYS_READ_NAME) + 15) & ~15) & 0xFFF)  # .data
+    a.labels.update(digest=digest, sys_read=name, count=count)
+    data = {digest + 4 * i: w for i, w in enumerate(NULL_DIGEST)}
+    nm = SYS_READ_NAME + b"\0" * (-len(SYS_READ_NAME) % 4)
+    for i in range(0, len(nm), 4):
+        data[name + i] = int.from_bytes(nm[i:i + 4], "little")
+    data[count] = 0
+    return a.words(), data, a.labels["loop"], count
+
+
+def v1compat_kernel(base=KERNEL_START):
+    """the v1compat kernel (risc0/zkos/v1compat/src/kernel.s): _start (global pointer, kernel
+    stack, the ecall dispatch address, tp = USER_REGS_ADDR, the table, MEPC = user entry - 4,
+    mret), the ecall table and dispatch, _ecall_halt (the output digest to GLOBAL_OUTPUT_ADDR,
+    then the terminate host ecall) and _ecall_software. ecall_software / sys_read are Rust in
+    main.rs:283-304, 500-548; they are restated here for the Read syscall only, as assembly
+    with main.rs's calls: one chunk (nbytes <= MAX_IO_BYTES), the main host read of whole words,
+    read_a0_a1 (a host read of 8 bytes into the kernel stack), the final-word copy, set_ureg
+    of a0 and a4. The other table entries lead to `unimp`. The compiled v1compat.elf ships as a
+    prebuilt binary and is neither run nor loaded, so these instructions are a restatement
+    with the same calls and memory traffic per syscall, not the ELF's instruction stream."""
+    k = Asm(base)
+    SP, RA, GP, TP, T0, T1, T2, T3 = REG_SP, REG_RA, REG_GP, REG_TP, REG_T0, REG_T1, REG_T2, REG_T3
+    A0, A1, A2, A3, A4, A7, S1, S2, S3, S4, S5 = (REG_A0, REG_A1, REG_A2, REG_A3, REG_A4, REG_A7, REG_S1, REG_S2,
+                                                  REG_S3, REG_S4, REG_S5)
+    USER_REGS = 0xFFFF0080
+    k.label("_start")
+    k.la(GP, "__global_pointer$")
+    k.li(SP, 0xFFF00000)                 # STACK_TOP
+    k.li(T0, ECALL_DISPATCH_WADDR * 4)
+    k.la(T1, "_ecall_dispatch")
+    k("sw", T1, T0, 0)
+    k.li(TP, USER_REGS)
+    k.la(S1, "_ecall_table")
+    k.li(S2, 8)                          # ECALL_TABLE_SIZE
+    k.li(A0, USER_START_WADDR * 4)
+    k.li(A1, MEPC_WADDR * 4)
+    k("lw", A2, A0, 0)
+    k("addi", A2, A2, -4)
+    k("sw", A2, A1, 0)
+    k("mret")
+    k.label("_ecall_table")
+    for tgt in ("_ecall_halt", "_unimp", "_ecall_software", "_unimp", "_unimp", None, "_unimp", "_unimp"):
+        k("jal", 0, tgt) if tgt else k("unimp")
+    k.label("_ecall_dispatch")
+    k("lw", A0, TP, 4 * REG_T0)
+    k("bgeu", A0, S2, "_unimp")
+    k("slli", A0, A0, 2)
+    k("add", A1, S1, A0)
+    k("jalr", 0, A1, 0)
+    k.label("_ecall_halt")
+    k("lw", T0, TP, 4 * REG_A1)          # out_state
+    k.li(T1, GLOBAL_OUTPUT_WADDR * 4)
+    for i in range(8):
+        k("lw", T2, T0, 4 * i)
+        k("sw", T2, T1, 4 * i)
+    k("lw", A0, TP, 4 * REG_A0)
+    k("srli", A1, A0, 8)
+    k("andi", A1, A1, 0xFF)
+    k("slli", A1, A1, 16)
+    k("andi", A0, A0, 0xFF)
+    k("or", A0, A1, A0)
+    k("andi", T0, A0, 0xFF)
+    k.li(A1, 0)
+    k.li(A7, 0)                          # HOST_ECALL_TERMINATE
+    k("ecall")
+    k("beq", T0, 0, "_unimp")
+    k("mret")
+    k.label("_ecall_software")
+    k("lw", A0, TP, 4 * REG_T6)          # syscall nr
+    k("lw", A1, TP, 4 * REG_A2)          # syscall name (the host read's fd)
+    k("lw", A2, TP, 4 * REG_A0)          # from_host_ptr
+    k("lw", A3, TP, 4 * REG_A1)          # from_host_len
+    k("jal", RA, "ecall_software")
+    k("mret")
+    k.label("ecall_software")            # main.rs:283-304: Syscall::Read => sys_read(fd, buf, nbytes)
+    k.li(T0, 12)
+    k("bne", A0, T0, "_unimp")
+    k("addi", SP, SP, -16)
+    k("sw", RA, SP, 12)
+    k("add", T1, A2, A3)                 # assert_user_raw_slice(buf, nbytes)
+    k.li(T2, 0xC0000000)
+    k("bltu", T2, T1, "_unimp")
+    k("lw", S3, TP, 4 * REG_A4)          # user_nbytes = get_ureg(REG_A4)
+    k("sw", A3, TP, 4 * REG_A4)          # set_ureg(REG_A4, chunk nbytes)
+    k("andi", S4, A3, -4)                # nbytes_main
+    k("addi", S5, A2, 0)
+    k("addi", A0, A1, 0)                 # host_ecall_read(fd, buf, nbytes_main)
+    k("addi", A1, A2, 0)
+    k("addi", A2, S4, 0)
+    k.li(A7, 1)                          # HOST_ECALL_READ
+    k("ecall")
+    k.li(A0, 0)                          # read_a0_a1: host_ecall_read(0, &buf, 8)
+    k("addi", A1, SP, 0)
+    k.li(A2, 8)
+    k.li(A7, 1)
+    k("ecall")
+    k("lw", T1, SP, 0)                   # nread_bytes
+    k("lw", T2, SP, 4)                   # final_word
+    k("bltu", A3, T1, "_unimp")          # nread_bytes > nbytes: illegal_instruction
+    k("bgeu", S4, T1, "_done")
+    k("sub", T3, T1, S4)                 # the final partial word's bytes
+    k("add", T0, S5, S4)
+    k.label("_tail")
+    k("sb", T2, T0, 0)
+    k("srli", T2, T2, 8)
+    k("addi", T0, T0, 1)
+    k("addi", T3, T3, -1)
+    k("bne", T3, 0, "_tail")
+    k.label("_done")
+    k("sw", T1, TP, 4 * REG_A0)          # set_ureg(REG_A0, total_bytes)
+    k("sw", S3, TP, 4 * REG_A4)          # set_ureg(REG_A4, user_nbytes)
+    k("lw", RA, SP, 12)
+    k("addi", SP, SP, 16)
+    k("jalr", 0, RA, 0)                  # ret
+    k.label("_unimp")
+    k("unimp")
+    k.labels["__global_pointer$"] = base + 0x800
+    return k.words()
+
+
+def loop_s_iterations(po2):
+    """the datasheet's iteration count for a segment of 2^po2 rows (datasheet.rs:42-58)"""
+    return ITERATIONS_FULL_PO2_20_SEGMENT if po2 == 20 else CYCLES_PO2_ITERS[po2]
+
+
+def loop_s_trace(po2, iterations=None, seed=1, fast=True):
+    """the datasheet's loop guest (risc0/zkvm/examples/loop.s) run under the v1compat kernel
+    as one segment of 2^po2 rows: the boot into user mode, the SYS_READ of `count` (the host's
+    SysRead answers the main read with the four bytes and read_a0_a1 with (4, 0):
+    executor.rs:356-396), `count` loop iterations, the halt (output digest, terminate).
+    iterations: default the datasheet's count for po2 (ITERATIONS_FULL_PO2_20_SEGMENT at 20).
+    seed draws the Poseidon2 z-check challenge and the sparse Merkle image's off-path digests.
+    fast: emit the loop's iterations as numpy blocks (Trace._bulk_loop); fast=False steps
+    every instruction, as the tests compare."""
+    n = loop_s_iterations(po2) if iterations is None else iterations
+    assert n >= 1
+    code, data, head, count = loop_s_program()
+    kernel = v1compat_kernel()
+    # iterations still to run at the head: count - a4; the user registers live in memory
+    left = lambda tr: n - tr.mem.get(USER_REGS_WADDR + REG_A4, 0)
+    return Trace(po2, code, base_pc=LOOP_S_TEXT, data=data, seed=seed, kernel=kernel, boot_kernel=True,
+                 zero_digests=True, read_record=[n.to_bytes(4, "little"), (4).to_bytes(4, "little") + bytes(4)],
+                 fast_loop=(head, left) if fast else None)

@@ -216,3 +216,112 @@ def test_prove_segment_trace_resident_matches_host_path(hal):
     s2, m2 = r.prove_segment_trace_resident(hal, rt, bigint_records=te.bigint_records())
     assert np.array_equal(s2, seal) and np.array_equal(m2, mix)
     assert r.verify_seal("rv32im", hal.suite, seal, check_validity=True) == 14
+
+
+def _trace_job(r, t, pinned=False):
+    cyc, tx = t.arrays()
+    idx, off, val = W.injector_arrays(t)
+    arrs = [W.global_words(t), idx, off, val, cyc, tx]
+    if pinned:
+        arrs = [r.pinned_copy(a) for a in arrs]
+    return r.TraceJob(*arrs, t.table_split_cycle, bigint=t.bigint_array(), bigint_records=t.bigint_records())
+
+
+def test_prove_segments_trace_jobs_match_single(hal):
+    """the segment pipeline's trace jobs (r0hip_segment_job.trace: an uploader stages each
+    preflight trace into one of in_flight + 1 device trace sets while the provers run, as r0vm's
+    GPU queue does): six distinct po2=14 segments — loop guests of different lengths, a random
+    loop body, a BigInt ecall trace; page-locked and pageable inputs — over 2 provers and 3 sets
+    give the seals and mixes of r0hip_prove_segment_trace, job by job"""
+    import risc0_amd as r
+    traces = [T.loop_s_trace(14, 300 + 97 * i, seed=40 + i) for i in range(3)] + \
+        [T.loop_trace(14, body_len=24, seed=13), T.ecall_trace(14, seed=6, bigint=True), T.loop_s_trace(14, 5, seed=9)]
+    jobs = [_trace_job(r, t, pinned=i % 2 == 1) for i, t in enumerate(traces)]
+    got = r.prove_trace_segments(hal, 14, jobs, in_flight=2)
+    for t, j, (seal, mix) in zip(traces, jobs, got):
+        ref_seal, ref_mix = r.prove_segment_trace(hal, 14, j.glob, j.index, j.offsets, j.values, j.cycles, j.txns,
+                                                  t.table_split_cycle, bigint=t.bigint_array(),
+                                                  bigint_records=t.bigint_records())
+        assert np.array_equal(seal, ref_seal) and np.array_equal(mix, ref_mix)
+        assert r.verify_seal("rv32im", hal.suite, seal, check_validity=True) == 14
+    assert len({s.tobytes() for s, _ in got}) == len(traces)
+    # one in-flight prover, more jobs than sets: the same seals
+    again = r.prove_trace_segments(hal, 14, jobs[:4], in_flight=1)
+    assert all(np.array_equal(a[0], b[0]) for a, b in zip(again, got[:4]))
+
+
+def test_prove_segments_trace_job_errors(hal):
+    """a trace job whose injector index decreases fails with the host check's message (the other
+    jobs still prove), a call mixing trace and witness jobs is refused, and the next call is clean"""
+    import risc0_amd as r
+    t = T.loop_s_trace(14, 100, seed=3)
+    good = _trace_job(r, t)
+    bad = _trace_job(r, t)
+    bad.index[1001] = bad.index[1000] - 1
+    with pytest.raises(r.R0HipError, match="segment 1: .*injector index decreases"):
+        r.prove_trace_segments(hal, 14, [good, bad, good], in_flight=2)
+    (seal, mix), = r.prove_trace_segments(hal, 14, [good])
+    ref = r.prove_segment_trace(hal, 14, good.glob, good.index, good.offsets, good.values, good.cycles, good.txns,
+                                t.table_split_cycle)
+    assert np.array_equal(seal, ref[0])
+
+
+def test_prove_segment_trace_pinned_inputs_match_pageable(hal):
+    """r0hip_prove_segment_trace copies host arrays of 64 KiB or more that lie in r0hip_host_alloc
+    blocks straight to the device (no staging): the cycles, transactions and injector arrays in
+    page-locked memory give the seal and mix of the same arrays in pageable memory"""
+    import risc0_amd as r
+    t = T.loop_s_trace(16, seed=77)
+    cyc, tx = t.arrays()
+    idx, off, val = W.injector_arrays(t)
+    assert min(a.nbytes for a in (cyc, tx, idx, off, val)) >= 64 << 10
+    g = W.global_words(t)
+    ref = r.prove_segment_trace(hal, 16, g, idx, off, val, cyc, tx, t.table_split_cycle)
+    pin = [r.pinned_copy(a) for a in (idx, off, val, cyc, tx)]
+    got = r.prove_segment_trace(hal, 16, g, *pin[:3], pin[3], pin[4], t.table_split_cycle)
+    assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
+
+
+def test_loop_s_guest_seal_matches_cpu_path(hal, oracle):
+    """BASELINE configs[0] on the device: the datasheet's loop guest (loop.s under the v1compat
+    kernel, 16 K iterations at po2=16) from its preflight trace gives the CPU path's seal and mix
+    (compiled reference witgen + accumulation around the oracle prover), and it is valid"""
+    import risc0_amd as r
+    t = T.loop_s_trace(16, seed=16)
+    ref_seal, ref_mix, _, _, _ = W.prove_from_trace(t, oracle.POSEIDON2, oracle)
+    cyc, tx = t.arrays()
+    idx, off, val = W.injector_arrays(t)
+    seal, mix = r.prove_segment_trace(hal, 16, W.global_words(t), idx, off, val, cyc, tx, t.table_split_cycle)
+    assert np.array_equal(mix, ref_mix) and np.array_equal(seal, ref_seal)
+    assert r.verify_seal("rv32im", hal.suite, seal, check_validity=True) == 16
+
+
+def test_loop_s_witgen_po2_22_matches_reference(hal):
+    """po2=22 (the datasheet's 1,835,008 iterations, 14.7 M memory transactions): the GPU
+    witness generation equals the compiled reference's word for word"""
+    import risc0_amd as r
+    t = T.loop_s_trace(22, seed=22)
+    data, glob, cyc, tx = W.inputs(t)
+    ref_d, ref_g = W.run(data, glob, cyc, tx, t.table_split_cycle, 1 << 22, W.MODE_PARALLEL)
+    d, g = gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle)
+    del data
+    bad = np.flatnonzero(d != ref_d)
+    assert bad.size == 0, f"{bad.size} words differ; first (col, row): {[(int(i) >> 22, int(i) & ((1 << 22) - 1)) for i in bad[:8]]}"
+    assert np.array_equal(g, ref_g)
+    r.trim()
+
+
+def test_loop_s_trace_po2_24_proves_and_verifies(hal):
+    """BASELINE configs[2] from a trace: the maximum segment (po2=24, the datasheet's 8,126,464
+    loop iterations, 16.25 M user cycles, 211 x 2^24 data words) proved from its preflight —
+    witness generation, accumulation, prove — passes the native verifier with the validity
+    equation"""
+    import risc0_amd as r
+    r.trim()
+    t = T.loop_s_trace(24, seed=24)
+    job = _trace_job(r, t)
+    del t
+    (seal, _mix), = r.prove_trace_segments(hal, 24, [job], in_flight=1)
+    del job
+    assert r.verify_seal("rv32im", hal.suite, seal, check_validity=True) == 24
+    r.trim()

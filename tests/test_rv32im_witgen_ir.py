@@ -118,7 +118,7 @@ def test_trace_seal_verifies_with_validity(oracle):
     assert r.verify_seal("rv32im", r.POSEIDON2, seal_e, check_validity=True) == 14
     rows = 1 << 13
     d2 = d.copy()
-    row = next(i for i in range(rows) if t.cycles[i][0] == T.DECODE)
+    row = int(np.flatnonzero(t.arrays()[0]["state"] == T.DECODE)[0])
     d2[W.layout()["cycle"] * rows + row] = W.encode(row + 1)  # the cycle counter of a user row
     code = np.zeros(rows, np.uint32)
     bad, _, _ = oracle.prove_segment("rv32im", oracle.POSEIDON2, 13, code, d2, acc, g, version=2)
@@ -141,3 +141,42 @@ def test_trace_poseidon2_constants_match_oracle():
         assert T.RC[r * 24:(r + 1) * 24] == rc[r * 24:(r + 1) * 24]
     assert [T.RC[(4 + i) * 24] for i in range(21)] == [rc[(4 + i) * 24] for i in range(21)]
     assert T.M_INT_DIAG == diag
+
+
+def test_loop_s_bulk_iterations_match_stepped():
+    """the benchmark guest (loop.s under the v1compat kernel): its addi/bltu iterations
+    written as numpy blocks (Trace._bulk_loop) give the trace, injector and global vector of
+    stepping every instruction, for loops shorter and longer than the affine check's window"""
+    for n in (1, 4, 7, 600):
+        a, b = T.loop_s_trace(14, n, fast=False), T.loop_s_trace(14, n)
+        assert a.terminated and b.terminated
+        for x, y in zip(a.arrays() + a.injector_arrays(), b.arrays() + b.injector_arrays()):
+            assert np.array_equal(x, y)
+        assert np.array_equal(a.global_words(), b.global_words())
+        # the halt copied loop.s's null digest to GLOBAL_OUTPUT_ADDR; a4 counted to `count`
+        assert [b.mem[T.GLOBAL_OUTPUT_WADDR + i] for i in range(8)] == T.NULL_DIGEST
+        assert b.mem[T.USER_REGS_WADDR + T.REG_A4] == n
+
+
+def test_loop_s_datasheet_segments_fit():
+    """datasheet.rs:42-58: CYCLES_PO2_ITERS fills a segment of its po2 (here 16; po2 20 with
+    ITERATIONS_FULL_PO2_20_SEGMENT is covered by the bench and the GPU tests)"""
+    t = T.loop_s_trace(16)
+    cyc, tx = t.arrays()
+    assert len(cyc) == 1 << 16 and t.terminated
+    user = int(np.sum((cyc["state"] == T.DECODE)[:t.table_split_cycle]))
+    assert user >= 2 * T.loop_s_iterations(16)
+    assert T.loop_s_iterations(20) == 1024 * 494 + 817 and T.loop_s_iterations(24) == 1024 * 256 * 31
+
+
+@needs_ref
+def test_loop_s_guest_proves_and_verifies_on_cpu(oracle):
+    """BASELINE configs[0]: the benchmarks' loop guest, one po2=16 segment (16 K iterations,
+    datasheet.rs:44) proved on the CPU path — the compiled reference witgen and accumulation
+    around the oracle prover — and the receipt's seal passes the native verifier with the
+    validity equation, as the datasheet's prove + verify does (datasheet.rs:245-262)"""
+    import risc0_amd as r
+    t = T.loop_s_trace(16, seed=16)
+    seal, mix, d, g, acc = W.prove_from_trace(t, oracle.POSEIDON2, oracle)
+    assert r.verify_seal("rv32im", r.POSEIDON2, seal, check_validity=True) == 16
+    assert g[W.layout()["global"]["is_terminate"]] == W.encode(1)
