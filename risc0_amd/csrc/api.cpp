@@ -336,12 +336,13 @@ std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const 
   stage_reset();
   Span span("prove_segment_trace");
   DevBuf code(c->group_size(1) * n), data(data_cols * n), global(c->output_size), accum(c->group_size(0) * n);
-  HIP_OK(hipMemsetD32Async(code.p, 0u, code.words, s));  // INVALID, zeroized: nothing writes code
-  HIP_OK(hipMemsetD32Async(data.p, 0xFFFFFFFFu, data.words, s));
+  // the groups as WitnessGenerator::new / ::accum allocate them (INVALID), already zeroized where
+  // nothing reads INVALID, with the injector scattered in: one pass (rv32im_prover_groups_init)
   if (resident) {
     if (inputs_ready) inputs_ready(s);
     HIP_OK(hipMemcpyAsync(global.p, global_in, global.words * 4, hipMemcpyDeviceToDevice, s));
-    scatter(s, data.p, inj_index, inj_offsets, inj_values, inj_rows, data.words);
+    rv32im_prover_groups_init(s, data.p, code.p, accum.p, n, c->group_size(0), inj_index, inj_offsets, inj_values,
+                              inj_rows, data.words);
     Span w("witgen");
     rv32im_witgen_dev(s, mode, data.p, global.p, n, static_cast<const rvwg::PreflightCycle*>(pf->cycles),
                       static_cast<const rvwg::MemoryTxn*>(pf->txns), pf->txns_len, pf->bigint_bytes,
@@ -350,23 +351,21 @@ std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const 
     check_injector(inj_index, inj_rows, inj_offsets, inj_values, data_cols * n);
     const size_t n_inj = inj_index[inj_rows];
     upload_async(global.p, global_in, global.words * 4);
-    if (n_inj) {
-      auto* idx = static_cast<uint32_t*>(scratch((inj_rows + 1) * 4, kSlotRvInjIndex));
-      auto* off = static_cast<uint32_t*>(scratch(n_inj * 4, kSlotRvInjOffsets));
-      auto* val = static_cast<uint32_t*>(scratch(n_inj * 4, kSlotRvInjValues));
-      upload_async(idx, inj_index, (inj_rows + 1) * 4);
-      upload_async(off, inj_offsets, n_inj * 4);
-      upload_async(val, inj_values, n_inj * 4);
-      scatter(s, data.p, idx, off, val, inj_rows);
-    }
+    auto* idx = static_cast<uint32_t*>(scratch((inj_rows + 1) * 4, kSlotRvInjIndex));
+    auto* off = static_cast<uint32_t*>(scratch(n_inj * 4 + 4, kSlotRvInjOffsets));
+    auto* val = static_cast<uint32_t*>(scratch(n_inj * 4 + 4, kSlotRvInjValues));
+    upload_async(idx, inj_index, (inj_rows + 1) * 4);
+    upload_async(off, inj_offsets, n_inj * 4);
+    upload_async(val, inj_values, n_inj * 4);
+    rv32im_prover_groups_init(s, data.p, code.p, accum.p, n, c->group_size(0), idx, off, val, inj_rows, data.words);
     Span w("witgen");
     rv32im_witgen(s, mode, data.p, global.p, n, static_cast<const rvwg::PreflightCycle*>(pf->cycles),
                   static_cast<const rvwg::MemoryTxn*>(pf->txns), pf->txns_len, pf->bigint_bytes, pf->bigint_bytes_len,
                   pf->table_split_cycle, uint32_t(n), true);
   }
   eltwise_zeroize(s, global.p, global.words);  // the data group was zeroized by the witgen merge
-  HIP_OK(hipMemsetD32Async(accum.p, 0xFFFFFFFFu, accum.words, s));
-  const AccumStep acc{accum.p, n, false, h_bigint, n_bigint};
+  AccumStep acc{accum.p, n, false, h_bigint, n_bigint};
+  acc.zeroed = true;
   return prove_segment(*c, suite, po2, code.p, data.p, nullptr, global.p, true, 2, mix, nullptr, &acc);
 }
 

@@ -635,7 +635,7 @@ std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2
     } else {
       R0_REQUIRE(false, "prove_segment: no device accumulation for circuit " + name);
     }
-    eltwise_zeroize(s, acc->accum, rows * cols);
+    if (!acc->zeroed) eltwise_zeroize(s, acc->accum, rows * cols);
     prof.mark("accumulate");
     p.commit_group(0, acc->accum);  // nothing to wait for: the group never uploads
   } else {

@@ -232,6 +232,10 @@ struct AccumStep {
   // final mix before the step (witgen/mod.rs:178-205)
   const r0hip_bigint_back* bigint = nullptr;
   size_t n_bigint = 0;
+  // the group starts as rv32im_prover_groups_init leaves it (0 where the reference's INVALID
+  // would be zeroized, INVALID where phase 3 adds to it), with every row stepped: the zeroize
+  // after the accumulation would change nothing and is skipped
+  bool zeroed = false;
 };
 // BigIntAccum::step over the records (byte_poly.rs:403-470): 12 words per record (poly, term,
 // total), in record order; throws on an invalid EqZero as the reference does

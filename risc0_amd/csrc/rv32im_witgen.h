@@ -330,13 +330,24 @@ uint32_t rv32im_witgen_nslots(uint32_t major);
 const char* rv32im_witgen_message(uint32_t k);
 // the driver (rv32im_witgen.hip): both phases over cycles [0, last_cycle) with the preflight
 // arrays resident on the device; synchronises, throws on a failed check
-// zeroize (the prover's path): the data group is the prover's own, all INVALID but the injector's
-// words, and the merge writes 0 for INVALID words (eltwise_zeroize fused, as
-// hal_generate_witness does right after stepExec, witgen/mod.rs:166-169)
+// zeroize (the prover's path): the data group is the prover's own, INVALID in the injected
+// columns but the injector's words (rv32im_prover_groups_init; its other words are never read),
+// and the merge writes 0 for INVALID words (eltwise_zeroize fused, as hal_generate_witness does
+// right after stepExec, witgen/mod.rs:166-169)
 void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
                        const rvwg::PreflightCycle* d_cycles, const rvwg::MemoryTxn* d_txns, size_t n_txns,
                        const uint8_t* d_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle,
                        bool zeroize = false);
+// The prover's groups before witness generation, in one pass over the rows (replacing the INVALID
+// fills of WitnessGenerator::new and ::accum, witgen/mod.rs:135-170, 178-186, and the injector's
+// scatter): data INVALID in the injected columns — the only ones any arm or the prover-mode merge
+// reads back (every other data word is written by the merge) — then the injector's entries
+// (offsets at or past `limit` skipped, reads clamped to index[inj_rows]); code 0; accum INVALID in
+// the machine columns the accumulation's phase 3 adds to, 0 elsewhere: its zeroize then has
+// nothing left to change (AccumStep::zeroed; every row is stepped)
+void rv32im_prover_groups_init(hipStream_t s, uint32_t* data, uint32_t* code, uint32_t* accum, size_t rows,
+                               size_t accum_cols, const uint32_t* index, const uint32_t* offsets,
+                               const uint32_t* values, size_t inj_rows, uint64_t limit);
 // the same from host preflight arrays (uploaded first), as RawPreflightTrace hands them over
 void rv32im_witgen(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
                    const rvwg::PreflightCycle* h_cycles, const rvwg::MemoryTxn* h_txns, size_t n_txns,

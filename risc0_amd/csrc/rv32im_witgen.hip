@@ -116,9 +116,16 @@ __global__ __launch_bounds__(kMergeThreads) void merge_kernel(uint32_t* data, ui
                                                              const uint32_t* pos, const int16_t* slot_of, BinTable T,
                                                              bool prover, bool xcd_tiles) {
   constexpr uint32_t kMaskWords = (rvwg::kDataCols + 31) / 32;
-  __shared__ int16_t slot[rvwg::kMajors * rvwg::kDataCols];
+  __shared__ int16_t slot[(rvwg::kMajors + 1) * rvwg::kDataCols];
   __shared__ uint32_t msk[kMaskWords][kMergeThreads];  // this thread's row: its arm's stored-slot bits
   for (uint32_t t = threadIdx.x; t < rvwg::kMajors * rvwg::kDataCols; t += kMergeThreads) slot[t] = slot_of[t];
+  // rows past the stepped cycles keep their data words: in the prover's group only the injected
+  // columns hold them (the others were never written, and become 0)
+  for (uint32_t t = threadIdx.x; t < rvwg::kDataCols; t += kMergeThreads) {
+    uint32_t inj = prover ? 0u : uint32_t(rvwg::kInjectedCol);
+    for (uint32_t k = 0; prover && k < rvwg::kMajors; k++) inj |= uint32_t(slot_of[k * rvwg::kDataCols + t]) & rvwg::kInjectedCol;
+    slot[rvwg::kMajors * rvwg::kDataCols + t] = int16_t(rvwg::kNoSlot | inj);
+  }
   // xcd_tiles: consecutive workgroups go to the 8 XCDs in turn; renumbered, each XCD takes one
   // contiguous run of rows, so the compact lines that neighbouring row tiles share stay in its L2
   // (po2 20 loop guest: 0.71 -> 0.68 ms, profiles/r4v_witgen_merge_ab.txt)
@@ -138,21 +145,74 @@ __global__ __launch_bounds__(kMergeThreads) void merge_kernel(uint32_t* data, ui
     msk[w][threadIdx.x] = stepped && 32 * w < ns ? cb[size_t(ns + w) * n + i] : 0u;
   __syncthreads();
   if (r >= rows) return;
-  const int16_t* sl = slot + arm * rvwg::kDataCols;
+  const int16_t* sl = slot + (stepped ? arm : rvwg::kMajors) * rvwg::kDataCols;
 #pragma unroll 8
   for (uint32_t col = 0; col < rvwg::kDataCols; col++) {
-    const uint32_t e = stepped ? uint32_t(sl[col]) : uint32_t(rvwg::kNoSlot | rvwg::kInjectedCol);
+    const uint32_t e = uint32_t(sl[col]);
     const uint32_t slot = e & rvwg::kNoSlot;
     uint32_t* p = data + uint64_t(col) * rows + r;
     const bool stored = slot != rvwg::kNoSlot && ((msk[slot >> 5][threadIdx.x] >> (slot & 31)) & 1u);
-    uint32_t v = stored ? cb[size_t(slot) * n + i] : rvwg::kInvalid;
-    if (v == rvwg::kInvalid && (!prover || (e & rvwg::kInjectedCol))) v = *p;
+    // the stored value and the data word the row keeps otherwise, loaded side by side (the
+    // read-back no longer waits on the compact load's result)
+    const uint32_t c = stored ? cb[size_t(slot) * n + i] : rvwg::kInvalid;
+    const uint32_t d = !prover || (e & rvwg::kInjectedCol) ? *p : rvwg::kInvalid;
+    uint32_t v = c != rvwg::kInvalid ? c : d;
     if (prover && v == rvwg::kInvalid) v = 0u;
     *p = v;
   }
 }
 
+// one lane per row: the injected columns INVALID, the row's injector entries, code and accum 0
+struct InjectedCols {
+  uint32_t n;
+  uint8_t col[rvwg::kDataCols];
+};
+__global__ __launch_bounds__(kMergeThreads) void prover_groups_init_kernel(
+    uint32_t* data, uint32_t* code, uint32_t* accum, uint32_t rows, uint32_t accum_cols, InjectedCols U,
+    const uint32_t* index, const uint32_t* offsets, const uint32_t* values, uint32_t inj_rows, uint64_t limit,
+    uint32_t acc_inv_begin, uint32_t acc_inv_end) {
+  const uint32_t r = blockIdx.x * kMergeThreads + threadIdx.x;
+  if (r >= rows) return;
+  for (uint32_t k = 0; k < U.n; k++) data[uint64_t(U.col[k]) * rows + r] = rvwg::kInvalid;
+  code[r] = 0u;
+  for (uint32_t c = 0; c < accum_cols; c++)
+    accum[uint64_t(c) * rows + r] = c >= acc_inv_begin && c < acc_inv_end ? rvwg::kInvalid : 0u;
+  if (r < inj_rows) {
+    const uint32_t end = min(index[r + 1], index[inj_rows]);
+    for (uint32_t i = index[r]; i < end; i++)
+      if (offsets[i] < limit) data[offsets[i]] = values[i];
+  }
+}
+
 }  // namespace
+
+void rv32im_prover_groups_init(hipStream_t s, uint32_t* data, uint32_t* code, uint32_t* accum, size_t rows,
+                               size_t accum_cols, const uint32_t* index, const uint32_t* offsets,
+                               const uint32_t* values, size_t inj_rows, uint64_t limit) {
+  using namespace rvwg;
+  R0_REQUIRE(rows <= (size_t(1) << 24) && inj_rows <= rows, "rv32im_prover_groups_init: bad shape");
+  // accum: the machine columns phase 3 adds the previous row's totals to (kUserAccumSplit = 23 up
+  // to the last group, rv32im-sys/kernels/cxx/ffi.cpp:341-356) stay INVALID as the reference
+  // leaves the cells stepAccum does not write (INVALID + total is what it stores there); every
+  // other accum cell is written by the step or is INVALID only to be zeroized, so it starts 0
+  R0_REQUIRE(accum_cols == 103, "rv32im_prover_groups_init: the rv32im accum group has 103 columns");
+  const uint32_t acc_inv_begin = 23, acc_inv_end = 23 + 4 * ((103 - 23) / 4 - 1);
+  static const InjectedCols U = [] {
+    InjectedCols u{};
+    const int16_t* t = rv32im_witgen_slot_table();
+    for (uint32_t c = 0; c < kDataCols; c++) {
+      bool inj = false;
+      for (uint32_t k = 0; k < kMajors; k++) inj |= (uint32_t(t[k * kDataCols + c]) & kInjectedCol) != 0;
+      if (inj) u.col[u.n++] = uint8_t(c);
+    }
+    return u;
+  }();
+  KScope ks("rv32im_groups_init", double(rows) * 4.0 * (U.n + 1 + accum_cols));
+  hipLaunchKernelGGL(prover_groups_init_kernel, dim3(uint32_t((rows + kMergeThreads - 1) / kMergeThreads)),
+                     dim3(kMergeThreads), 0, s, data, code, accum, uint32_t(rows), uint32_t(accum_cols), U, index,
+                     offsets, values, uint32_t(inj_rows), limit, acc_inv_begin, acc_inv_end);
+  HIP_OK(hipGetLastError());
+}
 
 void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
                        const rvwg::PreflightCycle* d_cycles, const rvwg::MemoryTxn* d_txns, size_t n_txns,

@@ -378,11 +378,102 @@ def mat_config(circuit, budget):
     return [int(v) for v in t.get("mat", [])]
 
 
+def resplit_config(circuit, budget):
+    """Kernels re-packed at a smaller cost budget after the schedule: {kernel: budget} from
+    EC_RESPLIT ("5:2000,9:2500") or the tuning file's "resplit", with per-piece tuning
+    overrides ("resplit_tune": {"5.1": {"waves": 3}}). A re-split kernel's pieces keep its
+    tuning unless overridden; they carry fewer live values per lane, so they can run more waves
+    per SIMD (the kernels whose issue stalls follow their register budget)."""
+    spec = os.environ.get("EC_RESPLIT")
+    over = {}
+    if spec is None:
+        path = os.path.join(ROOT, "risc0_amd", "circuits", circuit + ".ectune.json")
+        if not os.path.exists(path):
+            return {}, {}
+        import json
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("budget") != budget:
+            return {}, {}
+        return {int(k): int(v) for k, v in t.get("resplit", {}).items()}, t.get("resplit_tune", {})
+    out = {}
+    for part in filter(None, spec.split(",")):
+        k, b = part.split(":")
+        out[int(k)] = int(b)
+    for part in filter(None, os.environ.get("EC_RESPLIT_WAVES", "").split(",")):
+        k, w = part.split(":")  # "5.1:3"
+        over[k] = {"waves": int(w)}
+    return out, over
+
+
+def split_terms(pg, items, budget):
+    """the linear split of schedule() step 1 applied again to one kernel's terms, down to
+    `budget`: an accumulation term ACC + T*pm (or ACC + T*U*pm) becomes ACC's term and T's term
+    with the extra factor, so each piece's cone is smaller (its pieces then recompute what
+    they share)"""
+    byid = pg.byid
+    out = []
+    for it in items:
+        if it[2] != "term":
+            out.append(it)
+            continue
+        pieces = [it[3]]
+        while True:
+            best, bestc = None, -1
+            for i, t in enumerate(pieces):
+                if byid[t[0]][0] in "ab":
+                    c = pg.cone_cost(term_roots(t))
+                    if c > bestc:
+                        best, bestc = i, c
+            if best is None or bestc <= budget:
+                break
+            e, f = pieces[best]
+            ins = byid[e]
+            if ins[0] == "a":
+                new = [(ins[2], f), (ins[3], f + [("pm", ins[4])])]
+            else:
+                T, U = ins[3], ins[4]
+                if byid[U][0] in "ab" and byid[T][0] not in "ab":
+                    T, U = U, T
+                new = [(ins[2], f), (T, f + [("v", U), ("pm", ins[5])])]
+            pieces[best:best + 1] = new
+        out += [(it[0], it[1], "term", t) for t in pieces]
+    return out
+
+
+def repack(pg, items, budget):
+    """one kernel's items (in dependency order) greedily packed again under `budget`"""
+    items = split_terms(pg, items, budget)
+    out, cur, cur_roots = [], [], []
+    for it in items:
+        roots = [it[3]] if it[2] == "mat" else term_roots(it[3])
+        if cur and pg.cone_cost(cur_roots + roots) > budget:
+            out.append(cur)
+            cur, cur_roots = [], []
+        cur.append(it)
+        cur_roots += roots
+    if cur:
+        out.append(cur)
+    return out
+
+
 def emit(circuit, outdir, budget, host=False):
     pg = Program(circuit)
     pg.mat = set(mat_config(circuit, budget))
     terms, kernels = schedule(pg, budget)
-    tune = kernel_config(circuit, budget)
+    tune0 = kernel_config(circuit, budget)
+    resplit, piece_tune = resplit_config(circuit, budget)
+    tune = {}
+    split_kernels = []
+    for k, items in enumerate(kernels):
+        pieces = repack(pg, items, resplit[k]) if k in resplit else [items]
+        for j, piece in enumerate(pieces):
+            t = dict(tune0.get(k, {}))
+            if len(pieces) > 1:
+                t.update(piece_tune.get(f"{k}.{j}", {}))
+            tune[len(split_kernels)] = t
+            split_kernels.append(piece)
+    kernels = split_kernels
     prog, types = pg.prog, pg.types
     nargs = 1 + max(ins[2] for ins in prog if ins[0] in ("l", "g"))
     npm = max([ins[4] for ins in prog if ins[0] == "a"] + [ins[5] for ins in prog if ins[0] == "b"]) + 1
