@@ -338,30 +338,42 @@ std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const 
   DevBuf code(c->group_size(1) * n), data(data_cols * n), global(c->output_size), accum(c->group_size(0) * n);
   // the groups as WitnessGenerator::new / ::accum allocate them (INVALID), already zeroized where
   // nothing reads INVALID, with the injector scattered in: one pass (rv32im_prover_groups_init)
+  const uint32_t *idx = inj_index, *off = inj_offsets, *val = inj_values;
+  const rvwg::PreflightCycle* cyc = static_cast<const rvwg::PreflightCycle*>(pf->cycles);
+  const rvwg::MemoryTxn* txn = static_cast<const rvwg::MemoryTxn*>(pf->txns);
+  const uint8_t* big = pf->bigint_bytes;
   if (resident) {
     if (inputs_ready) inputs_ready(s);
     HIP_OK(hipMemcpyAsync(global.p, global_in, global.words * 4, hipMemcpyDeviceToDevice, s));
-    rv32im_prover_groups_init(s, data.p, code.p, accum.p, n, c->group_size(0), inj_index, inj_offsets, inj_values,
-                              inj_rows, data.words);
-    Span w("witgen");
-    rv32im_witgen_dev(s, mode, data.p, global.p, n, static_cast<const rvwg::PreflightCycle*>(pf->cycles),
-                      static_cast<const rvwg::MemoryTxn*>(pf->txns), pf->txns_len, pf->bigint_bytes,
-                      pf->bigint_bytes_len, pf->table_split_cycle, uint32_t(n), true);
   } else {
+    R0_REQUIRE((pf->txns_len == 0 || pf->txns) && (pf->bigint_bytes_len == 0 || pf->bigint_bytes),
+               "r0hip_prove_segment_trace: null trace array with a nonzero count");
     check_injector(inj_index, inj_rows, inj_offsets, inj_values, data_cols * n);
     const size_t n_inj = inj_index[inj_rows];
     upload_async(global.p, global_in, global.words * 4);
-    auto* idx = static_cast<uint32_t*>(scratch((inj_rows + 1) * 4, kSlotRvInjIndex));
-    auto* off = static_cast<uint32_t*>(scratch(n_inj * 4 + 4, kSlotRvInjOffsets));
-    auto* val = static_cast<uint32_t*>(scratch(n_inj * 4 + 4, kSlotRvInjValues));
-    upload_async(idx, inj_index, (inj_rows + 1) * 4);
-    upload_async(off, inj_offsets, n_inj * 4);
-    upload_async(val, inj_values, n_inj * 4);
-    rv32im_prover_groups_init(s, data.p, code.p, accum.p, n, c->group_size(0), idx, off, val, inj_rows, data.words);
+    auto* d_idx = static_cast<uint32_t*>(scratch((inj_rows + 1) * 4, kSlotRvInjIndex));
+    auto* d_off = static_cast<uint32_t*>(scratch(n_inj * 4 + 4, kSlotRvInjOffsets));
+    auto* d_val = static_cast<uint32_t*>(scratch(n_inj * 4 + 4, kSlotRvInjValues));
+    upload_async(d_idx, inj_index, (inj_rows + 1) * 4);
+    upload_async(d_off, inj_offsets, n_inj * 4);
+    upload_async(d_val, inj_values, n_inj * 4);
+    idx = d_idx, off = d_off, val = d_val;
+    cyc = rv32im_upload_cycles(cyc, n);
+    auto* d_txn = static_cast<rvwg::MemoryTxn*>(scratch(size_t(pf->txns_len) * sizeof(rvwg::MemoryTxn) + 16, kSlotRvwgTxns));
+    auto* d_big = static_cast<uint8_t*>(scratch(size_t(pf->bigint_bytes_len) + 16, kSlotRvwgBigint));
+    upload_async(d_txn, pf->txns, size_t(pf->txns_len) * sizeof(rvwg::MemoryTxn));
+    upload_async(d_big, pf->bigint_bytes, pf->bigint_bytes_len);
+    txn = pf->txns_len ? d_txn : nullptr;
+    big = pf->bigint_bytes_len ? d_big : nullptr;
+  }
+  auto* ierr = static_cast<uint32_t*>(scratch(16, kSlotRvInitErr));
+  HIP_OK(hipMemsetD32Async(ierr, 0u, 4, s));
+  rv32im_prover_groups_init(s, data.p, code.p, accum.p, n, c->group_size(0), idx, off, val, inj_rows, data.words, cyc,
+                            ierr);
+  {
     Span w("witgen");
-    rv32im_witgen(s, mode, data.p, global.p, n, static_cast<const rvwg::PreflightCycle*>(pf->cycles),
-                  static_cast<const rvwg::MemoryTxn*>(pf->txns), pf->txns_len, pf->bigint_bytes, pf->bigint_bytes_len,
-                  pf->table_split_cycle, uint32_t(n), true);
+    rv32im_witgen_dev(s, mode, data.p, global.p, n, cyc, txn, pf->txns_len, big, pf->bigint_bytes_len,
+                      pf->table_split_cycle, uint32_t(n), true, ierr);
   }
   eltwise_zeroize(s, global.p, global.words);  // the data group was zeroized by the witgen merge
   AccumStep acc{accum.p, n, false, h_bigint, n_bigint};

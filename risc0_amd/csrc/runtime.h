@@ -113,6 +113,7 @@ enum ScratchSlot : int {
   kSlotRvInjIndex = 80,
   kSlotRvInjOffsets = 81,
   kSlotRvInjValues = 82,
+  kSlotRvInitErr = 87,
 };
 
 // Scratch buffer reused across calls (grown on demand; stream-ordered use only).

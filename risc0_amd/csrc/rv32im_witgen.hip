@@ -54,6 +54,9 @@ std::string witgen_error(const uint32_t* e) {
     case kErrBigint: return "bigint bytes past the preflight's" + at;
     case kErrDiffCount: return "getDiffCount past the preflight's cycles" + at;
     case kErrMajor: return "cycle major " + std::to_string(detail) + " selects no instruction arm" + at;
+    case kErrInjectorCol:
+      return "injector sets col " + std::to_string(detail) + ", which this row's instruction arm does not take from "
+             "the injector" + at;
     default: return "witness generation error " + std::to_string(code) + at;
   }
 }
@@ -114,7 +117,7 @@ __global__ __launch_bounds__(kBucketThreads) void bin_pos_kernel(const uint32_t*
 __global__ __launch_bounds__(kMergeThreads) void merge_kernel(uint32_t* data, uint32_t rows, uint32_t ncycles,
                                                              const uint32_t* cbuf, const uint8_t* keys,
                                                              const uint32_t* pos, const int16_t* slot_of, BinTable T,
-                                                             bool prover, bool xcd_tiles) {
+                                                             bool prover, bool xcd_tiles, uint32_t* err) {
   constexpr uint32_t kMaskWords = (rvwg::kDataCols + 31) / 32;
   __shared__ int16_t slot[(rvwg::kMajors + 1) * rvwg::kDataCols];
   __shared__ uint32_t msk[kMaskWords][kMergeThreads];  // this thread's row: its arm's stored-slot bits
@@ -156,6 +159,12 @@ __global__ __launch_bounds__(kMergeThreads) void merge_kernel(uint32_t* data, ui
     // read-back no longer waits on the compact load's result)
     const uint32_t c = stored ? cb[size_t(slot) * n + i] : rvwg::kInvalid;
     const uint32_t d = !prover || (e & rvwg::kInjectedCol) ? *p : rvwg::kInvalid;
+    // the caller's data group (the public witgen) holds a word the arm does not take from the
+    // injector: the arms never read or checked it (the prover's injector is checked at init)
+    if (!prover && stepped && !(e & rvwg::kInjectedCol) && d != rvwg::kInvalid && atomicCAS(err, 0u, rvwg::kErrInjectorCol) == 0u) {
+      err[1] = r;
+      err[2] = col;
+    }
     uint32_t v = c != rvwg::kInvalid ? c : d;
     if (prover && v == rvwg::kInvalid) v = 0u;
     *p = v;
@@ -166,11 +175,13 @@ __global__ __launch_bounds__(kMergeThreads) void merge_kernel(uint32_t* data, ui
 struct InjectedCols {
   uint32_t n;
   uint8_t col[rvwg::kDataCols];
+  uint32_t arm_mask[rvwg::kMajors][(rvwg::kDataCols + 31) / 32];  // kInjectedCol per arm, as bits
 };
 __global__ __launch_bounds__(kMergeThreads) void prover_groups_init_kernel(
     uint32_t* data, uint32_t* code, uint32_t* accum, uint32_t rows, uint32_t accum_cols, InjectedCols U,
     const uint32_t* index, const uint32_t* offsets, const uint32_t* values, uint32_t inj_rows, uint64_t limit,
-    uint32_t acc_inv_begin, uint32_t acc_inv_end) {
+    uint32_t acc_inv_begin, uint32_t acc_inv_end, const rvwg::PreflightCycle* cycles, uint32_t row_shift,
+    uint32_t* err) {
   const uint32_t r = blockIdx.x * kMergeThreads + threadIdx.x;
   if (r >= rows) return;
   for (uint32_t k = 0; k < U.n; k++) data[uint64_t(U.col[k]) * rows + r] = rvwg::kInvalid;
@@ -179,8 +190,18 @@ __global__ __launch_bounds__(kMergeThreads) void prover_groups_init_kernel(
     accum[uint64_t(c) * rows + r] = c >= acc_inv_begin && c < acc_inv_end ? rvwg::kInvalid : 0u;
   if (r < inj_rows) {
     const uint32_t end = min(index[r + 1], index[inj_rows]);
-    for (uint32_t i = index[r]; i < end; i++)
-      if (offsets[i] < limit) data[offsets[i]] = values[i];
+    const uint32_t arm = cycles[r].major;  // a major past the arms fails in the bucket kernel
+    for (uint32_t i = index[r]; i < end; i++) {
+      const uint32_t off = offsets[i];
+      if (off >= limit) continue;
+      data[off] = values[i];
+      const uint32_t col = off >> row_shift;
+      if (arm < rvwg::kMajors && !((U.arm_mask[arm][col >> 5] >> (col & 31)) & 1u) &&
+          atomicCAS(err, 0u, rvwg::kErrInjectorCol) == 0u) {
+        err[1] = r;
+        err[2] = col;
+      }
+    }
   }
 }
 
@@ -188,9 +209,11 @@ __global__ __launch_bounds__(kMergeThreads) void prover_groups_init_kernel(
 
 void rv32im_prover_groups_init(hipStream_t s, uint32_t* data, uint32_t* code, uint32_t* accum, size_t rows,
                                size_t accum_cols, const uint32_t* index, const uint32_t* offsets,
-                               const uint32_t* values, size_t inj_rows, uint64_t limit) {
+                               const uint32_t* values, size_t inj_rows, uint64_t limit,
+                               const rvwg::PreflightCycle* d_cycles, uint32_t* err) {
   using namespace rvwg;
-  R0_REQUIRE(rows <= (size_t(1) << 24) && inj_rows <= rows, "rv32im_prover_groups_init: bad shape");
+  R0_REQUIRE(rows >= 4 && rows <= (size_t(1) << 24) && (rows & (rows - 1)) == 0 && inj_rows <= rows,
+             "rv32im_prover_groups_init: bad shape");
   // accum: the machine columns phase 3 adds the previous row's totals to (kUserAccumSplit = 23 up
   // to the last group, rv32im-sys/kernels/cxx/ffi.cpp:341-356) stay INVALID as the reference
   // leaves the cells stepAccum does not write (INVALID + total is what it stores there); every
@@ -202,7 +225,11 @@ void rv32im_prover_groups_init(hipStream_t s, uint32_t* data, uint32_t* code, ui
     const int16_t* t = rv32im_witgen_slot_table();
     for (uint32_t c = 0; c < kDataCols; c++) {
       bool inj = false;
-      for (uint32_t k = 0; k < kMajors; k++) inj |= (uint32_t(t[k * kDataCols + c]) & kInjectedCol) != 0;
+      for (uint32_t k = 0; k < kMajors; k++)
+        if (uint32_t(t[k * kDataCols + c]) & kInjectedCol) {
+          inj = true;
+          u.arm_mask[k][c >> 5] |= 1u << (c & 31);
+        }
       if (inj) u.col[u.n++] = uint8_t(c);
     }
     return u;
@@ -210,14 +237,15 @@ void rv32im_prover_groups_init(hipStream_t s, uint32_t* data, uint32_t* code, ui
   KScope ks("rv32im_groups_init", double(rows) * 4.0 * (U.n + 1 + accum_cols));
   hipLaunchKernelGGL(prover_groups_init_kernel, dim3(uint32_t((rows + kMergeThreads - 1) / kMergeThreads)),
                      dim3(kMergeThreads), 0, s, data, code, accum, uint32_t(rows), uint32_t(accum_cols), U, index,
-                     offsets, values, uint32_t(inj_rows), limit, acc_inv_begin, acc_inv_end);
+                     offsets, values, uint32_t(inj_rows), limit, acc_inv_begin, acc_inv_end, d_cycles,
+                     uint32_t(__builtin_ctzll(rows)), err);
   HIP_OK(hipGetLastError());
 }
 
 void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
                        const rvwg::PreflightCycle* d_cycles, const rvwg::MemoryTxn* d_txns, size_t n_txns,
                        const uint8_t* d_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle,
-                       bool zeroize) {
+                       bool zeroize, const uint32_t* extra_err) {
   using namespace rvwg;
   R0_REQUIRE(mode <= 2, "rv32im_witgen: mode must be 0 (parallel), 1 (forward) or 2 (reverse)");
   R0_REQUIRE(rows >= 4 && (rows & (rows - 1)) == 0 && rows <= (size_t(1) << 24),
@@ -322,18 +350,27 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
     upload_async(d_slot, rv32im_witgen_slot_table(), slot_bytes);
     KScope ks("rv32im_witgen_merge", double(rows) * kDataCols * 8.0 + double(cwords) * 4.0);
     hipLaunchKernelGGL(merge_kernel, dim3(uint32_t((rows + kMergeThreads - 1) / kMergeThreads)), dim3(kMergeThreads), 0,
-                       s, data, uint32_t(rows), last_cycle, cbuf, keys, pos, d_slot, T, zeroize, merge_xcd);
+                       s, data, uint32_t(rows), last_cycle, cbuf, keys, pos, d_slot, T, zeroize, merge_xcd, A.err);
     HIP_OK(hipGetLastError());
   }
-  uint32_t h_err[3] = {0, 0, 0};
+  uint32_t h_err[3] = {0, 0, 0}, h_extra[3] = {0, 0, 0};
   HIP_OK(hipMemcpyAsync(h_err, A.err, 12, hipMemcpyDeviceToHost, s));
+  if (extra_err) HIP_OK(hipMemcpyAsync(h_extra, extra_err, 12, hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
+  R0_REQUIRE(h_extra[0] == 0, "rv32im witgen: " + witgen_error(h_extra));
   R0_REQUIRE(h_err[0] == 0, "rv32im witgen: " + witgen_error(h_err));
+}
+
+const rvwg::PreflightCycle* rv32im_upload_cycles(const rvwg::PreflightCycle* h_cycles, size_t n) {
+  auto* d = static_cast<rvwg::PreflightCycle*>(scratch(n * sizeof(rvwg::PreflightCycle) + 16, kSlotRvwgCycles));
+  upload_async(d, h_cycles, n * sizeof(rvwg::PreflightCycle));
+  return d;
 }
 
 void rv32im_witgen(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
                    const rvwg::PreflightCycle* h_cycles, const rvwg::MemoryTxn* h_txns, size_t n_txns,
-                   const uint8_t* h_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle, bool zeroize) {
+                   const uint8_t* h_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle, bool zeroize,
+                   const uint32_t* extra_err) {
   using namespace rvwg;
   R0_REQUIRE(last_cycle <= rows && last_cycle <= (size_t(1) << 24), "rv32im_witgen: more cycles than rows");
   R0_REQUIRE((last_cycle == 0 || h_cycles) && (n_txns == 0 || h_txns) && (n_bigint == 0 || h_bigint),
@@ -345,7 +382,7 @@ void rv32im_witgen(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* globa
   upload_async(d_txns, h_txns, n_txns * sizeof(MemoryTxn));
   upload_async(d_bigint, h_bigint, n_bigint);
   rv32im_witgen_dev(s, mode, data, global, rows, d_cycles, n_txns ? d_txns : nullptr, n_txns,
-                    n_bigint ? d_bigint : nullptr, n_bigint, table_split, last_cycle, zeroize);
+                    n_bigint ? d_bigint : nullptr, n_bigint, table_split, last_cycle, zeroize, extra_err);
 }
 
 }  // namespace r0

@@ -325,3 +325,31 @@ def test_loop_s_trace_po2_24_proves_and_verifies(hal):
     del job
     assert r.verify_seal("rv32im", hal.suite, seal, check_validity=True) == 24
     r.trim()
+
+
+def test_injector_outside_the_arms_columns_fails(hal):
+    """the generated arms take each arm's injected columns from the injector: an
+    injected word in a column the row's arm does not take — which the reference would read or
+    check — is refused, in the prover's init pass and in the public witgen's merge, and the
+    next call is clean"""
+    import risc0_amd as r
+    t = T.loop_s_trace(14, 200, seed=5)
+    cyc, tx = t.arrays()
+    lay = W.layout()
+    rows = 1 << 14
+    row = int(np.flatnonzero((cyc["state"] == T.DECODE) & (cyc["major"] == 0))[5])
+    col = lay["sha2_u32"][0]
+    idx, off, val = W.injector_arrays(t)
+    at = int(idx[row + 1])  # one more entry at the end of the row
+    off2 = np.insert(off, at, col * rows + row)
+    val2 = np.insert(val, at, W.encode(1))
+    idx2 = idx.copy()
+    idx2[row + 1:] += 1
+    with pytest.raises(r.R0HipError, match=f"injector sets col {col}"):
+        r.prove_segment_trace(hal, 14, W.global_words(t), idx2, off2, val2, cyc, tx, t.table_split_cycle)
+    data, glob, _, _ = W.inputs(t)
+    data[col * rows + row] = W.encode(1)
+    with pytest.raises(r.R0HipError, match=f"injector sets col {col}"):
+        gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle)
+    seal, _ = r.prove_segment_trace(hal, 14, W.global_words(t), idx, off, val, cyc, tx, t.table_split_cycle)
+    assert r.verify_seal("rv32im", hal.suite, seal, check_validity=True) == 14
