@@ -442,19 +442,23 @@ def split_terms(pg, items, budget):
 
 
 def repack(pg, items, budget):
-    """one kernel's items (in dependency order) greedily packed again under `budget`"""
+    """one kernel's items split (split_terms) and packed again under `budget`, first fit in
+    decreasing cone cost: the items of one kernel are independent of each other (what they
+    read was materialised by earlier kernels), so any grouping keeps the schedule valid"""
     items = split_terms(pg, items, budget)
-    out, cur, cur_roots = [], [], []
+    roots = lambda it: [it[3]] if it[2] == "mat" else term_roots(it[3])
+    items.sort(key=lambda it: -pg.cone_cost(roots(it)))
+    bins = []  # [items, roots]
     for it in items:
-        roots = [it[3]] if it[2] == "mat" else term_roots(it[3])
-        if cur and pg.cone_cost(cur_roots + roots) > budget:
-            out.append(cur)
-            cur, cur_roots = [], []
-        cur.append(it)
-        cur_roots += roots
-    if cur:
-        out.append(cur)
-    return out
+        r = roots(it)
+        for b in bins:
+            if pg.cone_cost(b[1] + r) <= budget:
+                b[0].append(it)
+                b[1] += r
+                break
+        else:
+            bins.append([[it], list(r)])
+    return [sorted(b[0], key=lambda it: (it[0], it[1])) for b in bins]
 
 
 def emit(circuit, outdir, budget, host=False):
