@@ -125,7 +125,10 @@ void drain_after_error() noexcept;
 
 // Stream-ordered host->device upload through a pinned bump arena, so the caller's
 // host data may die immediately. The arena is recycled by stage_reset() (call only
-// when the stream is idle).
+// when the stream is idle). Exception: a source of 64 KiB or more inside a live
+// r0hip_host_alloc block is copied to the device directly, with no staging, so it must
+// stay valid until the copy has run. Rule for every entry point that takes host arrays:
+// drain this thread's stream (or stage_reset) before returning to the caller.
 void upload_async(void* d_dst, const void* h_src, size_t bytes);
 void stage_reset();
 
