@@ -34,8 +34,10 @@ P = 15 * 2**27 + 1
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=6)  # a multiple of the segments in flight
-    ap.add_argument("--warmup", type=int, default=2)
+    # a multiple of the segments in flight; enough segments that the pipeline's fill and drain
+    # (the first trace's upload, the last segments finishing alone) are a small share
+    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--po2", type=int, default=20)
     ap.add_argument("--circuit", default="rv32im")
     ap.add_argument("--hashfn", default="poseidon2")

@@ -192,10 +192,11 @@ class Preflight:
         elif g(SEL["p2_full"]) == 1:
             safe = False
         elif g(SEL["p2_partial"]) == 1:
-            import oracle
-            cells = np.array([enc(x) for x in self.p2], np.uint32)
-            oracle.poseidon2_mix(cells)
-            self.p2 = [dec(x) for x in cells]
+            # the whole permutation at the partial-round row, on plain integers (the restated
+            # Poseidon2 of tests/rv32im_trace.py, pinned there to the oracle's constants), so a
+            # program's preflight needs nothing under oracle/ (bench.py builds them)
+            import rv32im_trace
+            self.p2 = rv32im_trace.permute(self.p2)
             safe = False
         elif g(SEL["p2_store"]) == 1:
             do_mont = g(8)

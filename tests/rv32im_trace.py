@@ -340,6 +340,17 @@ def ancestors(node):
     return out
 
 
+def permute(s):
+    """the Poseidon2 permutation on 24 plain integers (mod.rs:102-216)"""
+    s = _m_ext(list(s))
+    for i in range(ROUNDS_HALF_FULL):
+        s = _ext_round(s, i)
+    s = _int_rounds(s)
+    for i in range(ROUNDS_HALF_FULL, 2 * ROUNDS_HALF_FULL):
+        s = _ext_round(s, i)
+    return s
+
+
 def node_hash(d_hi, d_lo):
     """a node's digest from its children (rest() with is_elem = 1, count = 1: children
     2n+1 then 2n)"""

@@ -6,9 +6,10 @@ TAG=$1; R=${2:-$TAG}
 O=gpurun_out/$TAG
 cd "$(dirname "$0")/.."
 f() { find $O/$1 -name "$2" | head -1; }
-# proofs per profiled run (tools/gpu_round.sh, round-5 bench): stats 11 (2 pipeline warmup + 6 timed
-# trace jobs, 1 unpipelined, 2 roofline launches), PMC runs 8 (2 + 3 + 1 + 2); round 4: 10 and 6
-NS=${3:-11}; NP=${4:-8}
+# proofs per profiled run (tools/gpu_round.sh, round-5 bench): stats 18 (3 pipeline warmup + 12 timed
+# trace jobs, 1 unpipelined, 2 roofline launches), PMC runs 8 (2 + 3 + 1 + 2); r5c: 11 (6-step
+# default); round 4: 10 and 6
+NS=${3:-18}; NP=${4:-8}
 python3 tools/rocprof_families.py "$(f stats '*kernel_stats.csv')" $NS > profiles/${R}_rocprof_families.txt
 cp "$(f stats '*kernel_stats.csv')" profiles/${R}_rocprof_kernel_stats.csv
 python3 tools/pmc_summary.py "$(f valu '*counter_collection.csv')" profiles/${R}_pmc_valu.json > profiles/${R}_pmc_valu.txt
