@@ -142,6 +142,11 @@ def main():
     # groups are only read and are shared
     globs = [dg] + [hal.copy_from_elem("global", glob) for _ in range(k - 1)]
     trace_mode = args.circuit == "rv32im" and not args.witness
+    # recursion: a whole proof from the program and its preflight (RecursionProverImpl::prove,
+    # circuit/recursion/src/prove/mod.rs:160-230: witness generation, ZK noise, accumulation,
+    # prove), the lift/join shape with random programs (the lift/join .zkr files are not in the
+    # reference checkout)
+    program_mode = args.circuit == "recursion" and not args.witness
 
     def prove_witness(slot):
         return r.prove_segment(hal, args.circuit, args.po2, dc, dd, da, globs[slot], version=version)
@@ -183,6 +188,24 @@ def main():
         print(f"rank {rank}: {len(traces)} {args.guest} traces built in {time.perf_counter() - t0:.1f} s (trace 0: "
               f"{trace.table_split_cycle} rows before the tables, {len(trace.arrays()[1])} memory transactions, "
               f"{tjobs[0].h2d_bytes() / 1e6:.0f} MB to upload)", file=sys.stderr)
+
+    progs = []
+    if program_mode:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import recursion_program as RP  # restated recursion preflight (test infrastructure, no oracle)
+        nprog = args.traces if args.traces is not None else 2
+        t0 = time.perf_counter()
+        n = 1 << args.po2
+        for i in range(max(1, nprog)):
+            prng = np.random.default_rng(0x5249534330 + 64 * rank + i)
+            prog, inp = RP.random_program(prng, n - RP.ZK_CYCLES - 1)
+            pf = RP.preflight(prog, inp)
+            wom, cyc_, iops = RP.trace_arrays(pf)
+            u = lambda a: np.ascontiguousarray(np.asarray(a, dtype=np.uint32).reshape(-1))  # once, not per proof
+            progs.append({"prog": prog, "pf": pf, "ctrl": hal.copy_from_elem("ctrl", RP.ctrl_group(prog, args.po2)),
+                          "wom": u(wom), "cycles": u(cyc_), "iops": u(iops), "seed": 0x5EED + 64 * rank + i})
+        print(f"rank {rank}: {len(progs)} recursion programs built in {time.perf_counter() - t0:.1f} s "
+              f"({len(progs[0]['prog'].rows)} rows in program 0)", file=sys.stderr)
 
     def timed_leg(prove_one, label):
         phase_tot, last = {}, {}
@@ -240,6 +263,18 @@ def main():
                                 "from k host threads): the round-4 headline, no H2D"}
         if not args.no_prove_only:
             t_w, seal_w, _ = timed_leg(prove_witness, "prove_only")
+    elif program_mode:
+        import itertools
+        counter = itertools.count()
+
+        def prove_program(slot, j=None):
+            p = progs[next(counter) % len(progs) if j is None else j]
+            return r.prove_recursion(hal, args.po2, p["ctrl"], p["wom"], p["cycles"], p["iops"], p["seed"])
+        t, _, _ = timed_leg(prove_program, "program")
+        seal, mix = prove_program(0, 0)  # program 0's seal, for the CPU parity check
+        program_valid = r.verify_seal("recursion", hal.suite, seal, check_validity=True) == args.po2
+        if not args.no_prove_only:
+            t_w, seal_w, _ = timed_leg(prove_witness, "prove_only")
     else:
         t, seal, mix = timed_leg(prove_witness, "prove")
     mem = r.mem_stats()  # this rank's device footprint with k segments in flight
@@ -252,7 +287,7 @@ def main():
     value = cycles_total / t
     ms_per_step = 1000.0 * t / args.steps
     prove_only = None
-    if trace_mode and not args.no_prove_only:
+    if (trace_mode or program_mode) and not args.no_prove_only:
         prove_only = {"value": round(cycles_total / t_w, 1), "unit": "cycles/s",
                       "ms_per_step": round(1000.0 * t_w / args.steps, 3),
                       "seal_sha256_rank0": hashlib.sha256(seal_w.tobytes()).hexdigest()[:16],
@@ -266,7 +301,7 @@ def main():
     acc_leg = None
     if rank == 0:
         prove_timed = ((lambda: r.prove_segment_trace_resident(hal, rt, bigint_records=bigint_records)) if trace_mode
-                       else (lambda: prove_witness(0)))
+                       else (lambda: prove_program(0, 0)) if program_mode else (lambda: prove_witness(0)))
         roofline = kernel_roofline(r, args, prove_timed)
         # the side legs keep 2 in flight below po2 21 unless --inflight says otherwise: the
         # pipeline's uploader and a third prover measured slower there (63.1 against 57.6 ms)
@@ -276,7 +311,9 @@ def main():
         if args.accum_steps > 0 and args.circuit == "rv32im" and host_witness is not None:
             acc_leg = with_accumulation(r, hal, args, host_witness, kl, version)
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline_trace(args, trace, seal, mix) if trace_mode else cpu_baseline(args, circ, seal, mix)
+            cpu = (cpu_baseline_trace(args, trace, seal, mix) if trace_mode else
+                   cpu_baseline_program(args, progs[0], seal, mix) if program_mode else
+                   cpu_baseline(args, circ, seal, mix))
     del host_witness
 
     if rank == 0:
@@ -284,6 +321,10 @@ def main():
                     "host memory: upload -> witness generation -> accumulation -> seal on host (the reference's "
                     "prove_core), through the native segment pipeline (r0hip_prove_segments trace jobs)"
                     if trace_mode else
+                    f"recursion segment po2={args.po2}, {args.hashfn} hashfn, from the program (control group resident) "
+                    "and its preflight in host memory: witness generation -> ZK noise -> accumulation -> seal on host "
+                    "(RecursionProverImpl::prove, r0hip_prove_recursion)"
+                    if program_mode else
                     f"{args.circuit} segment po2={args.po2}, {args.hashfn} hashfn, witness resident in HBM -> seal on host")
         if trace_mode and args.guest == "loop_s":
             data = (f"synthetic: the datasheet's loop guest (risc0/zkvm/examples/loop.s under a restated v1compat kernel; "
@@ -294,6 +335,11 @@ def main():
             data = (f"synthetic (a loop guest: random 32-instruction RV32IM body, repeated until the segment suspends; "
                     f"preflight restated from the reference executor, tests/rv32im_trace.py; {len(traces)} distinct "
                     "seeded traces per rank)")
+        elif program_mode:
+            data = (f"synthetic: {len(progs)} random recursion programs per rank (micro ops, Poseidon2 load/partial/"
+                    "store, IOP reads, mix_rng; tests/recursion_program.py with its restated preflight), "
+                    f"{len(progs[0]['prog'].rows)} rows in program 0; the lift/join programs are not in the "
+                    "reference checkout")
         else:
             data = "synthetic (uniform BabyBear witness, seeded per segment)"
         line = {
@@ -318,6 +364,8 @@ def main():
                            "distinct_seals_rank0": seals_distinct,
                            "h2d_bytes_per_segment": int(tjobs[0].h2d_bytes()),
                            "ms_one_segment_unpipelined": round(1000.0 * t_one, 1)} if trace_mode else {}),
+                       **({"programs_per_rank": len(progs), "seal_valid_rank0": bool(program_valid)}
+                          if program_mode else {}),
                        "ranks_share_devices": any(shared[i] for i in range(world))},
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -655,6 +703,64 @@ def cpu_baseline_trace(args, trace, gpu_seal, gpu_mix):
                 "oracle_mix_sha256": dig(cmix), "gpu_mix_sha256": dig(gpu_mix),
                 "parity_note": ("CPU prove_core of rank 0's trace 0 against the GPU seal the timed pipeline proved from "
                                 "that trace" if compare else "po2=20 sample; no parity at the bench's size")}
+    except Exception as e:  # the baseline is reported, never required
+        print(f"cpu baseline failed: {e}", file=sys.stderr)
+        return None
+
+
+def cpu_baseline_program(args, p, gpu_seal, gpu_mix):
+    """The reference's recursion prove path on the host for rank 0's program 0: the compiled
+    reference witness generation (risc0_circuit_recursion_cpu_witgen) and accumulation
+    (risc0_circuit_recursion_cpu_accum) from oracle/_ref, the ZK noise words
+    r0hip_prove_recursion draws (oracle.splitmix_fill of the same seeds), and the CPU oracle
+    prover, on every host core the process may use; seal and mix compared with the GPU's."""
+    try:
+        cores = host_cores()
+        os.environ["ORACLE_THREADS"] = str(cores)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle
+        import accum_ir as A
+        import recursion_program as RP
+        if oracle.ref_lib() is None or not RP.available():
+            return None
+        import hashlib
+        suite = {"poseidon2": oracle.POSEIDON2, "sha-256": oracle.SHA256, "poseidon_254": oracle.POSEIDON254}[args.hashfn]
+        po2, n, zk = args.po2, 1 << args.po2, RP.ZK_CYCLES
+        oracle.op_times(reset=True)
+        t0 = time.perf_counter()
+        ctrl, data, glob = RP.witgen(p["prog"], p["pf"], po2, raw=True)
+        t_wg = time.perf_counter() - t0
+        data = data.reshape(RP.DATA, n)
+        data[:, n - zk:] = oracle.splitmix_fill(p["seed"], RP.DATA * zk).reshape(RP.DATA, zk)
+        data = np.where(data == RP.INVALID, 0, data).astype(np.uint32).reshape(-1)
+        glob = np.where(glob == RP.INVALID, 0, glob).astype(np.uint32)
+        acc0 = np.full((RP.ACCUM, n), RP.INVALID, np.uint32)
+        acc0[:, n - zk:] = oracle.splitmix_fill(p["seed"] + 1, RP.ACCUM * zk).reshape(RP.ACCUM, zk)
+        acc0 = acc0.reshape(-1)
+        acc_s = []
+
+        def fill(mix):
+            ta = time.perf_counter()
+            acc = acc0.copy()
+            A.ref_accum(ctrl, glob, data, mix, acc, len(p["prog"].rows), n)
+            acc[acc == RP.INVALID] = 0
+            acc_s.append(time.perf_counter() - ta)
+            return acc
+        cseal, cmix, _, _ = oracle.prove_segment_cb("recursion", suite, po2, ctrl, data, glob, fill, RP.ACCUM * n)
+        t = time.perf_counter() - t0
+        ops = {"witgen (reference risc0_circuit_recursion_cpu_witgen)": round(t_wg, 3),
+               "accumulate (reference risc0_circuit_recursion_cpu_accum)": round(sum(acc_s), 3)}
+        ops.update({k: round(v[0], 3) for k, v in sorted(oracle.op_times().items(), key=lambda kv: -kv[1][0])})
+        ops["other (noise, zeroize, transcript, openings)"] = round(t - sum(ops.values()), 3)
+        dig = lambda a: hashlib.sha256(np.ascontiguousarray(a, dtype=np.uint32).tobytes()).hexdigest()
+        return {"value": round(n / t, 1), "unit": "cycles/s", "cores": int(oracle.num_threads()), "kind": "port",
+                "sample": f"one recursion segment at po2={po2} ({args.hashfn}) from rank 0's program 0, {t:.1f} s wall: "
+                          "the reference's compiled recursion witgen and accumulation (oracle/_ref) and the oracle prover",
+                "seconds_by_hal_op": ops,
+                "seal_equal": bool(np.array_equal(cseal, gpu_seal)), "mix_equal": bool(np.array_equal(cmix, gpu_mix)),
+                "oracle_seal_sha256": dig(cseal), "gpu_seal_sha256": dig(gpu_seal),
+                "parity_note": "CPU recursion prove of rank 0's program 0 against the GPU seal of the same program"}
     except Exception as e:  # the baseline is reported, never required
         print(f"cpu baseline failed: {e}", file=sys.stderr)
         return None
