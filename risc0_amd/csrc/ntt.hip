@@ -172,20 +172,29 @@ template <int B, int C>
 struct ColTwiddles {
   static constexpr uint32_t LR = 8 - C;  // log2 rows per i
   static constexpr uint32_t E = 1u << (B - LR);
-  uint32_t pw[E];
-  __device__ __forceinline__ void init(const PassArgs& p, uint32_t ex, uint32_t t0) {
+  static constexpr uint32_t S = E < 8 ? E : 8;
+  // f(i, w) for every i < E with w = base * c^k, k = rev_{B-LR}(i), walking k in order: S
+  // running products advance by c^S, so only S twiddles are live at a time (a table of all E
+  // held 32 more VGPRs per lane in the B = 9 column pass: 165 VGPRs, 3 waves per SIMD)
+  template <typename F>
+  __device__ __forceinline__ static void apply(const PassArgs& p, uint32_t ex, uint32_t t0, F&& f) {
     const uint32_t c = fp_mul(p.sc_hi[ex >> p.sc_split], p.sc_lo[ex & ((1u << p.sc_split) - 1)]);
-    constexpr uint32_t S = E < 8 ? E : 8;
-    pw[0] = fp_pow(c, uint64_t(bitrev_n(t0, LR)) << (B - LR));
+    uint32_t cur[S];
+    cur[0] = fp_pow(c, uint64_t(bitrev_n(t0, LR)) << (B - LR));
 #pragma unroll
-    for (uint32_t k = 1; k < S; k++) pw[k] = fp_mul(pw[k - 1], c);
+    for (uint32_t k = 1; k < S; k++) cur[k] = fp_mul(cur[k - 1], c);
     uint32_t step = c;
 #pragma unroll
     for (uint32_t k = 1; k < S; k <<= 1) step = fp_mul(step, step);  // c^S
 #pragma unroll
-    for (uint32_t k = S; k < E; k++) pw[k] = fp_mul(pw[k - S], step);
+    for (uint32_t k0 = 0; k0 < E; k0 += S) {
+#pragma unroll
+      for (uint32_t s = 0; s < S; s++) {
+        f(bitrev_n(k0 + s, B - LR), cur[s]);
+        if (k0 + S < E) cur[s] = fp_mul(cur[s], step);
+      }
+    }
   }
-  __device__ __forceinline__ uint32_t at(uint32_t i) const { return pw[bitrev_n(i, B - LR)]; }
 };
 
 // Column passes with 2^C < 32 columns cover half an L2 line per workgroup. Consecutive
@@ -274,16 +283,14 @@ __global__ __launch_bounds__(NT) void ntt_pass_kernel(PassArgs p) {
     constexpr uint32_t E = total / NT;
     constexpr uint32_t R = NT >> C;  // rows per i
     const uint32_t j = tid & ((1u << C) - 1), t0 = tid >> C;
+    // a uniform base and 32-bit byte offsets (a pass spans 2^(a+B) <= 2^L words): saddr-form
+    // loads, one VGPR of offset per load instead of a 64-bit address pair
+    const char* cbase = reinterpret_cast<const char*>(p.in + (g_hi << (p.a + B)) + low0);
+    const uint32_t off0 = ((t0 << p.a) + j) * 4u, ostep = (R << p.a) * 4u;
     uint32_t r[E];
 #pragma unroll
-    for (uint32_t i = 0; i < E; i++)
-      r[i] = p.in[(g_hi << (p.a + B)) + (uint64_t(R * i + t0) << p.a) + low0 + j];
-    if (!INV) {
-      ColTwiddles<B, C> tf;
-      tf.init(p, low0 + j, t0);
-#pragma unroll
-      for (uint32_t i = 0; i < E; i++) r[i] = fp_mul(r[i], tf.at(i));
-    }
+    for (uint32_t i = 0; i < E; i++) r[i] = *reinterpret_cast<const uint32_t*>(cbase + (off0 + i * ostep));
+    if (!INV) ColTwiddles<B, C>::apply(p, low0 + j, t0, [&](uint32_t i, uint32_t w) { r[i] = fp_mul(r[i], w); });
 #pragma unroll
     for (uint32_t i = 0; i < E; i++) lds[lidx<COLS, B, C>(j, R * i + t0)] = r[i];
   }
@@ -295,14 +302,16 @@ __global__ __launch_bounds__(NT) void ntt_pass_kernel(PassArgs p) {
     constexpr uint32_t E = total / NT;
     constexpr uint32_t R = NT >> C;
     const uint32_t j = tid & ((1u << C) - 1), t0 = tid >> C;
-    ColTwiddles<B, C> tf;
-    if (INV) tf.init(p, low0 + j, t0);
+    char* obase = reinterpret_cast<char*>(p.out + (g_hi << (p.a + B)) + low0);
+    const uint32_t off0 = ((t0 << p.a) + j) * 4u, ostep = (R << p.a) * 4u;
+    auto put = [&](uint32_t i, uint32_t v) { *reinterpret_cast<uint32_t*>(obase + (off0 + i * ostep)) = v; };
+    if (INV) {
+      ColTwiddles<B, C>::apply(p, low0 + j, t0, [&](uint32_t i, uint32_t w) {
+        put(i, fp_mul(lds[lidx<COLS, B, C>(j, R * i + t0)], w));
+      });
+    } else {
 #pragma unroll
-    for (uint32_t i = 0; i < E; i++) {
-      const uint32_t t = R * i + t0;
-      uint32_t v = lds[lidx<COLS, B, C>(j, t)];
-      if (INV) v = fp_mul(v, tf.at(i));
-      p.out[(g_hi << (p.a + B)) + (uint64_t(t) << p.a) + low0 + j] = v;
+      for (uint32_t i = 0; i < E; i++) put(i, lds[lidx<COLS, B, C>(j, R * i + t0)]);
     }
     return;
   }

@@ -20,3 +20,11 @@ for v in ("new", "old"):
             print(v, r["Name"][40:120], r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), "us")
     print(v, "total ntt_pass ms", round(tot / 1e6, 3))
 PY
+# the headline (trace jobs, 12 steps, no side legs), alternating builds
+for rep in 1 2; do
+  for v in new old; do
+    if [ $v = old ]; then export R0HIP_LIB=$PWD/risc0_amd/lib_variants/libr0hip_old.so; else unset R0HIP_LIB; fi
+    timeout -k 10 300 python3 bench.py --steps 12 --warmup 3 --no-cpu-baseline --no-prove-only --e2e-steps 0 --accum-steps 0 --resident-steps 0 > $O/bench_${v}_$rep.json 2> $O/bench_${v}_$rep.err || { tail -5 $O/bench_${v}_$rep.err; exit 1; }
+    python3 -c "import json; d=json.load(open('$O/bench_${v}_$rep.json')); print('$v', d['value'], d['ms_per_step'])"
+  done
+done
