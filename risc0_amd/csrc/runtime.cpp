@@ -203,7 +203,8 @@ void* scratch(size_t bytes, int slot) {
       // new one would otherwise hipMalloc its eval_check scratch again, GBs at po2 >= 20)
       std::lock_guard<std::mutex> lk(g_mu);
       auto& orph = g_scratch_orphans[slot];
-      auto ot = orph.lower_bound(bytes);
+      auto ot = orph.find(want);  // the size this request allocates itself, else the best fit
+      if (ot == orph.end()) ot = orph.lower_bound(bytes);
       // at most 8x the block this request would allocate: a po2=10 proof must not pin a
       // po2=24 block (it would stay live and count in mem_stats), while a slot whose proof
       // asks small first and then grows (eval_check's, 5.6x between its two requests) still
@@ -334,7 +335,11 @@ void* dev_alloc(size_t bytes) {
     // best fit, exact or up to 25% larger, as for the orphans below: a block taken from the
     // orphans at its own (larger) size comes back here under that size, and an exact-size
     // lookup would then miss it and allocate again in a steady state
-    auto it = t_ctx.pool.lower_bound(bytes);
+    // an exact size first, then the best fit up to 25% larger: a request that takes a larger
+    // block than it needs can leave another thread's request for that size without one (the
+    // threads of a batch race for the blocks exited threads left)
+    auto it = t_ctx.pool.find(bytes);
+    if (it == t_ctx.pool.end()) it = t_ctx.pool.lower_bound(bytes);
     if (it != t_ctx.pool.end() && it->first <= bytes + bytes / 4) {
       void* p = it->second;
       const size_t have = it->first;
@@ -345,7 +350,8 @@ void* dev_alloc(size_t bytes) {
       return p;
     }
     std::lock_guard<std::mutex> lk(g_mu);
-    auto ot = g_orphans.lower_bound(bytes);  // exact or up to 25% larger
+    auto ot = g_orphans.find(bytes);  // exact, else up to 25% larger
+    if (ot == g_orphans.end()) ot = g_orphans.lower_bound(bytes);
     if (ot != g_orphans.end() && ot->first <= bytes + bytes / 4) {
       void* p = ot->second;
       g_live[p] = ot->first;

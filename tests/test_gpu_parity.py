@@ -723,14 +723,14 @@ def test_steady_state_proving_makes_no_hipmalloc(oracle):
     # within a proof, and blocks go back to a shared pool at thread exit, so which thread
     # finds which block depends on the race; once the pool holds blocks of every size both
     # interleavings need, proving allocates no more (a leak would keep allocating here)
-    # (two batches in a row, since one interleaving that happens to allocate nothing does
-    # not mean the pool holds enough for the other)
+    # (three batches in a row, since one or two interleavings that happen to allocate nothing
+    # do not mean the pool holds enough for the others)
     quiet = 0
-    for k in range(10):
+    for k in range(16):
         m0 = r.mem_stats()["mallocs"]
         batch(f"warm{k}")
         quiet = quiet + 1 if k and r.mem_stats()["mallocs"] == m0 else 0
-        if quiet == 2:
+        if quiet == 3:
             break
     else:
         raise AssertionError("warm batches kept allocating device memory")
