@@ -5,6 +5,7 @@ noted per test) plus what DualHal does not cover (combos_prepare/combos_divide,
 eval_check, whole-segment seals). The bar is bit-exact equality of u32 words.
 """
 import os
+import time
 
 import numpy as np
 import pytest
@@ -718,6 +719,10 @@ def test_steady_state_proving_makes_no_hipmalloc(oracle):
             t.start()
         for t in ts:
             t.join()
+        # a thread hands its blocks back in its C++ thread_local destructor, which runs as the
+        # OS thread exits — after Thread.join() has returned — so the next batch's threads could
+        # otherwise start before the blocks are back and allocate (a test race, not a leak)
+        time.sleep(0.2)
 
     # warm until a whole batch allocates nothing: some slots are asked small and then grown
     # within a proof, and blocks go back to a shared pool at thread exit, so which thread
