@@ -21,7 +21,8 @@ namespace r0 {
 void combos_sub(hipStream_t s, uint32_t* combos, const uint32_t* deltas, size_t rows, size_t width,
                 size_t cycles);
 void run_eval_check(const CircuitDef& c, uint32_t* check, const uint32_t* const* groups, const uint32_t* mix,
-                    const uint32_t* global, FpExt poly_mix, size_t po2);
+                    const uint32_t* global, FpExt poly_mix, size_t po2, const uint32_t* h_mix = nullptr,
+                    const uint32_t* h_global = nullptr);
 std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2, const uint32_t* code,
                                     const uint32_t* data, const uint32_t* accum, uint32_t* global,
                                     bool write_version, uint32_t version, std::vector<uint32_t>* mix_out,

@@ -19,6 +19,8 @@ struct EvalCheckArgs {
   uint32_t* mat_ext;            // scratch: mat_ext x domain FpExt
   uint32_t domain;
   uint32_t tile = 0;            // points per tile (0 = whole domain per launch)
+  int64_t wide = -1;            // bit k: kernel k addresses taps from colptr (-1 = tuned default)
+  const uint32_t* uniform = nullptr;  // info.uniform's table (4 words per value), on the device
 };
 
 struct EvalCheckInfo {
@@ -27,10 +29,15 @@ struct EvalCheckInfo {
   int npm;            // number of poly_mix powers the kernels index directly
   int nargs;
   int mat_fp, mat_ext, kernels;
-  double modmuls_per_point;
+  double modmuls_per_point;  // field multiplications of the restated poly_fp (+4 for the 1/Z scale)
   int ncols;             // columns the program reads: (argument, column) pairs
   const int* col_arg;
-  const int* col_idx;  // field multiplications of the restated poly_fp (+4 for the 1/Z scale)
+  const int* col_idx;
+  // lane-independent values the kernels read (4 words each), evaluated on the host from host
+  // copies of the eval_check arguments (only mix and global are read: g[i] null otherwise)
+  // and the poly_mix powers (FpExt AoS)
+  int n_uniform;
+  void (*uniform)(const uint32_t* const* g, const uint32_t* poly_mix, uint32_t* out);
 };
 
 void eval_check_rv32im(hipStream_t s, const EvalCheckArgs& e);

@@ -219,7 +219,8 @@ std::vector<FpExt> map_pow(FpExt base, const uint32_t* exps, size_t n) {  // fie
 
 // eval_check for one circuit (rv32im/src/prove/hal/cpu.rs:145-207 semantics)
 void run_eval_check(const CircuitDef& c, uint32_t* check, const uint32_t* const* groups, const uint32_t* mix,
-                    const uint32_t* global, FpExt poly_mix, size_t po2) {
+                    const uint32_t* global, FpExt poly_mix, size_t po2, const uint32_t* h_mix,
+                    const uint32_t* h_global) {
   hipStream_t s = stream();
   EvalCheckInfo info;
   c.info(&info);
@@ -258,6 +259,29 @@ void run_eval_check(const CircuitDef& c, uint32_t* check, const uint32_t* const*
   for (size_t i = 0; i < pm.size(); i++) pmn[i] = fe_mul_fp(pm[i], kNBeta);
   e.poly_mix_nb = upload(pmn, kSlotEcPolyMixNb);
   e.vinv = upload(vinv, kSlotEcVinv);
+  // the lane-independent values (functions of mix, global and poly_mix only), from host
+  // copies of mix and global (read back here when the caller has none)
+  std::vector<uint32_t> uv(4 * size_t(info.n_uniform > 0 ? info.n_uniform : 1), 0);
+  if (info.n_uniform > 0) {
+    std::vector<uint32_t> hm, hg;
+    if (!h_mix && c.mix_size) {
+      hm.resize(c.mix_size);
+      d2h(hm.data(), mix, c.mix_size * 4);
+      h_mix = hm.data();
+    }
+    if (!h_global && c.output_size) {
+      hg.resize(c.output_size);
+      d2h(hg.data(), global, c.output_size * 4);
+      h_global = hg.data();
+    }
+    std::vector<const uint32_t*> hargs(c.n_eval_args, nullptr);
+    for (size_t i = 0; i < c.n_eval_args; i++) {
+      if (c.eval_args[i] == -1) hargs[i] = h_mix;
+      if (c.eval_args[i] == -2) hargs[i] = h_global;
+    }
+    info.uniform(hargs.data(), reinterpret_cast<const uint32_t*>(pm.data()), uv.data());
+  }
+  e.uniform = upload(uv, kSlotEcUniform);
   e.acc = static_cast<uint32_t*>(scratch(domain * 16, kSlotEcAcc));
   e.mat_fp = static_cast<uint32_t*>(scratch(size_t(info.mat_fp) * domain * 4 + 16, kSlotEcMatFp));
   e.mat_ext = static_cast<uint32_t*>(scratch(size_t(info.mat_ext) * domain * 16 + 16, kSlotEcMatExt));
@@ -269,6 +293,12 @@ void run_eval_check(const CircuitDef& c, uint32_t* check, const uint32_t* const*
       return t ? uint32_t(strtoul(t, nullptr, 0)) : 0u;
     }();
     e.tile = tile_env;
+    // R0_EC_WIDE (experiments): mask of the kernels that take the column-base tap form
+    static const int64_t wide_env = [] {
+      const char* t = getenv("R0_EC_WIDE");
+      return t ? int64_t(strtoull(t, nullptr, 0)) : int64_t(-1);
+    }();
+    e.wide = wide_env;
   }
   double bytes = 16.0 * domain;
   for (int g = 0; g < 3; g++) bytes += 4.0 * domain * c.group_sizes[g];
@@ -327,14 +357,14 @@ struct Prover {
   }
 
   // prover.rs:111-393
-  void finalize(const uint32_t* mix, const uint32_t* global) {
+  void finalize(const uint32_t* mix, const uint32_t* global, const uint32_t* h_mix, const uint32_t* h_global) {
     Span span("finalize");
     hipStream_t s = stream();
     FpExt poly_mix = iop.rng->random_ext_elem();
     size_t domain = cycles * INV_RATE;
     DevBuf check(EXT * domain);
     const uint32_t* gptr[3] = {groups[0]->evaluated.p, groups[1]->evaluated.p, groups[2]->evaluated.p};
-    run_eval_check(c, check.p, gptr, mix, global, poly_mix, po2);
+    run_eval_check(c, check.p, gptr, mix, global, poly_mix, po2, h_mix, h_global);
     if (prof) prof->mark("eval_check");
     ntt_interpolate(s, check.p, EXT, uint32_t(po2 + 2), false);
     PolyGroup check_group(suite, std::move(check), CHECK_SIZE, po2);
@@ -642,7 +672,7 @@ std::vector<uint32_t> prove_segment(const CircuitDef& c, int suite, uint32_t po2
     commit(0, 2, accum);
   }
   prof.mark("commit_accum");
-  p.finalize(dmix.p, global);
+  p.finalize(dmix.p, global, mix.data(), header.data());
   HIP_OK(hipStreamSynchronize(s));
   g_last_profile = prof.finish();
   return std::move(p.iop.proof);

@@ -65,6 +65,7 @@ enum ScratchSlot : int {
   kSlotEcMatExt = 24,
   kSlotEcPolyMixNb = 25,
   kSlotEcColPtr = 26,
+  kSlotEcUniform = 27,
   // prover uploads (prover.cpp): evaluation points per group (3 groups), check points,
   // mix_poly_coeffs row lists, combos deltas, query gather tables
   kSlotTapXs = 33,  // .. 35

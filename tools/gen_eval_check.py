@@ -76,12 +76,50 @@ class Program:
                 t[ins[1]] = "e" if "e" in (t[ins[2]], t[ins[3]]) else "f"
         self.types = t
         self.mat = set()
+        self.uprog, self.uslot = [], {}
+
+    def hoist_uniform(self, terms):
+        """Lane-independent values — cones of constants and `g` loads only (mix and global
+        words, the same for every point) — that a point's arithmetic reads are evaluated once
+        on the host (eval_check_<circuit>_uniform) and read by the kernels from a table
+        (A.uv, scalar loads); every kernel that needed one recomputed its cone per lane.
+        Applied after scheduling, so kernel packing (and its tuning) is unchanged."""
+        uni = {}
+        for ins in self.prog:
+            op = ins[0]
+            if op == "r":
+                continue
+            if op in "ceg":
+                uni[ins[1]] = True
+            elif op == "l":
+                uni[ins[1]] = False
+            else:
+                uni[ins[1]] = all(uni[d] for d in deps(ins))
+        need = set()
+        for ins in self.prog:
+            if ins[0] in "+-*ab" and not uni[ins[1]]:
+                need.update(d for d in deps(ins) if uni[d])
+        for t in terms:
+            need.update(v for v in term_roots(t) if uni[v])
+        need.update(v for v in self.mat if uni[v])  # a stored value that is the same everywhere
+        hoist = sorted((v for v in need if self.byid[v][0] in "+-*ab"), key=self.order.get)
+        self.mat -= set(hoist)
+        cone, stack = set(), list(hoist)
+        while stack:
+            v = stack.pop()
+            if v not in cone:
+                cone.add(v)
+                stack.extend(deps(self.byid[v]))
+        self.uprog = [self.byid[v] for v in sorted(cone, key=self.order.get)]
+        self.uslot = {v: n for n, v in enumerate(hoist)}
+        for v in hoist:
+            self.byid[v] = ("u", v, self.uslot[v])
 
     def cost(self, v):
         ins = self.byid[v]
         op = ins[0]
         ty = self.types
-        if op in "clge":
+        if op in "clgeu":
             return 0
         if op in "+-":
             return 4 if ty[v] == "e" else 1
@@ -189,7 +227,7 @@ def schedule(pg, budget):
         while pg.cone_cost(roots) > budget:
             best, bestc = None, -1
             for v in pg.cone(roots):
-                if v in roots or v in pg.mat or byid[v][0] in "clge":
+                if v in roots or v in pg.mat or byid[v][0] in "clgeu":
                     continue
                 c = pg.cone_cost([v])
                 if bestc < c <= budget:
@@ -290,6 +328,8 @@ PIN = os.environ.get("EC_PIN", "0") == "1"
 # returns 16 B to each of the 64 lanes through the texture data path, ~360 per wave; not
 # adopted.
 PMV = os.environ.get("EC_PMV", "0") == "1"
+# EC_HOIST=0: every kernel computes the lane-independent values it reads itself (no host table)
+HOIST = os.environ.get("EC_HOIST", "1") == "1"
 PMD = int(os.environ.get("EC_PMD", "64"))
 # EC_PINB=n (or a kernel's "pinb"): the poly_mix terms (acc_fp, acc_ext) go in batches of n;
 # batch b's table pointer is pinned to the running sum after the first term of batch b-1,
@@ -461,10 +501,58 @@ def repack(pg, items, budget):
     return [sorted(b[0], key=lambda it: (it[0], it[1])) for b in bins]
 
 
+def uniform_fn(pg):
+    """Host evaluation of the hoisted lane-independent values (Program.hoist_uniform), in
+    program order with canonical host arithmetic (bb31.h); g[ARG] are host copies of the
+    uniform arguments (mix, global), pm the poly_mix powers (FpExt AoS)."""
+    ty = pg.types
+    L = ["// lane-independent values (cones of constants, mix and global words), evaluated once",
+         "// per eval_check on the host; slot s holds 4 words (an Fp value in word 0)",
+         f"constexpr int NUV = {len(pg.uslot)};",
+         "void uniform(const uint32_t* const* g, const uint32_t* pmw, uint32_t* out) {",
+         "  const FpExt* pm = reinterpret_cast<const FpExt*>(pmw);",
+         "  (void)g; (void)pm; (void)out;"]
+
+    def x(v):
+        return f"u{v}" if ty[v] == "e" else f"fe_from_fp(u{v})"
+
+    for ins in pg.uprog:
+        op, i = ins[0], ins[1]
+        if op == "c":
+            L.append(f"  const uint32_t u{i} = {enc(ins[2])}u;")
+        elif op == "e":
+            L.append(f"  const FpExt u{i} = FpExt{{{{{', '.join(str(enc(v)) + 'u' for v in ins[2:6])}}}}};")
+        elif op == "g":
+            L.append(f"  const uint32_t u{i} = g[{ins[2]}][{ins[3]}];")
+        elif op in "+-*":
+            a, b = ins[2], ins[3]
+            if ty[i] == "f":
+                fn = {"+": "fp_add", "-": "fp_sub", "*": "fp_mul"}[op]
+                L.append(f"  const uint32_t u{i} = {fn}(u{a}, u{b});")
+            else:
+                fn = {"+": "fe_add", "-": "fe_sub", "*": "fe_mul"}[op]
+                L.append(f"  const FpExt u{i} = {fn}({x(a)}, {x(b)});")
+        elif op == "a":
+            L.append(f"  const FpExt u{i} = fe_add(u{ins[2]}, fe_mul({x(ins[3])}, pm[{ins[4]}]));")
+        elif op == "b":
+            L.append(f"  const FpExt u{i} = fe_add(u{ins[2]}, fe_mul(fe_mul({x(ins[3])}, {x(ins[4])}), pm[{ins[5]}]));")
+        else:
+            raise RuntimeError(f"unexpected op {op} in a lane-independent cone")
+    for v, n in sorted(pg.uslot.items(), key=lambda kv: kv[1]):
+        if ty[v] == "f":
+            L.append(f"  out[{4 * n}] = u{v}; out[{4 * n + 1}] = out[{4 * n + 2}] = out[{4 * n + 3}] = 0;")
+        else:
+            L.append(f"  for (int k = 0; k < 4; k++) out[{4 * n} + k] = u{v}.c[k];")
+    L.append("}")
+    return L
+
+
 def emit(circuit, outdir, budget, host=False):
     pg = Program(circuit)
     pg.mat = set(mat_config(circuit, budget))
     terms, kernels = schedule(pg, budget)
+    if HOIST:
+        pg.hoist_uniform(terms)
     tune0 = kernel_config(circuit, budget)
     resplit, piece_tune = resplit_config(circuit, budget)
     tune = {}
@@ -524,6 +612,8 @@ def emit(circuit, outdir, budget, host=False):
         "  uint32_t* me;         // materialised FpExt values, [slot][domain] AoS",
         "  uint32_t domain;",
         "  uint32_t base, count;  // this launch covers points [base, base + count)",
+        "  uint64_t wide;         // bit k: kernel k takes its taps from the column bases (A.cp)",
+        "  const uint32_t* uv;    // lane-independent values evaluated on the host, 4 words each",
         "};",
         f"constexpr int NPM = {npm};",
         "// one more than the largest tapped column index of any argument: 32-bit tap indices",
@@ -682,6 +772,8 @@ def emit(circuit, outdir, budget, host=False):
     for ki, items in enumerate(kernels):
         # per-kernel arithmetic mode: tuned "canon" (1 canonical, 0 range analysis) or EC_CANON
         kcanon = CANON_ALL if "EC_CANON_FORCE" in os.environ else bool(tune.get(ki, {}).get("canon", CANON_ALL))
+        # (a scheduled "mat" item that hoist_uniform took out of pg.mat has nothing to store)
+        items = [it for it in items if it[2] != "mat" or it[3] in pg.mat]
         roots = []
         for it in items:
             roots += [it[3]] if it[2] == "mat" else term_roots(it[3])
@@ -938,7 +1030,7 @@ def emit(circuit, outdir, budget, host=False):
         kpinb = int(os.environ.get("EC_PINB", tune.get(ki, {}).get("pinb", PINB)))
         if ORDER == "dfs":
             byid_ = pg.byid
-            leaves = set(v for v in need if v in loaded or byid_[v][0] in "clge")
+            leaves = set(v for v in need if v in loaded or byid_[v][0] in "clgeu")
             oroots = sorted(set(roots), key=lambda v: pg.order[v])
             body = [v for v in dfs_order(pg, need, oroots, leaves) if v not in leaves]
             first_use = {}
@@ -946,10 +1038,10 @@ def emit(circuit, outdir, budget, host=False):
                 for d in deps(byid_[v]):
                     if d in leaves and d not in first_use:
                         first_use[d] = n_
-            consts = [v for v in leaves if byid_[v][0] in "ceg"]
+            consts = [v for v in leaves if byid_[v][0] in "cegu"]
             slots = {}
             for v in leaves:
-                if byid_[v][0] in "ceg":
+                if byid_[v][0] in "cegu":
                     continue
                 slots.setdefault(max(0, first_use.get(v, 0) - kpf), []).append(v)
             seq = sorted(consts, key=lambda v: pg.order[v])
@@ -975,7 +1067,7 @@ def emit(circuit, outdir, budget, host=False):
         qv = {}
         term_at = {}
         for ti, (e, f) in enumerate(mine):
-            rts = [x for x in term_roots((e, f)) if pg.byid[x][0] not in "ceg"]
+            rts = [x for x in term_roots((e, f)) if pg.byid[x][0] not in "cegu"]
             term_at.setdefault(max([order_pos[x] for x in rts] + [-1]), []).append(ti)
         done_terms = set()
 
@@ -1072,6 +1164,13 @@ def emit(circuit, outdir, budget, host=False):
             elif op == "g":
                 w(f"  const uint32_t v{i} = A.a[{ins[2]}][{ins[3]}];")
                 Mv[i] = PM
+            elif op == "u":
+                q = 4 * ins[2]
+                if types[i] == "f":
+                    w(f"  const uint32_t v{i} = A.uv[{q}];")
+                else:
+                    w(f"  const FpExt v{i} = FpExt{{{{A.uv[{q}], A.uv[{q + 1}], A.uv[{q + 2}], A.uv[{q + 3}]}}}};")
+                Mv[i] = PM
             elif op in "ab":
                 ps, pos = acc_parts(ins[2])
                 if op == "a":
@@ -1137,6 +1236,7 @@ def emit(circuit, outdir, budget, host=False):
         f"  info->nargs = {nargs}; info->mat_fp = {nf}; info->mat_ext = {ne}; info->kernels = {len(kernels)};",
         f"  info->modmuls_per_point = {modmuls(pg) + 4};",
         f"  info->ncols = {len(colslot)}; info->col_arg = ec_{circuit}::kColArg; info->col_idx = ec_{circuit}::kColIdx;",
+        f"  info->n_uniform = ec_{circuit}::NUV; info->uniform = ec_{circuit}::uniform;",
         "}",
     ]
     combos_line = f"const int kPmCombos[] = {{{', '.join(str(x) for x in flat) or '0'}}};"
@@ -1159,6 +1259,7 @@ def emit(circuit, outdir, budget, host=False):
         T.append(f"constexpr int NK = {len(bodies)};")
         T.append(f"static void (*const kTable[NK])(const Args&, uint32_t) = {{{', '.join(f'k{i}' for i in range(len(bodies)))}}};")
         T.append(combos_line)
+        T += uniform_fn(pg)
         T.append(f"}}  // namespace ec_{circuit}")
         T.append("}  // namespace r0")
         T += [
@@ -1174,7 +1275,10 @@ def emit(circuit, outdir, budget, host=False):
             f"  for (int i = 0; i < {len(colslot)}; i++) cp[i] = args[kColArg[i]] + size_t(kColIdx[i]) * domain;",
             "  A.cp = cp;",
             "  A.pm = pm; A.pmn = pmn; A.acc = acc; A.check = check; A.vinv = vinv; A.mf = mf; A.me = me;",
-            "  A.domain = domain; A.base = 0; A.count = domain;",
+            "  A.domain = domain; A.base = 0; A.count = domain; A.wide = 0;",
+            "  uint32_t uvt[4 * (NUV ? NUV : 1)];",
+            "  uniform(args, pm, uvt);",
+            "  A.uv = uvt;",
             "  for (int k = 0; k < NK; k++)",
             "    for (uint32_t c = 0; c < domain; c++) kTable[k](A, c);",
             "}",
@@ -1191,7 +1295,7 @@ def emit(circuit, outdir, budget, host=False):
         K += L
         K.append("}")
         K.append(f"void launch_k{ki}(hipStream_t s, const Args& A) {{")
-        K.append(f"  if (uint64_t(kTapCols) * A.domain > (uint64_t(1) << 32))")
+        K.append(f"  if (((A.wide >> {ki}) & 1) || uint64_t(kTapCols) * A.domain > (uint64_t(1) << 32))")
         K.append(f"    hipLaunchKernelGGL(k{ki}<true>, dim3(div_up(A.count, 256)), dim3(256), 0, s, A);")
         K.append("  else")
         K.append(f"    hipLaunchKernelGGL(k{ki}<false>, dim3(div_up(A.count, 256)), dim3(256), 0, s, A);")
@@ -1201,11 +1305,16 @@ def emit(circuit, outdir, budget, host=False):
         K.append("}  // namespace r0")
         with open(os.path.join(outdir, f"eval_check_{circuit}_k{ki}.hip"), "w") as f:
             f.write("\n".join(K) + "\n")
+    # kernels tuned to the scalar-column-base tap form at every size ("wide" in the tuning file)
+    assert len(kernels) <= 64
+    wide_list = [k for k in range(len(kernels)) if tune.get(k, {}).get("wide")]
+    wide_default = sum(1 << k for k in wide_list)
     L = [head]
     w = L.append
     for ki in range(len(kernels)):
         w(f"void launch_k{ki}(hipStream_t s, const Args& A);")
     w(combos_line)
+    L += uniform_fn(pg)
     w(f"}}  // namespace ec_{circuit}")
     L += info
     w(f"void eval_check_{circuit}(hipStream_t s, const EvalCheckArgs& e) {{")
@@ -1215,7 +1324,9 @@ def emit(circuit, outdir, budget, host=False):
     w(f"  for (int i = 0; i < {nargs}; i++) A.a[i] = e.args[i];")
     w("  A.cp = e.colptr;")
     w("  A.pm = e.poly_mix; A.pmn = e.poly_mix_nb; A.acc = e.acc; A.check = e.check; A.vinv = e.vinv; A.domain = e.domain;")
-    w("  A.mf = e.mat_fp; A.me = e.mat_ext;")
+    w("  A.mf = e.mat_fp; A.me = e.mat_ext; A.uv = e.uniform;")
+    w(f"  R0_REQUIRE(NUV == 0 || e.uniform, \"eval_check_{circuit}: no lane-independent value table\");")
+    w(f"  A.wide = e.wide >= 0 ? uint64_t(e.wide) : {wide_default}ull;  // tuned: {wide_list}")
     w("  // tiles of e.tile points run every kernel before the next tile, so a tile's")
     w("  // trace columns are re-read from the Infinity Cache rather than HBM")
     w("  const uint32_t tile = e.tile ? e.tile : e.domain;")
