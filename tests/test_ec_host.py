@@ -25,9 +25,12 @@ P = 15 * 2**27 + 1
 u32p = C.POINTER(C.c_uint32)
 
 
-# generator variants: the default (canonical results), and the lazy range analysis with
-# saddr tap loads and split accumulation chains (tools/gen_eval_check.py knobs)
-VARIANTS = {"canonical": {}, "lazy": {"EC_CANON": "0", "EC_SADDR": "1", "EC_SPLIT": "2"}}
+# generator variants: the default (tuned per kernel), the lazy range analysis with saddr tap
+# loads and split accumulation chains, and 64-bit sums of products (EC_FUSE) in canonical and
+# lazy kernels (tools/gen_eval_check.py knobs)
+VARIANTS = {"canonical": {}, "lazy": {"EC_CANON": "0", "EC_SADDR": "1", "EC_SPLIT": "2"},
+            "fused": {"EC_FUSE_FORCE": "1"}, "fused_canon": {"EC_FUSE_FORCE": "1", "EC_CANON_FORCE": "1"},
+            "fused_lazy": {"EC_FUSE_FORCE": "1", "EC_CANON_FORCE": "0"}}
 
 
 @pytest.fixture(scope="module", params=sorted(VARIANTS))

@@ -328,6 +328,10 @@ PIN = os.environ.get("EC_PIN", "0") == "1"
 # returns 16 B to each of the 64 lanes through the texture data path, ~360 per wave; not
 # adopted.
 PMV = os.environ.get("EC_PMV", "0") == "1"
+# EC_FUSE=1 (or a kernel's "fuse" in the tuning file): sums of products are accumulated in
+# 64 bits (one v_mad_u64_u32 per product, one REDC per sum) instead of a REDC per product
+# and a reduction per addition; EC_FUSE_FORCE=0/1 overrides the tuning file
+FUSE = os.environ.get("EC_FUSE", "0") == "1"
 # EC_HOIST=0: every kernel computes the lane-independent values it reads itself (no host table)
 HOIST = os.environ.get("EC_HOIST", "1") == "1"
 PMD = int(os.environ.get("EC_PMD", "64"))
@@ -553,6 +557,18 @@ def emit(circuit, outdir, budget, host=False):
     terms, kernels = schedule(pg, budget)
     if HOIST:
         pg.hoist_uniform(terms)
+    # uses of each value over the whole program (after hoisting); term roots and materialised
+    # values count twice, so a fused sum never swallows a value something else reads
+    nuse, consumer = {}, {}
+    for ins in pg.byid.values():
+        for d in deps(ins):
+            nuse[d] = nuse.get(d, 0) + 1
+            consumer[d] = ins[1]
+    for t in terms:
+        for r in term_roots(t):
+            nuse[r] = nuse.get(r, 0) + 2
+    for v in pg.mat:
+        nuse[v] = nuse.get(v, 0) + 2
     tune0 = kernel_config(circuit, budget)
     resplit, piece_tune = resplit_config(circuit, budget)
     tune = {}
@@ -691,6 +707,35 @@ def emit(circuit, outdir, budget, host=False):
         "  for (int i = 0; i < 4; i++) a.c[i] += b.c[i];",
         "  return a;",
         "}",
+        "// 64-bit sums of products (EC_FUSE): a term x enters as x * 2^32 (x * kFoldC), a product",
+        "// a * b as itself, so one REDC of the sum gives the Montgomery word of the sum",
+        "EC_FN Acc acc_mf(Acc s, FpExt a, uint32_t b) {",
+        "#pragma unroll",
+        "  for (int i = 0; i < 4; i++) s.c[i] += uint64_t(a.c[i]) * b;",
+        "  return s;",
+        "}",
+        "EC_FN Acc acc_m0(Acc s, uint32_t a, uint32_t b) { s.c[0] += uint64_t(a) * b; return s; }",
+        "EC_FN Acc acc_me(Acc s, FpExt a, FpExt b) {",
+        "  const uint32_t n1 = fp_mul(kNBeta, b.c[1]), n2 = fp_mul(kNBeta, b.c[2]), n3 = fp_mul(kNBeta, b.c[3]);",
+        "  s.c[0] += uint64_t(a.c[0]) * b.c[0] + uint64_t(a.c[1]) * n3 + uint64_t(a.c[2]) * n2 + uint64_t(a.c[3]) * n1;",
+        "  s.c[1] += uint64_t(a.c[0]) * b.c[1] + uint64_t(a.c[1]) * b.c[0] + uint64_t(a.c[2]) * n3 + uint64_t(a.c[3]) * n2;",
+        "  s.c[2] += uint64_t(a.c[0]) * b.c[2] + uint64_t(a.c[1]) * b.c[1] + uint64_t(a.c[2]) * b.c[0] + uint64_t(a.c[3]) * n3;",
+        "  s.c[3] += uint64_t(a.c[0]) * b.c[3] + uint64_t(a.c[1]) * b.c[2] + uint64_t(a.c[2]) * b.c[1] + uint64_t(a.c[3]) * b.c[0];",
+        "  return s;",
+        "}",
+        "EC_FN Acc acc_plus(Acc s, FpExt x) {",
+        "#pragma unroll",
+        "  for (int i = 0; i < 4; i++) s.c[i] += uint64_t(x.c[i]) * kFoldC;",
+        "  return s;",
+        "}",
+        "EC_FN Acc acc_plusf(Acc s, uint32_t x) { s.c[0] += uint64_t(x) * kFoldC; return s; }",
+        "EC_FN Acc acc_add0(Acc s, uint64_t x) { s.c[0] += x; return s; }",
+        "EC_FN Acc acc_negk(Acc s, uint64_t k) {",
+        "#pragma unroll",
+        "  for (int i = 0; i < 4; i++) s.c[i] = k - s.c[i];",
+        "  return s;",
+        "}",
+        "EC_FN FpExt xneg(FpExt a, uint32_t kp) { return FpExt{{kp - a.c[0], kp - a.c[1], kp - a.c[2], kp - a.c[3]}}; }",
         "// the table pointer, made to depend on `a` (no instruction): pm[k] is loaded after `a`",
         "#ifdef R0_EC_HOST",
         "EC_FN const uint32_t* pin(const uint32_t* p, const Acc&) { return p; }",
@@ -816,8 +861,165 @@ def emit(circuit, outdir, budget, host=False):
             tmp["n"] += 1
             return f"t{tmp['n']}"
 
+        # EC_FUSE: a product whose only use is an addition or subtraction is deferred (pend:
+        # its two operands), and a sum whose only use is another sum stays a 64-bit Fp sum or an
+        # Acc (sums: kind, variable, bound); the value is reduced to a word where it is read
+        kfuse = (os.environ["EC_FUSE_FORCE"] == "1" if "EC_FUSE_FORCE" in os.environ
+                 else bool(tune.get(ki, {}).get("fuse", FUSE)))
+        rootset = set(roots)
+        fuse_ok = set()
+        if kfuse:
+            for v in need:
+                ins_ = pg.byid[v]
+                if (ins_[0] in "+-*" and nuse.get(v, 0) == 1 and v not in rootset and v not in produced
+                        and v not in loaded and consumer[v] in need and pg.byid[consumer[v]][0] in "+-"):
+                    fuse_ok.add(v)
+        pend, sums = {}, {}
+        qn = {"n": 0}
+
+        def qname():
+            qn["n"] += 1
+            return f"q{qn['n']}"
+
+        def f_reduce(expr, bd, name):
+            """word of a 64-bit Fp sum (canonical in canonical kernels)"""
+            if kcanon:
+                if bd >= RED:
+                    expr, bd = f"fold64({expr})", fold_max(bd)
+                w(f"  const uint32_t {name} = mont_reduce({expr});")
+                return PM
+            if bd + U32 * P > U64 or redc_max(bd) > U32:
+                expr, bd = f"fold64({expr})", fold_max(bd)
+            w(f"  const uint32_t {name} = redc_lazy({expr});")
+            return redc_max(bd)
+
+        def materialize(x):
+            if x in pend:
+                a, b = pend.pop(x)
+                Mv[x] = op_mul(a, b, name=f"v{x}")[1]
+                return
+            kind, var, bd = sums.pop(x)
+            Mv[x] = acc_to_ext(var, bd, f"v{x}") if kind == "E" else f_reduce(var, bd, f"v{x}")
+
         def opd(x):
+            if x not in Mv and (x in pend or x in sums):
+                materialize(x)
             return (f"v{x}", Mv[x], types[x], x)
+
+        def negw(o):
+            """k p - o for a word operand (k p >= its bound, k p < 2^32)"""
+            while -(-o[1] // P) * P > U32:
+                o = reduce1(o)
+            kp = max(1, -(-o[1] // P)) * P
+            nm = fresh()
+            if o[2] == "f":
+                w(f"  const uint32_t {nm} = {kp}u - {o[0]};")
+            else:
+                w(f"  const FpExt {nm} = xneg({o[0]}, {kp}u);")
+            return (nm, kp, o[2], None)
+
+        LIM = U64 - fold_max(U64)
+
+        def sum_of(i, op, xa, xb):
+            """64-bit sum for x_a + x_b or x_a - x_b, operands deferred products, sums or words"""
+            E = types[i] == "e"
+            st = {"e": None, "b": 0}
+
+            def push(make, tb):
+                cur, cb = st["e"], st["b"]
+                if cur is not None and cb + tb > U64:
+                    nm = qname()
+                    w(f"  const {'Acc' if E else 'uint64_t'} {nm} = {'acc_fold' if E else 'fold64'}({cur});")
+                    cur, cb = nm, fold_max(cb)
+                assert cb + tb <= U64
+                nm = qname()
+                if E:
+                    w(f"  const Acc {nm} = {make(cur if cur is not None else 'Acc{{0, 0, 0, 0}}')};")
+                else:
+                    w(f"  const uint64_t {nm} = {make(cur)};")
+                st["e"], st["b"] = nm, cb + tb
+
+            def f_add(cur, term):
+                return term if cur is None else f"{cur} + {term}"
+
+            def contrib(x, neg):
+                if x in sums:
+                    kind, var, bd = sums.pop(x)
+                    if bd > LIM:
+                        nm = qname()
+                        w(f"  const {'Acc' if kind == 'E' else 'uint64_t'} {nm} = "
+                          f"{'acc_fold' if kind == 'E' else 'fold64'}({var});")
+                        var, bd = nm, fold_max(bd)
+                    if neg:
+                        if -(-bd // P) * P > U64:
+                            nm = qname()
+                            w(f"  const {'Acc' if kind == 'E' else 'uint64_t'} {nm} = "
+                              f"{'acc_fold' if kind == 'E' else 'fold64'}({var});")
+                            var, bd = nm, fold_max(bd)
+                        K = max(1, -(-bd // P)) * P
+                        if kind == "E":
+                            push(lambda c: f"acc_add({c}, acc_negk({var}, {K}ull))", K)
+                        elif E:
+                            push(lambda c: f"acc_add0({c}, {K}ull - {var})", K)
+                        else:
+                            push(lambda c: f_add(c, f"({K}ull - {var})"), K)
+                    else:
+                        if kind == "E":
+                            push(lambda c: f"acc_add({c}, {var})", bd)
+                        elif E:
+                            push(lambda c: f"acc_add0({c}, {var})", bd)
+                        else:
+                            push(lambda c: f_add(c, var), bd)
+                    return
+                if x in pend:
+                    a, b = pend.pop(x)
+                    if a[2] == "f" and b[2] == "e":
+                        a, b = b, a
+                    # every term below LIM, so a folded running sum always has room for it
+                    while (4 if a[2] == b[2] == "e" else 1) * a[1] * max(b[1], PM if a[2] == b[2] == "e" else 0) > LIM:
+                        if a[1] >= b[1]:
+                            a = reduce1(a)
+                        else:
+                            b = reduce1(b)
+                    if a[2] == "e" and b[2] == "e":
+                        if neg:
+                            a = negw(a)
+                        push(lambda c: f"acc_me({c}, {a[0]}, {b[0]})", 4 * a[1] * max(b[1], PM))
+                    elif a[2] == "e":
+                        if neg:
+                            b = negw(b)
+                        push(lambda c: f"acc_mf({c}, {a[0]}, {b[0]})", a[1] * b[1])
+                    else:
+                        if neg:
+                            b = negw(b)
+                        if E:
+                            push(lambda c: f"acc_m0({c}, {a[0]}, {b[0]})", a[1] * b[1])
+                        else:
+                            push(lambda c: f_add(c, f"uint64_t({a[0]}) * {b[0]}"), a[1] * b[1])
+                    return
+                o = opd(x)
+                if neg:
+                    o = negw(o)
+                if o[2] == "e":
+                    push(lambda c: f"acc_plus({c}, {o[0]})", o[1] * FOLDC)
+                elif E:
+                    push(lambda c: f"acc_plusf({c}, {o[0]})", o[1] * FOLDC)
+                else:
+                    push(lambda c: f_add(c, f"uint64_t({o[0]}) * {FOLDC}u"), o[1] * FOLDC)
+
+            contrib(xa, False)
+            contrib(xb, op == "-")
+            sums[i] = ("E" if E else "F", st["e"], st["b"])
+            if i not in fuse_ok:
+                materialize(i)
+
+        def special_mul(a, b):
+            """products op_mul shortcuts (constant operands 1, 2, -1; FpExt constants)"""
+            if a[2] == "f" and b[2] == "f":
+                return any(cval.get(x[3]) in (one, two, mone) for x in (a, b) if x[3] is not None)
+            if a[2] == "e" and b[2] == "e":
+                return any(x[3] is not None and x[3] in ecval for x in (a, b))
+            return False
 
         def decl(ty):
             return "uint32_t" if ty == "f" else "FpExt"
@@ -1188,6 +1390,10 @@ def emit(circuit, outdir, budget, host=False):
                 if i in canon:
                     e_, b_ = acc_src(i)
                     Mv[i] = acc_to_ext(e_, b_, f"v{i}")
+            elif kfuse and op == "*" and i in fuse_ok and not special_mul(opd(ins[2]), opd(ins[3])):
+                pend[i] = (opd(ins[2]), opd(ins[3]))
+            elif kfuse and op in "+-" and any(x in pend or x in sums for x in (ins[2], ins[3])):
+                sum_of(i, op, ins[2], ins[3])
             else:
                 fn = {"+": op_add, "-": op_sub, "*": op_mul}[op]
                 Mv[i] = fn(opd(ins[2]), opd(ins[3]), name=f"v{i}")[1]
