@@ -425,11 +425,13 @@ def kernel_roofline(r, args, prove):
     traffic, tsrc = pmc_traffic(name, calls, args)
     fam = name.split("_poseidon2")[0].split("_sha")[0]
     insts, busy, vsrc = pmc_valu(fam, args)
+    vsrc, vmatch = vsrc if vsrc else (None, None)
     if fam in VALU_BOUND and insts:
         gips = insts / avg_s / 1e9
         out = {"kernel": name, "bound": "valu", "achieved": round(gips, 1), "peak": VALU_PEAK_GIPS,
                "unit": "G VALU instructions/s (wave64)", "frac": round(gips / VALU_PEAK_GIPS, 4),
                "valu_insts_per_launch": int(insts), "issue_busy_frac": busy, "valu_source": vsrc,
+               "valu_source_matches_library": vmatch,
                "note": "integer modular arithmetic bound by VALU issue: executed VALU instructions per launch "
                        "(PMC SQ_INSTS_VALU) over the launch time, against 1024 SIMDs x one wave64 instruction "
                        "per 4 cycles at 2.4 GHz; VOP2 v_add/v_sub (about a quarter of eval_check's) can issue "
@@ -443,6 +445,15 @@ def kernel_roofline(r, args, prove):
     if tsrc:
         out["traffic_source"] = tsrc
     return out
+
+
+def lib_fingerprint():
+    """first 16 hex digits of the sha256 of the loaded libr0hip.so: the committed PMC summaries
+    record the library they were measured on (tools/gpu_round.sh), so a stale count is visible"""
+    import hashlib
+    from risc0_amd import hal
+    with open(hal.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
 def pmc_valu(family, args):
@@ -459,7 +470,9 @@ def pmc_valu(family, args):
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from rocprof_families import family as fam_of
     with open(files[-1]) as f:
-        ks = json.load(f)["kernels"]
+        doc = json.load(f)
+    ks = doc["kernels"]
+    matches = doc.get("lib_sha256_16") == lib_fingerprint()
     insts = tot = busy = 0.0
     for k, d in ks.items():
         if fam_of(k) != family or not d["dispatches"]:
@@ -474,7 +487,7 @@ def pmc_valu(family, args):
         insts = None  # launches per proof differ per kernel: only eval_check is quoted per launch
     if tot == 0:
         return None, None, None
-    return insts, round(busy / tot, 3), os.path.relpath(files[-1], ROOT)
+    return insts, round(busy / tot, 3), (os.path.relpath(files[-1], ROOT), matches)
 
 
 def mixed_arm_rows(data, n):

@@ -21,7 +21,10 @@ scheduled as a short sequence of kernels, each below a cost budget:
      polynomial inverse (4 distinct values on the 4N domain, from the host) and
      writes the 4 SoA planes.
 Trace taps are reloaded by every kernel that needs them (coalesced per column).
-Products of several poly_mix powers are folded into host-computed constants.
+Products of several poly_mix powers are folded into host-computed constants, and values
+that depend only on constants, mix and global words are evaluated once on the host
+(Program.hoist_uniform). Per kernel (tuning file): sums of products as 64-bit sums with one
+REDC per sum ("fuse"), and tap addressing by column base pointers ("wide").
 
 Usage: gen_eval_check.py CIRCUIT OUTDIR [BUDGET]
 Writes OUTDIR/eval_check_<circuit>_k<i>.hip (one per kernel, compiled in parallel)

@@ -7,6 +7,7 @@
 TAG=${1:-round}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/$TAG; mkdir -p $O
+sha256sum risc0_amd/lib/libr0hip.so | cut -c1-16 > $O/lib_sha256_16
 B="bench.py --no-cpu-baseline --no-prove-only --e2e-steps 0 --accum-steps 0 --resident-steps 0 --steps 3 --warmup 1 --inflight 1"
 # a failing test (exit 1) still leaves the profile worth taking; a crash or time limit ends the call
 timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
