@@ -64,7 +64,7 @@ def measure():
 def kernel_times(d, circuit):
     out = {}
     for r in csv.DictReader(open(os.path.join(d, "run_kernel_stats.csv"))):
-        km = re.search(r"ec_" + circuit + r"::k(\d+)<false>", r["Name"])
+        km = re.search(r"ec_" + circuit + r"::k(\d+)<(?:false|true)>", r["Name"])
         if km:
             out[int(km.group(1))] = float(r["AverageNs"]) / 1e3
     return out
