@@ -131,25 +131,40 @@ __device__ __forceinline__ void stage_group(uint32_t* lds, const uint32_t* tw, c
   __syncthreads();
 }
 
-// DIT stages [S, B] ascending, radix-8 groups first; the first group of an expanding pass
+// Stages per register group: n remaining stages in groups of at most MAXR (row passes
+// R0_NTT_MAXR_ROW, column passes R0_NTT_MAXR_COL), sizes balanced, the larger ones first.
+#ifndef R0_NTT_MAXR_ROW
+#define R0_NTT_MAXR_ROW 3
+#endif
+#ifndef R0_NTT_MAXR_COL
+#define R0_NTT_MAXR_COL 3
+#endif
+template <bool COLS>
+constexpr int group_stages(int n) {
+  const int maxr = COLS ? R0_NTT_MAXR_COL : R0_NTT_MAXR_ROW;
+  const int g = (n + maxr - 1) / maxr;
+  return (n + g - 1) / g;
+}
+
+// DIT stages [S, B] ascending, larger groups first; the first group of an expanding pass
 // (S == EB + 1) reads the compact (unreplicated) input. Compile-time recursion, so each
 // group's first stage is a constant.
 template <bool COLS, int B, int C, int EB, int NT, int S>
 __device__ __forceinline__ void fwd_stages(uint32_t* lds, const uint32_t* tw, const uint32_t* csrc) {
   if constexpr (S <= B) {
     constexpr int n = B - S + 1;
-    constexpr int NST = n >= 3 ? 3 : n;
+    constexpr int NST = group_stages<COLS>(n);
     constexpr int FROM = (S == EB + 1 && EB > 0) ? EB : 0;
     stage_group<false, COLS, B, C, NST, FROM, NT, S>(lds, tw, csrc);
     fwd_stages<COLS, B, C, EB, NT, S + NST>(lds, tw, csrc);
   }
 }
 
-// DIF stages [1, S] descending, radix-8 groups first
+// DIF stages [1, S] descending, larger groups first
 template <bool COLS, int B, int C, int NT, int S>
 __device__ __forceinline__ void inv_stages(uint32_t* lds, const uint32_t* tw) {
   if constexpr (S >= 1) {
-    constexpr int NST = S >= 3 ? 3 : S;
+    constexpr int NST = group_stages<COLS>(S);
     stage_group<true, COLS, B, C, NST, 0, NT, S - NST + 1>(lds, tw, nullptr);
     inv_stages<COLS, B, C, NT, S - NST>(lds, tw);
   }
