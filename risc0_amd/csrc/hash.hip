@@ -167,6 +167,18 @@ __constant__ static const uint32_t kK256[64] = {
     0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
 
 __device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_rotateright32(x, n); }
+// three-way XOR as one v_bitop3_b32 (gfx950; truth table 0x96 is symmetric in its inputs):
+// LLVM otherwise emits two v_xor_b32 after the three v_alignbit of every Σ/σ function
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+// Ch and Maj as one v_bitop3_b32 each (truth-table index = src0*4 + src1*2 + src2)
+__device__ __forceinline__ uint32_t sha_ch(uint32_t e, uint32_t f, uint32_t g) {
+  return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);  // e ? f : g
+}
+__device__ __forceinline__ uint32_t sha_maj(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);  // majority
+}
 
 // FIPS 180-4 compression; w[] holds the 16 big-endian message words.
 __device__ __forceinline__ void sha_compress(uint32_t* s, uint32_t* w) {
@@ -178,16 +190,16 @@ __device__ __forceinline__ void sha_compress(uint32_t* s, uint32_t* w) {
       wi = w[i];
     } else {
       uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-      uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
-      uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+      uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+      uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
       wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
       w[i & 15] = wi;
     }
-    uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
-    uint32_t ch = (e & f) ^ (~e & g);
+    uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+    uint32_t ch = sha_ch(e, f, g);
     uint32_t t1 = h + S1 + ch + kK256[i] + wi;
-    uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
-    uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+    uint32_t mj = sha_maj(a, b, c);
     h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
   }
   s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
