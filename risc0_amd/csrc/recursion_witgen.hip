@@ -5,7 +5,11 @@
 //   1. exec: step_exec over the work cycles (generated, gen/rwitgen/witgen_exec.hip), one
 //      lane per run of cycles — a run starts at cycle 0 or at a parallel-safe cycle and takes
 //      the following cycles that are not (MachineContext::parStepExec). Each cycle appends
-//      its WOM argument rows (addr, value) to its own slots.
+//      its WOM argument rows (addr, value) to its own slots. Runs are independent, so they
+//      are bucketed by major (the one-hot selector among control columns 1..7 shared by all
+//      of a run's cycles; bucket 8 for runs of several majors without the MACRO block; else
+//      bucket 0) and each bucket runs a step specialised to it: one register allocation per
+//      bucket instead of the union of all majors.
 //   2. verifyWom (ffi.cpp:118-135): the rows sorted as WomArgumentRow::operator< orders them
 //      (address, then the value's elements as field integers) — five stable LSD radix passes
 //      over 32-bit keys carrying a permutation; the per-cycle row counts exclusive-scanned
@@ -41,6 +45,44 @@ __global__ __launch_bounds__(kT) void row_key_kernel(const uint32_t* rows, const
   if (i >= n) return;
   const uint32_t* r = rows + uint64_t(perm[i]) * kRowWords;
   key[i] = pass == 4 ? r[0] : mont_reduce(r[4 - pass]);
+}
+
+// bucket of each run: the major m in 1..7 when every cycle of the run has control column m
+// equal to one and the other selectors zero; 8 when the cycles have different majors of that
+// form, none of them column 2 (the MACRO block, which alone needs 512 VGPRs and scratch); else
+// 0 (the generic step). Counts per bucket.
+constexpr uint32_t kBuckets = 9;
+__global__ __launch_bounds__(kT) void run_key_kernel(const uint32_t* ctrl, uint32_t steps, const uint32_t* run_start,
+                                                    uint32_t nruns, uint32_t* key, uint32_t* idx, uint32_t* counts) {
+  __shared__ uint32_t h[kBuckets];
+  if (threadIdx.x < kBuckets) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t r = blockIdx.x * kT + threadIdx.x;
+  if (r < nruns) {
+    uint32_t k = 0xFFu;
+    bool valid = true, macro = false;
+    for (uint32_t c = run_start[r]; c < run_start[r + 1]; c++) {
+      uint32_t m = 0, n = 0;
+      for (uint32_t j = 1; j <= 7; j++) {
+        const uint32_t v = ctrl[uint64_t(j) * steps + c];
+        if (v != 0u) {
+          n++;
+          m = v == kOne ? j : 0u;
+        }
+      }
+      const uint32_t cm = n == 1 ? m : 0u;
+      valid = valid && cm != 0u;
+      macro = macro || cm == 2u;
+      k = k == 0xFFu ? cm : (k == cm ? k : 8u);
+    }
+    if (!valid) k = 0u;
+    else if (k == 8u && macro) k = 0u;
+    key[r] = k;
+    idx[r] = r;
+    atomicAdd(&h[k], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < kBuckets && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
 }
 
 __global__ __launch_bounds__(kT) void iota_kernel(uint32_t* p, uint32_t n) {
@@ -143,7 +185,28 @@ void recursion_witgen(hipStream_t s, const uint32_t* ctrl, uint32_t* data, uint3
   A.err = err.p;
   {
     KScope ks("recursion_witgen_exec", double(ncycles) * 4 * (23 + 2 * 128));
-    recursion_witgen_exec(s, A);
+    // runs bucketed by major (radix sort on the 4-bit key), one specialised launch per bucket
+    uint32_t* key = static_cast<uint32_t*>(scratch(size_t(nruns) * 4, kSlotWitgenRunKey));
+    uint32_t* idx = static_cast<uint32_t*>(scratch(size_t(nruns) * 4, kSlotWitgenRunKey + 1));
+    uint32_t* key2 = static_cast<uint32_t*>(scratch(size_t(nruns) * 4, kSlotWitgenRunKey + 2));
+    uint32_t* idx2 = static_cast<uint32_t*>(scratch(size_t(nruns) * 4, kSlotWitgenRunKey + 3));
+    DevBuf counts(kBuckets);
+    HIP_OK(hipMemsetD32Async(counts.p, 0, kBuckets, s));
+    hipLaunchKernelGGL(run_key_kernel, dim3((nruns + kT - 1) / kT), dim3(kT), 0, s, ctrl, uint32_t(total_cycles),
+                       d_runs, nruns, key, idx, counts.p);
+    size_t sort_bytes = 0;
+    HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, key, key2, idx, idx2, int(nruns), 0, 4, s));
+    void* sort_temp = scratch(sort_bytes + 256, kSlotWitgenRunTemp);
+    HIP_OK(hipcub::DeviceRadixSort::SortPairs(sort_temp, sort_bytes, key, key2, idx, idx2, int(nruns), 0, 4, s));
+    uint32_t h_counts[kBuckets];
+    HIP_OK(hipMemcpyAsync(h_counts, counts.p, sizeof(h_counts), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    uint32_t off = 0;
+    for (int k = 0; k < int(kBuckets); k++) {
+      recursion_witgen_exec(s, A, k, idx2 + off, h_counts[k]);
+      off += h_counts[k];
+    }
+    R0_REQUIRE(off == nruns, "recursion_witgen: run buckets do not cover the runs");
   }
   {
     // verifyWom: lexicographic sort of the argument rows (five stable radix passes)

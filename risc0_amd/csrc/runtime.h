@@ -99,6 +99,8 @@ enum ScratchSlot : int {
   kSlotWitgenRuns = 72,
   kSlotWitgenIopIdx = 73,
   kSlotWitgenTemp = 74,
+  kSlotWitgenRunKey = 88,  // .. 91: run keys and indices, sorted
+  kSlotWitgenRunTemp = 92,
   // rv32im witness generation (rv32im_witgen.hip): the uploaded preflight trace, the cycle
   // lists per instruction arm, the lookup tables and the error record
   kSlotRvwgCycles = 75,

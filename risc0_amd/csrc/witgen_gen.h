@@ -109,7 +109,9 @@ __device__ __forceinline__ void iop_body(const WitgenArgs& A, uint32_t cycle, ui
 
 }  // namespace rwg
 
-void recursion_witgen_exec(hipStream_t s, const rwg::WitgenArgs& A);
+// step_exec over runs[0, n) (indices into A.run_start); maj 1..7: every cycle of those runs has
+// major selector column maj (rwg::exec_kernel<maj>), 8: majors other than column 2, 0: any runs
+void recursion_witgen_exec(hipStream_t s, const rwg::WitgenArgs& A, int maj, const uint32_t* runs, uint32_t n);
 void recursion_witgen_verify(hipStream_t s, const rwg::WitgenArgs& A);
 
 }  // namespace r0
