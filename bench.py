@@ -416,7 +416,7 @@ def kernel_roofline(r, args, prove):
     r.set_kernel_timing(False)
     if not times:
         return None
-    name, (ms, calls, alg_bytes, _alg_mm) = max(times.items(), key=lambda kv: kv[1][0])
+    name, (ms, calls, alg_bytes, alg_mm) = max(times.items(), key=lambda kv: kv[1][0])
     print(json.dumps({"kernel_times_ms": {k: [round(v[0], 3), v[1]] for k, v in times.items()}}), file=sys.stderr)
     avg_s = ms / 1000.0 / calls
     per_launch = alg_bytes / calls
@@ -440,6 +440,14 @@ def kernel_roofline(r, args, prove):
     else:
         out = {"kernel": name, "bound": "hbm", **hbm}
     out.update({"traffic": traffic, "alg_bytes_per_launch": int(per_launch), "avg_launch_ms": round(avg_s * 1000, 4)})
+    if alg_mm:
+        # the program's field multiplications (as the reference's poly_fp writes them) per second,
+        # against the issue roof spent on canonical Montgomery products (5 VALU instructions each);
+        # above 1 where the kernels need fewer instructions per product (lazy and fused sums)
+        tps = alg_mm / calls / avg_s / 1e12
+        peak = VALU_PEAK_GIPS * 64 / 5 / 1e3
+        out["alg_modmul"] = {"per_launch": int(alg_mm / calls), "achieved": round(tps, 3), "canonical_peak": round(peak, 3),
+                             "unit": "T modmul/s", "frac": round(tps / peak, 4)}
     if out["bound"] != "hbm":
         out["hbm"] = hbm
     if tsrc:
