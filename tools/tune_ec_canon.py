@@ -45,7 +45,9 @@ def build(circuit):
 
 def measure():
     os.makedirs(OUT, exist_ok=True)
-    for name in VARIANTS:
+    # the committed build (copied to libr0hip_tuned.so) is measured in the same run when present
+    names = list(VARIANTS) + (["tuned"] if os.path.exists(os.path.join(VAR, "libr0hip_tuned.so")) else [])
+    for name in names:
         lib = os.path.join(VAR, f"libr0hip_{name}.so")
         env = dict(os.environ, R0HIP_LIB=lib, TMPDIR="/tmp", R0_EC_CIRCUIT=CIRCUIT)
         subprocess.run(["timeout", "-k", "10", "200", "rocprofv3", "--kernel-trace", "--stats", "-d",
