@@ -293,12 +293,10 @@ void run_eval_check(const CircuitDef& c, uint32_t* check, const uint32_t* const*
       return t ? uint32_t(strtoul(t, nullptr, 0)) : 0u;
     }();
     e.tile = tile_env;
-    // R0_EC_WIDE (experiments): mask of the kernels that take the column-base tap form
-    static const int64_t wide_env = [] {
-      const char* t = getenv("R0_EC_WIDE");
-      return t ? int64_t(strtoull(t, nullptr, 0)) : int64_t(-1);
-    }();
-    e.wide = wide_env;
+    // R0_EC_WIDE (experiments, tests): mask of the kernels that take the column-base tap form,
+    // read on every call
+    const char* wide_env = getenv("R0_EC_WIDE");
+    e.wide = wide_env ? int64_t(strtoull(wide_env, nullptr, 0)) : int64_t(-1);
   }
   double bytes = 16.0 * domain;
   for (int g = 0; g < 3; g++) bytes += 4.0 * domain * c.group_sizes[g];

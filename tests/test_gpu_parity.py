@@ -400,6 +400,31 @@ def test_eval_check(hal, oracle, circuit, po2):
     assert np.array_equal(out.to_numpy(), ref)
 
 
+@pytest.mark.parametrize("circuit", ["rv32im", "recursion"])
+@pytest.mark.parametrize("wide", ["0", "0xffffffff"])
+def test_eval_check_both_tap_forms(hal, oracle, circuit, wide, monkeypatch):
+    """Every generated kernel is built with 32-bit tap indices and with column base pointers;
+    the tuning file picks one per kernel below po2=24 (the other runs only if R0_EC_WIDE asks
+    for it), so both forms of every kernel are checked against the compiled poly_fp here."""
+    if oracle.ref_lib() is None:
+        pytest.skip("oracle/_ref not built")
+    monkeypatch.setenv("R0_EC_WIDE", wide)
+    po2 = 6
+    d = oracle.load_circuit_json(circuit)
+    rng = np.random.default_rng(77)
+    D = 4 << po2
+    gs = d["group_sizes"]
+    groups = [oracle.rand_elems(rng, gs[g] * D) for g in range(3)]
+    mix = oracle.rand_elems(rng, d["mix_size"])
+    glob = oracle.rand_elems(rng, d["output_size"])
+    pm = oracle.rand_elems(rng, 4)
+    ref = np.zeros(4 * D, np.uint32)
+    oracle.eval_check(circuit, ref, groups, mix, glob, pm, po2)
+    out = hal.alloc_elem("check", 4 * D)
+    hal.eval_check(circuit, out, [dev(hal, g) for g in groups], dev(hal, mix), dev(hal, glob), pm, po2)
+    assert np.array_equal(out.to_numpy(), ref)
+
+
 @pytest.mark.parametrize("circuit,suite,po2", [("rv32im", "poseidon2", 8), ("rv32im", "poseidon2", 11),
                                                ("rv32im", "sha-256", 9), ("recursion", "poseidon2", 9),
                                                ("recursion", "sha-256", 8), ("recursion", "poseidon_254", 8),
