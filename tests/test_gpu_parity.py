@@ -733,7 +733,10 @@ def test_steady_state_proving_makes_no_hipmalloc(oracle):
     version = 2 if case["circuit"] == "rv32im" else None
     seals = {}
     # start from a clean pool: blocks other tests' threads left (other sizes) would be
-    # matched up to 25% larger in whatever order threads race for them
+    # matched up to 25% larger in whatever order threads race for them. Those threads hand
+    # their blocks back from thread-exit destructors, after their joins returned: wait for
+    # that first, or blocks of other sizes land in the pool mid-test
+    time.sleep(1.0)
     r.trim()
 
     def batch(tag):
