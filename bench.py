@@ -90,7 +90,17 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo", init_method="env://")
+        # gloo reports its connections on the C++ stdout ("[Gloo] Rank 0 is connected ..."):
+        # send that to stderr, so stdout carries only rank 0's JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", init_method="env://")
+            dist.barrier()
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
     import risc0_amd as r
     with open(os.path.join(ROOT, "risc0_amd", "circuits", args.circuit + ".taps.json")) as f:
         circ = json.load(f)
