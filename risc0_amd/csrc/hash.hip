@@ -86,6 +86,39 @@ __global__ __launch_bounds__(kThreads) void p2_fold_kernel(uint32_t* io, uint64_
   store_digest(io + (out_off + i) * 8, c);
 }
 
+// Wide layers, two nodes per lane: lane i hashes node i, then node i + m (m = ceil(n/2)), whose
+// two child digests are loaded before the first permutation, so those loads are in flight
+// while it runs (one node per lane waits for its loads with nothing to overlap them).
+__global__ __launch_bounds__(kThreads) void p2_fold2_kernel(uint32_t* io, uint64_t in_off, uint64_t out_off,
+                                                          uint64_t n) {
+  const uint64_t m = (n + 1) / 2;
+  const uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
+  if (i >= m) return;
+  const uint64_t j = i + m;
+  const bool two = j < n;
+  const uint4* s1 = reinterpret_cast<const uint4*>(io + (in_off + 2 * i) * 8);
+  uint4 a = s1[0], b = s1[1], d = s1[2], e = s1[3];
+  uint4 a2 = make_uint4(0, 0, 0, 0), b2 = a2, d2 = a2, e2 = a2;
+  if (two) {
+    const uint4* s2 = reinterpret_cast<const uint4*>(io + (in_off + 2 * j) * 8);
+    a2 = s2[0], b2 = s2[1], d2 = s2[2], e2 = s2[3];
+  }
+  uint32_t c[24];
+  c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w; c[4] = b.x; c[5] = b.y; c[6] = b.z; c[7] = b.w;
+  c[8] = d.x; c[9] = d.y; c[10] = d.z; c[11] = d.w; c[12] = e.x; c[13] = e.y; c[14] = e.z; c[15] = e.w;
+#pragma unroll
+  for (int k = 16; k < 24; k++) c[k] = 0;
+  poseidon2_mix(c);
+  store_digest(io + (out_off + i) * 8, c);
+  if (!two) return;
+  c[0] = a2.x; c[1] = a2.y; c[2] = a2.z; c[3] = a2.w; c[4] = b2.x; c[5] = b2.y; c[6] = b2.z; c[7] = b2.w;
+  c[8] = d2.x; c[9] = d2.y; c[10] = d2.z; c[11] = d2.w; c[12] = e2.x; c[13] = e2.y; c[14] = e2.z; c[15] = e2.w;
+#pragma unroll
+  for (int k = 16; k < 24; k++) c[k] = 0;
+  poseidon2_mix(c);
+  store_digest(io + (out_off + j) * 8, c);
+}
+
 // Small layers: four lanes per node (poseidon2_mix_quad), so a layer of n nodes keeps 4n
 // lanes busy. Lane q loads cells 4j + q (j < 4) of the two child digests and stores
 // digest words q and 4 + q.
@@ -395,6 +428,12 @@ static uint32_t quad_top_max() {
   return v;
 }
 
+// wide Poseidon2 layers two nodes per lane (R0_P2_FOLD_TWO=0: one)
+static bool fold_two() {
+  static const bool v = env_size("R0_P2_FOLD_TWO", 1) != 0;
+  return v;
+}
+
 void hash_fold(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t output_size) {
   if (output_size == 0) return;
   R0_REQUIRE(input_size == 2 * output_size, "hash_fold: input_size != 2*output_size");
@@ -403,6 +442,8 @@ void hash_fold(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t
   const uint64_t in = input_size, out = output_size;
   if (suite == 0 && output_size <= quad_fold_max())
     hipLaunchKernelGGL(p2_fold_quad_kernel, dim3(div_up(4 * output_size, kThreads)), block, 0, s, io, in, out, out);
+  else if (suite == 0 && fold_two())
+    hipLaunchKernelGGL(p2_fold2_kernel, dim3(div_up((output_size + 1) / 2, kThreads)), block, 0, s, io, in, out, out);
   else if (suite == 0)
     hipLaunchKernelGGL(p2_fold_kernel, grid, block, 0, s, io, in, out, out);
   else if (suite == 1)
