@@ -12,7 +12,7 @@ import sys
 FAMILIES = [
     (r"ec_rv32im::k\d+|ec_recursion::k\d+", "eval_check"),
     (r"p2_rows_kernel|sha_rows_kernel", "hash_rows"),
-    (r"p2_fold_kernel|p2_fold_quad_kernel|sha_fold_kernel|fold_top_kernel|p254_fold_kernel", "merkle_fold"),
+    (r"p2_fold_kernel|p2_fold2_kernel|p2_fold_quad_kernel|sha_fold_kernel|fold_top_kernel|p254_fold_kernel", "merkle_fold"),
     (r"ntt_pass_kernel<false", "ntt_evaluate"),
     (r"ntt_pass_kernel<true", "ntt_interpolate"),
     (r"bit_reverse", "bit_reverse"),
