@@ -232,7 +232,7 @@ def test_hash_rows(hal, hal_sha, oracle, suite):
     h, s = H(suite), S(oracle, suite)
     rng = np.random.default_rng(11)
     shapes = [(r, c) for r in (1, 2, 3, 4, 10) for c in (16, 32, 64, 128)]
-    shapes += [(4096, 1), (4096, 211), (1000, 103), (257, 17), (1 << 16, 16)]
+    shapes += [(4096, 1), (4096, 211), (1000, 103), (257, 17), (1 << 16, 16), (4097, 1), (1001, 12), (513, 16)]
     for rows, cols in shapes:
         m = oracle.rand_elems(rng, rows * cols)
         out = h.alloc_digest("out", rows)

@@ -54,6 +54,20 @@ def main():
         for k, (ms, calls, b, _mm) in sorted(r.kernel_times().items()):
             print(f"{k:28s} {ms / calls:9.3f} ms/launch")
         return
+    if "rows" in which:
+        # leaf rows of the narrow groups: 16 columns (check) and 1 column at 2^22 rows
+        D = 4 << 20
+        for c in (16, 1):
+            m = hal.copy_from_elem(f"m{c}", rng.integers(0, P, c * D, dtype=np.uint64).astype(np.uint32))
+            d = hal.alloc_digest(f"d{c}", D)
+            r.set_kernel_timing(True)
+            for _ in range(5):
+                hal.hash_rows(d, m)
+            hal.synchronize()
+            for k, (ms, calls, b, _mm) in sorted(r.kernel_times().items()):
+                print(f"cols={c:2d} {k:28s} {ms / calls:9.3f} ms/launch")
+            r.set_kernel_timing(False)
+        return
     cols, po2 = 211, 20
     n = 1 << po2
     inp = hal.copy_from_elem("in", rng.integers(0, P, cols * n, dtype=np.uint64).astype(np.uint32))
