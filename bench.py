@@ -474,20 +474,41 @@ def lib_fingerprint():
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
+def pmc_summary_file(kind):
+    """the committed PMC summary to quote (profiles/r<round><tag>_pmc_<kind>.json): the newest one
+    measured on the loaded library (its lib_sha256_16), else the newest. Round tags order by
+    round, then tag length, then tag (r5z < r5aa < r5an), not as plain strings."""
+    import glob
+    import re
+
+    def key(path):
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{kind}.json")), key=key)
+    if not files:
+        return None
+    lib = lib_fingerprint()
+    for path in reversed(files):
+        with open(path) as f:
+            if json.load(f).get("lib_sha256_16") == lib:
+                return path
+    return files[-1]
+
+
 def pmc_valu(family, args):
     """VALU instructions per launch of `family` and the time-weighted share of SIMD cycles
     issuing VALU, from the newest committed rocprofv3 --pmc summary of this bench
     (profiles/r*_pmc_valu.json, tools/pmc_summary.py). PMC counters cannot be read inside
     the timed process, so these are the committed measurement, labelled by file."""
-    import glob
     if args.circuit != "rv32im" or args.po2 != 20 or args.hashfn != "poseidon2":
         return None, None, None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_valu.json")))
-    if not files:
+    path = pmc_summary_file("valu")
+    if path is None:
         return None, None, None
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from rocprof_families import family as fam_of
-    with open(files[-1]) as f:
+    with open(path) as f:
         doc = json.load(f)
     ks = doc["kernels"]
     matches = doc.get("lib_sha256_16") == lib_fingerprint()
@@ -505,7 +526,7 @@ def pmc_valu(family, args):
         insts = None  # launches per proof differ per kernel: only eval_check is quoted per launch
     if tot == 0:
         return None, None, None
-    return insts, round(busy / tot, 3), (os.path.relpath(files[-1], ROOT), matches)
+    return insts, round(busy / tot, 3), (os.path.relpath(path, ROOT), matches)
 
 
 def mixed_arm_rows(data, n):
@@ -633,17 +654,16 @@ def pmc_traffic(family, calls, args):
     (profiles/r*_pmc_traffic.json, FETCH_SIZE/WRITE_SIZE passes of this same bench
     command, gfx950-corrected by tools/pmc_traffic.py). PMC counters cannot be read from
     inside the timed process, so the value is the committed measurement, labelled."""
-    import glob
     if args.circuit != "rv32im" or args.po2 != 20 or args.hashfn != "poseidon2":
         return None, None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
-    if not files:
+    path = pmc_summary_file("traffic")
+    if path is None:
         return None, None
-    with open(files[-1]) as f:
+    with open(path) as f:
         d = json.load(f)["per_proof"].get(family)
     if not d:
         return None, None
-    return int((d["read_bytes"] + d["write_bytes"]) / calls), os.path.relpath(files[-1], ROOT)
+    return int((d["read_bytes"] + d["write_bytes"]) / calls), os.path.relpath(path, ROOT)
 
 
 def host_cores():
