@@ -403,8 +403,8 @@ HBM_PEAK_GBS = 8000.0
 # Chip VALU issue roof in wave64 instructions/s: 256 CUs x 4 SIMDs, one wave64 instruction
 # per 4 cycles per SIMD at 2.4 GHz. That is the measured issue cost of the 32-bit integer
 # VOP3 ops these kernels are made of (v_mad_u64_u32, v_mul_lo_u32, v_min_u32, v_lshl_add_u64:
-# 29-34 T lane-instructions/s in profiles/r1_valu_rates.txt) and the unit SQ_ACTIVE_INST_VALU
-# counts in (ACTIVE_INST_VALU x 4 = SQ_INSTS_VALU exactly, profiles/r2a_pmc_valu.json).
+# 29-34 T lane-instructions/s in profiles/archive/r1_valu_rates.txt) and the unit SQ_ACTIVE_INST_VALU
+# counts in (ACTIVE_INST_VALU x 4 = SQ_INSTS_VALU exactly, profiles/archive/r2a_pmc_valu.json).
 VALU_PEAK_GIPS = 256 * 4 * 2.4e9 / 4 / 1e9
 # The binding resource of each launcher family: the hash, eval_check and
 # evaluate_any kernels are integer-VALU-issue bound; the NTT/eltwise ones move bytes.

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Load density of each rv32im eval_check kernel (tap loads + materialised reads per unit of
 the generator's VALU cost model) against its measured VALU issue share
-(profiles/r3t_pmc_valu.txt): does the load density predict which kernels stall?
+(profiles/archive/r3t_pmc_valu.txt): does the load density predict which kernels stall?
 (a load-aware split.)
 
   model_ec_loads.py [BUDGET] > profiles/r4_ec_load_density.txt
@@ -23,7 +23,7 @@ def main():
     pg.mat = set(G.mat_config("rv32im", budget))
     _, kernels = G.schedule(pg, budget)
     valu = {}
-    for line in open(os.path.join(ROOT, "profiles", "r3t_pmc_valu.txt")):
+    for line in open(os.path.join(ROOT, "profiles", "archive", "r3t_pmc_valu.txt")):
         m = re.match(r"ec_rv32im::k(\d+)<false>\s+([\d.]+)\s+(\d+)\s+([\d.]+)\s+([\d.]+)", line)
         if m:
             valu[int(m.group(1))] = (float(m.group(2)) / int(m.group(3)), float(m.group(5)))
