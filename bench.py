@@ -25,6 +25,14 @@ import time
 
 import numpy as np
 
+# HIP hardware queues per process, read once when the runtime starts (before anything here
+# touches a GPU): the pipeline keeps five streams busy (the uploader's, three provers', the main
+# thread's), and on the runtime's default of 4 two of them share a queue, whose kernels then
+# run in order. 8 queues: 53.3 against 54.9 ms per segment on one box
+# (profiles/r5aq_hwq_sweep.txt); a larger value in the environment is kept.
+if int(os.environ.get("GPU_MAX_HW_QUEUES") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -368,6 +376,7 @@ def main():
             "config": {"workload": workload,
                        "circuit": args.circuit, "po2": args.po2, "hashfn": args.hashfn,
                        "segments_per_gpu": args.steps, "segments_in_flight_per_gpu": k,
+                       "hip_hw_queues_per_process": int(os.environ["GPU_MAX_HW_QUEUES"]),
                        "parallelism": f"segment-per-gpu x{world}",
                        "seal_sha256_by_rank": [digests[i] for i in range(world)],
                        **({"guest": args.guest, "distinct_traces_per_rank": len(traces),
