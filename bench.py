@@ -26,9 +26,9 @@ import time
 import numpy as np
 
 # HIP hardware queues per process, read once when the runtime starts (before anything here
-# touches a GPU): the pipeline keeps five streams busy (the uploader's, three provers', the main
-# thread's), and on the runtime's default of 4 two of them share a queue, whose kernels then
-# run in order. 8 queues: 53.3 against 54.9 ms per segment on one box
+# touches a GPU): the process holds five streams (the uploader's, three provers', the main
+# thread's), and at the runtime's default of 4 some of them share a queue, which runs its
+# kernels in order. 8 queues: 53.3 against 54.9 ms per segment on one box
 # (profiles/r5aq_hwq_sweep.txt); a larger value in the environment is kept.
 if int(os.environ.get("GPU_MAX_HW_QUEUES") or 0) < 8:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
