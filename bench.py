@@ -30,7 +30,7 @@ import numpy as np
 # thread's), and at the runtime's default of 4 some of them share a queue, which runs its
 # kernels in order. 8 queues: 53.3 against 54.9 ms per segment on one box
 # (profiles/r5aq_hwq_sweep.txt); a larger value in the environment is kept.
-if int(os.environ.get("GPU_MAX_HW_QUEUES") or 0) < 8:
+if os.environ.get("R0_BENCH_HW_QUEUES_AS_IS") != "1" and int(os.environ.get("GPU_MAX_HW_QUEUES") or 0) < 8:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
