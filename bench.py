@@ -26,11 +26,11 @@ import time
 import numpy as np
 
 # HIP hardware queues per process, read once when the runtime starts (before anything here
-# touches a GPU). Streams that share a queue run their kernels in order: 8 queues took the
-# pipeline from 54.9 to 53.3 ms per segment (profiles/r5aq_hwq_sweep.txt) while it held five
-# streams; since one prover runs on the calling thread (four streams at 3 in flight) the
-# runtime's default 4 is as fast (r5ay_caller_prover_ab.txt), and 8 leaves room for --inflight 4+.
-# A larger value in the environment is kept.
+# touches a GPU): the process holds five streams (the uploader's, three provers', the main
+# thread's), and at the runtime's default of 4 some of them share a queue, which runs its
+# kernels in order. 8 queues: 53.3 against 54.9 ms per segment on one box
+# (profiles/r5aq_hwq_sweep.txt); a larger value in the environment is kept
+# (R0_BENCH_HW_QUEUES_AS_IS=1 keeps any value, for A/B runs).
 if os.environ.get("R0_BENCH_HW_QUEUES_AS_IS") != "1" and int(os.environ.get("GPU_MAX_HW_QUEUES") or 0) < 8:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 

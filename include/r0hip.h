@@ -293,9 +293,9 @@ const char* r0hip_prove_recursion(int suite, uint32_t po2, const uint32_t* d_ctr
 /* ---- segment pipeline (r0vm's per-GPU worker queue, r0vm/src/actors/worker.rs:75-76, over the
  * zkvm's per-segment prove loop, zkvm/src/host/server/prove/prover_impl.rs:84-94) ----
  * Proves njobs segments of one (circuit, suite, po2) from HOST inputs: an uploader thread copies
- * each job's inputs into one of in_flight+1 device buffer sets while in_flight provers (the
- * calling thread, in_flight-1 threads) prove on their own streams. Host buffers must stay valid
- * until the call returns, page-locked (r0hip_host_alloc) for full PCIe rate. Per job: seal into h_seal (seal_cap words),
+ * each job's inputs into one of in_flight+1 device buffer sets while in_flight prover threads
+ * prove on their own streams. Host buffers must stay valid until the call returns and should be
+ * page-locked (r0hip_host_alloc) for full PCIe rate. Per job: seal into h_seal (seal_cap words),
  * its length in seal_len, mix values into h_mix_out (optional), and error = NULL or a malloc'd
  * message (free() it). Returns NULL when every job succeeded.
  * Two job forms, one per call (all jobs of a call take the same form):

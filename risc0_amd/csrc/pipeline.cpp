@@ -110,22 +110,6 @@ struct Queue {
   }
 };
 
-// k provers: k - 1 threads and the calling thread, whose stream the process already holds, so
-// a call keeps k + 1 streams busy (the uploader's and the provers') and the runtime's default 4
-// hardware queues give each its own for k <= 3 (a shared queue runs its streams' kernels in
-// order). R0_PIPE_CALLER_PROVES=0: k prover threads (the calling thread only waits).
-template <typename F>
-void run_provers(size_t k, F& prover) {
-  static const bool caller = [] {
-    const char* e = getenv("R0_PIPE_CALLER_PROVES");
-    return !e || strtoul(e, nullptr, 10) != 0;
-  }();
-  std::vector<std::thread> threads;
-  for (size_t t = caller ? 1 : 0; t < k; t++) threads.emplace_back(prover);
-  if (caller) prover();  // returns at its stop token; never throws (errors are per job)
-  for (auto& t : threads) t.join();
-}
-
 char* dup_msg(const char* m) {
   size_t n = strlen(m) + 1;
   char* p = static_cast<char*>(malloc(n));
@@ -238,48 +222,51 @@ const char* prove_trace_jobs(int suite, uint32_t po2, r0hip_segment_job* jobs, s
     for (size_t t = 0; t < k; t++) ready_q.put(-1);
   });
 
-  auto prover = [&] {
-    for (;;) {
-      long s = ready_q.get();
-      if (s < 0) return;
-      TraceSet& b = sets[s];
-      r0hip_segment_job& j = jobs[b.job];
-      const r0hip_trace_input& tr = *j.trace;
-      try {
-        ensure_init();
-        r0hip_raw_preflight_trace pf = tr.preflight;  // the set's device copies
-        pf.cycles = b.cycles.p;
-        pf.txns = pf.txns_len ? b.txns.p : nullptr;
-        pf.bigint_bytes = pf.bigint_bytes_len ? reinterpret_cast<const uint8_t*>(b.bigint.p) : nullptr;
-        std::vector<uint32_t> mix;
-        std::vector<uint32_t> seal = prove_trace(
-            suite, po2, tr.mode, b.glob.p, b.index.p, tr.inj_rows, b.offsets.p, b.values.p, &pf, j.h_bigint,
-            j.n_bigint, true, &mix, [&](hipStream_t st) {
-              b.wait_landed();
-              {
-                std::lock_guard<std::mutex> lk(b.mu);
-                if (j.error) throw std::runtime_error(j.error);
-              }
-              HIP_OK(hipStreamWaitEvent(st, b.ev, 0));
-            });
-        HIP_OK(hipStreamSynchronize(stream()));
-        j.seal_len = seal.size();
-        if (j.h_mix_out) memcpy(j.h_mix_out, mix.data(), mix.size() * 4);
-        R0_REQUIRE(!j.h_seal || seal.size() <= j.seal_cap, "seal buffer too small");
-        if (j.h_seal) memcpy(j.h_seal, seal.data(), seal.size() * 4);
-      } catch (const std::exception& e) {
-        {
-          std::lock_guard<std::mutex> lk(b.mu);
-          if (!j.error) j.error = dup_msg(e.what());
+  std::vector<std::thread> provers;
+  for (size_t t = 0; t < k; t++) {
+    provers.emplace_back([&] {
+      for (;;) {
+        long s = ready_q.get();
+        if (s < 0) return;
+        TraceSet& b = sets[s];
+        r0hip_segment_job& j = jobs[b.job];
+        const r0hip_trace_input& tr = *j.trace;
+        try {
+          ensure_init();
+          r0hip_raw_preflight_trace pf = tr.preflight;  // the set's device copies
+          pf.cycles = b.cycles.p;
+          pf.txns = pf.txns_len ? b.txns.p : nullptr;
+          pf.bigint_bytes = pf.bigint_bytes_len ? reinterpret_cast<const uint8_t*>(b.bigint.p) : nullptr;
+          std::vector<uint32_t> mix;
+          std::vector<uint32_t> seal = prove_trace(
+              suite, po2, tr.mode, b.glob.p, b.index.p, tr.inj_rows, b.offsets.p, b.values.p, &pf, j.h_bigint,
+              j.n_bigint, true, &mix, [&](hipStream_t st) {
+                b.wait_landed();
+                {
+                  std::lock_guard<std::mutex> lk(b.mu);
+                  if (j.error) throw std::runtime_error(j.error);
+                }
+                HIP_OK(hipStreamWaitEvent(st, b.ev, 0));
+              });
+          HIP_OK(hipStreamSynchronize(stream()));
+          j.seal_len = seal.size();
+          if (j.h_mix_out) memcpy(j.h_mix_out, mix.data(), mix.size() * 4);
+          R0_REQUIRE(!j.h_seal || seal.size() <= j.seal_cap, "seal buffer too small");
+          if (j.h_seal) memcpy(j.h_seal, seal.data(), seal.size() * 4);
+        } catch (const std::exception& e) {
+          {
+            std::lock_guard<std::mutex> lk(b.mu);
+            if (!j.error) j.error = dup_msg(e.what());
+          }
+          drain_after_error();  // kernels queued before the throw may still read this set
         }
-        drain_after_error();  // kernels queued before the throw may still read this set
+        b.wait_landed();  // the uploader is done with this job before the set is refilled
+        free_q.put(s);
       }
-      b.wait_landed();  // the uploader is done with this job before the set is refilled
-      free_q.put(s);
-    }
-  };
-  run_provers(k, prover);
+    });
+  }
   uploader.join();
+  for (auto& t : provers) t.join();
   for (size_t i = 0; i < njobs; i++)
     if (jobs[i].error) return dup_msg((std::string("segment ") + std::to_string(i) + ": " + jobs[i].error).c_str());
   return nullptr;
@@ -403,48 +390,51 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
       for (size_t t = 0; t < k; t++) ready_q.put(-1);  // one stop token per prover
     });
 
-    auto prover = [&] {
-      for (;;) {
-        long s = ready_q.get();
-        if (s < 0) return;
-        BufSet& b = sets[s];
-        r0hip_segment_job& j = jobs[b.job];
-        // j.error is written by the uploader under b.mu while this job's copies are queued
-        auto failed = [&] {
-          std::lock_guard<std::mutex> lk(b.mu);
-          return j.error != nullptr;
-        };
-        if (!failed()) {
-          try {
-            ensure_init();
-            std::vector<uint32_t> mix;
-            const bool dev_accum = !j.h_accum;  // (rv32im only: checked by the uploader)
-            const AccumStep acc{b.g[2].p, n, true, j.h_bigint, j.n_bigint};
-            std::vector<uint32_t> seal =
-                prove_segment(*c, suite, po2, b.g[0].p, b.g[1].p, dev_accum ? nullptr : b.g[2].p, b.g[3].p,
-                              write_version != 0, version, &mix, &b, dev_accum ? &acc : nullptr);
-            HIP_OK(hipStreamSynchronize(stream()));
-            if (!failed()) {  // an upload error leaves the proof meaningless: drop it
-              j.seal_len = seal.size();
-              if (j.h_mix_out) memcpy(j.h_mix_out, mix.data(), mix.size() * 4);
-              R0_REQUIRE(!j.h_seal || seal.size() <= j.seal_cap, "seal buffer too small");
-              if (j.h_seal) memcpy(j.h_seal, seal.data(), seal.size() * 4);
+    std::vector<std::thread> provers;
+    for (size_t t = 0; t < k; t++) {
+      provers.emplace_back([&] {
+        for (;;) {
+          long s = ready_q.get();
+          if (s < 0) return;
+          BufSet& b = sets[s];
+          r0hip_segment_job& j = jobs[b.job];
+          // j.error is written by the uploader under b.mu while this job's copies are queued
+          auto failed = [&] {
+            std::lock_guard<std::mutex> lk(b.mu);
+            return j.error != nullptr;
+          };
+          if (!failed()) {
+            try {
+              ensure_init();
+              std::vector<uint32_t> mix;
+              const bool dev_accum = !j.h_accum;  // (rv32im only: checked by the uploader)
+              const AccumStep acc{b.g[2].p, n, true, j.h_bigint, j.n_bigint};
+              std::vector<uint32_t> seal =
+                  prove_segment(*c, suite, po2, b.g[0].p, b.g[1].p, dev_accum ? nullptr : b.g[2].p, b.g[3].p,
+                                write_version != 0, version, &mix, &b, dev_accum ? &acc : nullptr);
+              HIP_OK(hipStreamSynchronize(stream()));
+              if (!failed()) {  // an upload error leaves the proof meaningless: drop it
+                j.seal_len = seal.size();
+                if (j.h_mix_out) memcpy(j.h_mix_out, mix.data(), mix.size() * 4);
+                R0_REQUIRE(!j.h_seal || seal.size() <= j.seal_cap, "seal buffer too small");
+                if (j.h_seal) memcpy(j.h_seal, seal.data(), seal.size() * 4);
+              }
+            } catch (const std::exception& e) {
+              {
+                std::lock_guard<std::mutex> lk(b.mu);
+                if (!j.error) j.error = dup_msg(e.what());
+              }
+              // kernels queued before the throw may still read this buffer set: drain
+              // them before the uploader refills it
+              drain_after_error();
             }
-          } catch (const std::exception& e) {
-            {
-              std::lock_guard<std::mutex> lk(b.mu);
-              if (!j.error) j.error = dup_msg(e.what());
-            }
-            // kernels queued before the throw may still read this buffer set: drain
-            // them before the uploader refills it
-            drain_after_error();
           }
+          free_q.put(s);
         }
-        free_q.put(s);
-      }
-    };
-    run_provers(k, prover);
+      });
+    }
     uploader.join();
+    for (auto& t : provers) t.join();
     for (size_t i = 0; i < njobs; i++)
       if (jobs[i].error) return dup_msg((std::string("segment ") + std::to_string(i) + ": " + jobs[i].error).c_str());
     return nullptr;
