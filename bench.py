@@ -25,15 +25,6 @@ import time
 
 import numpy as np
 
-# HIP hardware queues per process, read once when the runtime starts (before anything here
-# touches a GPU): the process holds five streams (the uploader's, three provers', the main
-# thread's), and at the runtime's default of 4 some of them share a queue, which runs its
-# kernels in order. 8 queues: 53.3 against 54.9 ms per segment on one box
-# (profiles/r5aq_hwq_sweep.txt); a larger value in the environment is kept
-# (R0_BENCH_HW_QUEUES_AS_IS=1 keeps any value, for A/B runs).
-if os.environ.get("R0_BENCH_HW_QUEUES_AS_IS") != "1" and int(os.environ.get("GPU_MAX_HW_QUEUES") or 0) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -263,11 +254,19 @@ def main():
         out = {}
 
         def pipeline(jobs_):
-            out["res"] = r.prove_trace_segments(hal, args.po2, jobs_, in_flight=k)
+            # every seal checked by the native verifier beside the proofs (the worker unit returns
+            # only receipts that verified, prover_impl.rs:262-280); a failed check fails the bench
+            res = r.prove_trace_segments(hal, args.po2, jobs_, in_flight=k, per_job=True)
+            bad = [e for _, _, e, _ in res if e]
+            if bad:
+                raise RuntimeError(f"{len(bad)} of {len(res)} segments failed: {bad[0]}")
+            out["res"] = [(sl, m) for sl, m, _, _ in res]
+            out["verify_ms"] = [v for _, _, _, v in res]
         pipeline([tjobs[i % len(tjobs)] for i in range(max(args.warmup, k + 1))])  # warm every set, thread, pool
         _t, t = timed_segments(pipeline, [batch], 0, hal.synchronize, dist)
         seal, mix = out["res"][0]  # job 0 proved trace 0
         seals_distinct = len({sl.tobytes() for sl, _ in out["res"]})
+        verify_ms = sum(out["verify_ms"]) / len(out["verify_ms"])
         t0 = time.perf_counter()
         pipeline([tjobs[0]])
         t_one = time.perf_counter() - t0
@@ -321,7 +320,7 @@ def main():
     if rank == 0:
         prove_timed = ((lambda: r.prove_segment_trace_resident(hal, rt, bigint_records=bigint_records)) if trace_mode
                        else (lambda: prove_program(0, 0)) if program_mode else (lambda: prove_witness(0)))
-        roofline = kernel_roofline(r, args, prove_timed)
+        roofline = kernel_roofline(r, args, prove_timed, ms_per_step)
         # the side legs keep 2 in flight below po2 21 unless --inflight says otherwise: the
         # pipeline's uploader and a third prover measured slower there (63.1 against 57.6 ms)
         kl = k if args.inflight is not None else min(k, 2)
@@ -377,12 +376,14 @@ def main():
             "config": {"workload": workload,
                        "circuit": args.circuit, "po2": args.po2, "hashfn": args.hashfn,
                        "segments_per_gpu": args.steps, "segments_in_flight_per_gpu": k,
-                       "hip_hw_queues_per_process": int(os.environ["GPU_MAX_HW_QUEUES"]),
+                       # the runtime's default (4) unless the caller's environment sets another count
+                       "hip_hw_queues_per_process": int(os.environ.get("GPU_MAX_HW_QUEUES") or 4),
                        "parallelism": f"segment-per-gpu x{world}",
                        "seal_sha256_by_rank": [digests[i] for i in range(world)],
                        **({"guest": args.guest, "distinct_traces_per_rank": len(traces),
                            "distinct_seals_rank0": seals_distinct,
                            "h2d_bytes_per_segment": int(tjobs[0].h2d_bytes()),
+                           "receipts_verified": True, "verify_ms_per_segment": round(verify_ms, 2),
                            "ms_one_segment_unpipelined": round(1000.0 * t_one, 1)} if trace_mode else {}),
                        **({"programs_per_rank": len(progs), "seal_valid_rank0": bool(program_valid)}
                           if program_mode else {}),
@@ -421,7 +422,7 @@ VALU_PEAK_GIPS = 256 * 4 * 2.4e9 / 4 / 1e9
 VALU_BOUND = {"eval_check", "hash_rows", "merkle_fold", "batch_evaluate_any"}
 
 
-def kernel_roofline(r, args, prove):
+def kernel_roofline(r, args, prove, ms_per_step):
     """Time every kernel family of one proof with HIP events on the library stream
     (r0hip_kernel_times) and quote the dominant one against the resource that binds it:
     VALU instruction issue (SQ_INSTS_VALU per launch from the committed PMC pass of this
@@ -454,25 +455,80 @@ def kernel_roofline(r, args, prove):
                "valu_source_matches_library": vmatch,
                "note": "integer modular arithmetic bound by VALU issue: executed VALU instructions per launch "
                        "(PMC SQ_INSTS_VALU) over the launch time, against 1024 SIMDs x one wave64 instruction "
-                       "per 4 cycles at 2.4 GHz; VOP2 v_add/v_sub (about a quarter of eval_check's) can issue "
-                       "faster, so frac is an upper bound. issue_busy_frac is the same count over the SIMD "
-                       "cycles at the measured clock (SQ_ACTIVE_INST_VALU)"}
+                       "per 4 cycles at 2.4 GHz. Full-rate 32-bit ops issue in 2 cycles, so this frac is an upper "
+                       "bound: eval_check_issue prices each instruction at its own cost. issue_busy_frac is the "
+                       "same count over the SIMD cycles at the measured clock (SQ_ACTIVE_INST_VALU)"}
+        ec = ec_issue(args, avg_s, insts) if fam == "eval_check" else None
+        if ec:
+            out["eval_check_issue"] = ec
     else:
         out = {"kernel": name, "bound": "hbm", **hbm}
     out.update({"traffic": traffic, "alg_bytes_per_launch": int(per_launch), "avg_launch_ms": round(avg_s * 1000, 4)})
     if alg_mm:
-        # the program's field multiplications (as the reference's poly_fp writes them) per second,
-        # against the issue roof spent on canonical Montgomery products (5 VALU instructions each);
-        # above 1 where the kernels need fewer instructions per product (lazy and fused sums)
-        tps = alg_mm / calls / avg_s / 1e12
-        peak = VALU_PEAK_GIPS * 64 / 5 / 1e3
-        out["alg_modmul"] = {"per_launch": int(alg_mm / calls), "achieved": round(tps, 3), "canonical_peak": round(peak, 3),
-                             "unit": "T modmul/s", "frac": round(tps / peak, 4)}
+        # the program's field multiplications (as the reference's poly_fp writes them) per second:
+        # a rate, not a roof (the kernels need fewer instructions per product than a canonical
+        # Montgomery multiply, so no hardware peak bounds it)
+        out["alg_modmul"] = {"per_launch": int(alg_mm / calls), "achieved": round(alg_mm / calls / avg_s / 1e12, 3),
+                             "unit": "T modmul/s"}
+    seg = segment_valu(args, ms_per_step)
+    if seg:
+        out["segment_valu"] = seg
     if out["bound"] != "hbm":
         out["hbm"] = hbm
     if tsrc:
         out["traffic_source"] = tsrc
     return out
+
+
+def ec_issue(args, avg_s, insts):
+    """eval_check's launch against issue roofs that price each instruction at its own cost, from
+    the committed instruction mix of the generated kernels (profiles/r*_ec_inst_mix.json,
+    tools/ec_inst_mix.py: per-kernel static VALU counts of the straight-line kernels, equal to the
+    PMC per-wave counts): the guide's cycles (2 for full-rate 32-bit ops, 4 for the rest) at
+    2.4 GHz, and the chip rates measured for each instruction alone (r1_valu_rates.txt)."""
+    path = pmc_summary_file("ec_inst_mix", prefix="")
+    if path is None or args.circuit != "rv32im":
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    waves = insts / d["valu_per_point"]  # wave64 launches of the whole program
+    t_cyc = waves * d["issue_cycles_per_point"] / (256 * 4 * 2.4e9)
+    t_meas = waves * d["measured_rate_s_per_wave"]
+    t4 = insts * 4 / (256 * 4 * 2.4e9)
+    return {"valu_per_point": d["valu_per_point"], "issue_cycles_per_point": d["issue_cycles_per_point"],
+            "full_rate_share": round(sum(k["full_rate_share"] * k["valu_per_wave"] for k in d["kernels"].values())
+                                     / d["valu_per_point"], 4),
+            "frac_4cycle": round(t4 / avg_s, 4), "frac_issue_weighted": round(t_cyc / avg_s, 4),
+            "frac_measured_rates": round(t_meas / avg_s, 4),
+            "min_ms_issue_weighted": round(t_cyc * 1e3, 3), "min_ms_measured_rates": round(t_meas * 1e3, 3),
+            "source": os.path.relpath(path, ROOT), "source_matches_library": d.get("lib_sha256_16") == lib_fingerprint(),
+            "note": "the launch time against the time its instructions need at full issue: every instruction at 4 "
+                    "cycles (frac_4cycle, as frac), at the guide's cost (2 cycles for full-rate 32-bit ops, 4 for "
+                    "64-bit / multiply / VOP3-only ops; frac_issue_weighted, the lower bound), and at the chip rate "
+                    "measured for each instruction alone at 4 waves per SIMD (frac_measured_rates, which carries the "
+                    "clock the chip holds under integer load)"}
+
+
+def segment_valu(args, ms_per_step):
+    """the whole segment's executed VALU instructions (every kernel of a proof, from the committed
+    PMC pass of this bench) against the issue roof and the bench's own time per segment: how much
+    of the step the GPU needs at full 4-cycle issue"""
+    if args.circuit != "rv32im" or args.po2 != 20 or args.hashfn != "poseidon2":
+        return None
+    path = pmc_summary_file("valu")
+    if path is None:
+        return None
+    with open(path) as f:
+        ks = json.load(f)["kernels"]
+    proofs = ks.get("ec_rv32im::k0<true>", ks.get("ec_rv32im::k0<false>", {})).get("dispatches")
+    if not proofs:
+        return None
+    per_proof = sum(d["insts_valu"] for d in ks.values()) / proofs
+    ms = per_proof / (VALU_PEAK_GIPS * 1e9) * 1e3
+    return {"valu_insts_per_segment": int(per_proof), "ms_at_issue_peak": round(ms, 2), "ms_per_step": round(ms_per_step, 3),
+            "frac": round(ms / ms_per_step, 4), "source": os.path.relpath(path, ROOT),
+            "note": "every kernel's executed VALU instructions per proof (PMC SQ_INSTS_VALU over the run's proofs) at "
+                    "one wave64 instruction per 4 cycles on 1024 SIMDs at 2.4 GHz, over the bench's ms per segment"}
 
 
 def lib_fingerprint():
@@ -484,7 +540,7 @@ def lib_fingerprint():
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
-def pmc_summary_file(kind):
+def pmc_summary_file(kind, prefix="pmc_"):
     """the committed PMC summary to quote (profiles/r<round><tag>_pmc_<kind>.json): the newest one
     measured on the loaded library (its lib_sha256_16), else the newest. Round tags order by
     round, then tag length, then tag (r5z < r5aa < r5an), not as plain strings."""
@@ -495,7 +551,7 @@ def pmc_summary_file(kind):
         m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
         return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{kind}.json")), key=key)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{prefix}{kind}.json")), key=key)
     if not files:
         return None
     lib = lib_fingerprint()

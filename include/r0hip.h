@@ -292,35 +292,16 @@ const char* r0hip_prove_recursion(int suite, uint32_t po2, const uint32_t* d_ctr
 
 /* ---- segment pipeline (r0vm's per-GPU worker queue, r0vm/src/actors/worker.rs:75-76, over the
  * zkvm's per-segment prove loop, zkvm/src/host/server/prove/prover_impl.rs:84-94) ----
- * Proves njobs segments of one (circuit, suite, po2) from HOST inputs: an uploader thread copies
- * each job's inputs into one of in_flight+1 device buffer sets while in_flight prover threads
- * prove on their own streams. Host buffers must stay valid until the call returns and should be
- * page-locked (r0hip_host_alloc) for full PCIe rate. Per job: seal into h_seal (seal_cap words),
- * its length in seal_len, mix values into h_mix_out (optional), and error = NULL or a malloc'd
- * message (free() it). Returns NULL when every job succeeded.
- * Two job forms, one per call (all jobs of a call take the same form):
- *  - witness jobs (trace == NULL): the witness groups, copied in 48-column chunks; a prover
- *    starts a job at once and commits each group chunk by chunk as it lands (Poseidon2 and
- *    SHA-256; Poseidon254 waits for whole groups). Seals equal r0hip_prove_segment's.
- *  - trace jobs (trace != NULL, rv32im only, write_version = 1 and version = 2): the job is
- *    SegmentProverImpl::prove_core from a preflight trace (circuit/rv32im/src/prove/hal/mod.rs:
- *    143-224), the unit r0vm's GPU worker runs from the executor's segments
- *    (r0vm/src/actors/worker.rs:186-260, job/proof.rs:238-323), with the CUDA prove_core's trace
- *    upload (circuit/rv32im/src/prove/witgen/mod.rs:135-176) done by the uploader: the trace, the
- *    injector and the global vector go into one of in_flight+1 device trace sets while the
- *    provers run witness generation, accumulation and the proof from the others. The injector is
- *    checked on the host as r0hip_prove_segment_trace checks it. h_bigint/n_bigint are the
- *    trace's BigInt backs; h_code/h_data/h_accum/h_global are unused. Seals equal
- *    r0hip_prove_segment_trace's. */
-typedef struct r0hip_trace_input {
-  uint32_t mode;                      /* as r0hip_rv32im_witgen */
-  const uint32_t* h_global;           /* build_global_vec's 90 Montgomery words */
-  const uint32_t* h_inj_index;        /* inj_rows + 1 entries */
-  size_t inj_rows;
-  const uint32_t* h_inj_offsets;      /* h_inj_index[inj_rows] entries each */
-  const uint32_t* h_inj_values;
-  r0hip_raw_preflight_trace preflight; /* host pointers; 2^po2 cycle records */
-} r0hip_trace_input;
+ * Proves njobs segments of one (circuit, suite, po2) from HOST witness groups: an uploader thread
+ * copies each job's groups into one of in_flight+1 device buffer sets, in 48-column chunks, while
+ * in_flight provers (in_flight - 1 threads and the calling thread) prove on their own streams; a
+ * prover starts a job at once and commits each group chunk by chunk as it lands (Poseidon2 and
+ * SHA-256; Poseidon254 waits for whole groups). Host buffers must stay valid until the call
+ * returns and should be page-locked (r0hip_host_alloc) for full PCIe rate. Per job: seal into
+ * h_seal (seal_cap words), its length in seal_len, mix values into h_mix_out (optional), and
+ * error = NULL or a malloc'd message (free() it). Returns NULL when every job succeeded. Seals
+ * equal r0hip_prove_segment's. (Round 5 appended a `trace` pointer to this struct; trace jobs
+ * now have their own entry point below and this struct has its round-4 layout again.) */
 typedef struct r0hip_segment_job {
   const uint32_t* h_code;
   const uint32_t* h_data;
@@ -334,10 +315,46 @@ typedef struct r0hip_segment_job {
   size_t seal_len;
   uint32_t* h_mix_out;
   const char* error;
-  const r0hip_trace_input* trace;    /* non-NULL: a trace job (see above) */
 } r0hip_segment_job;
 const char* r0hip_prove_segments(const char* circuit, int suite, uint32_t po2, int write_version, uint32_t version,
                                  r0hip_segment_job* jobs, size_t njobs, uint32_t in_flight);
+
+/* ---- the GPU worker unit from preflight traces: rv32im SegmentProverImpl::prove_core
+ * (circuit/rv32im/src/prove/hal/mod.rs:143-224) per job, as r0vm's GPU worker runs it from the
+ * executor's segments (r0vm/src/actors/worker.rs:186-260, job/proof.rs:238-323), with the CUDA
+ * prove_core's trace upload (circuit/rv32im/src/prove/witgen/mod.rs:135-176) done by an uploader
+ * thread: the trace, the injector and the global vector go into one of in_flight+1 device trace
+ * sets while in_flight provers (in_flight - 1 threads and the calling thread) run witness
+ * generation, accumulation and the proof from the others. The injector is checked on the host as
+ * r0hip_prove_segment_trace checks it. Seals equal r0hip_prove_segment_trace's (version word 2).
+ * verify != 0: every seal is checked by r0hip_verify_seal (the validity equation included) on a
+ * host thread while the GPU proves the next jobs, as ProverImpl::prove_segment_core verifies a
+ * receipt before returning it (zkvm/src/host/server/prove/prover_impl.rs:262-280); a seal that
+ * fails sets that job's error ("receipt verification failed: ...") and the other jobs still
+ * return. Host arrays must stay valid until the call returns. */
+typedef struct r0hip_trace_input {
+  uint32_t mode;                      /* as r0hip_rv32im_witgen */
+  const uint32_t* h_global;           /* build_global_vec's 90 Montgomery words */
+  const uint32_t* h_inj_index;        /* inj_rows + 1 entries */
+  size_t inj_rows;
+  const uint32_t* h_inj_offsets;      /* h_inj_index[inj_rows] entries each */
+  const uint32_t* h_inj_values;
+  r0hip_raw_preflight_trace preflight; /* host pointers; 2^po2 cycle records */
+} r0hip_trace_input;
+typedef struct r0hip_trace_job {
+  r0hip_trace_input trace;
+  const r0hip_bigint_back* h_bigint;  /* the trace's BigInt backs (NULL, 0 if none) */
+  size_t n_bigint;
+  uint32_t* h_seal;                   /* out: the seal (seal_cap words), its length in seal_len */
+  size_t seal_cap;
+  size_t seal_len;
+  uint32_t* h_mix_out;                /* out (optional): the 36 mix words */
+  const char* error;                  /* out: NULL or a malloc'd message (free() it) */
+  int verified;                       /* out: 1 when the seal passed r0hip_verify_seal */
+  double verify_ms;                   /* out: host milliseconds of that check */
+} r0hip_trace_job;
+const char* r0hip_prove_trace_segments(int suite, uint32_t po2, r0hip_trace_job* jobs, size_t njobs,
+                                       uint32_t in_flight, int verify);
 
 /* ---- seal verification (risc0/zkp/src/verify/mod.rs:500-560 `verify`, with merkle.rs:79-186,
  * fri.rs:36-155, read_iop.rs:20-84; rv32im seals lead with the version word 2,

@@ -35,7 +35,7 @@ pub struct R0HipBigIntBack {
     pub bytes: [u8; 16],
 }
 
-/// A preflight trace as a trace job of r0hip_prove_segments takes it (struct r0hip_trace_input):
+/// A preflight trace as a job of r0hip_prove_trace_segments takes it (struct r0hip_trace_input):
 /// host pointers; `preflight` has the repr(C) layout of risc0_circuit_rv32im_sys::RawPreflightTrace.
 #[repr(C)]
 pub struct R0HipTraceInput {
@@ -48,8 +48,7 @@ pub struct R0HipTraceInput {
     pub preflight: risc0_circuit_rv32im_sys::RawPreflightTrace,
 }
 
-/// One job of r0hip_prove_segments: host witness groups in (trace NULL), or a preflight trace
-/// (trace non-NULL, rv32im prove_core); seal out.
+/// One job of r0hip_prove_segments: host witness groups in, seal out (struct r0hip_segment_job).
 #[repr(C)]
 pub struct R0HipSegmentJob {
     pub h_code: *const u32,
@@ -63,7 +62,22 @@ pub struct R0HipSegmentJob {
     pub seal_len: usize,
     pub h_mix_out: *mut u32,
     pub error: *const c_char,
-    pub trace: *const R0HipTraceInput,
+}
+
+/// One job of r0hip_prove_trace_segments (struct r0hip_trace_job): the rv32im prove_core of one
+/// preflight trace; seal out, and with `verify` the receipt check's outcome.
+#[repr(C)]
+pub struct R0HipTraceJob {
+    pub trace: R0HipTraceInput,
+    pub h_bigint: *const R0HipBigIntBack,
+    pub n_bigint: usize,
+    pub h_seal: *mut u32,
+    pub seal_cap: usize,
+    pub seal_len: usize,
+    pub h_mix_out: *mut u32,
+    pub error: *const c_char,
+    pub verified: c_int,
+    pub verify_ms: f64,
 }
 
 #[link(name = "r0hip")]
@@ -331,6 +345,14 @@ unsafe extern "C" {
         jobs: *mut R0HipSegmentJob,
         njobs: usize,
         in_flight: u32,
+    ) -> *const c_char;
+    pub fn r0hip_prove_trace_segments(
+        suite: c_int,
+        po2: u32,
+        jobs: *mut R0HipTraceJob,
+        njobs: usize,
+        in_flight: u32,
+        verify: c_int,
     ) -> *const c_char;
 
     // ---- verification (host-only) ----

@@ -33,6 +33,8 @@ std::string last_profile();
 using namespace r0;
 
 namespace {
+// The call's work is complete on return, and the calling thread's idle device memory goes back
+// to the shared pool (release_thread_memory), so a caller's thread holds none between calls.
 template <typename F>
 const char* wrap(F f) {
   try {
@@ -40,11 +42,14 @@ const char* wrap(F f) {
     HIP_OK(hipStreamSynchronize(stream()));
   } catch (const std::exception& e) {
     drain_after_error();
+    release_thread_memory();
     return strdup(e.what());
   } catch (...) {
     drain_after_error();
+    release_thread_memory();
     return strdup("r0hip: unknown error");
   }
+  release_thread_memory();
   return nullptr;
 }
 // host-only entry points: no stream, no device
@@ -312,15 +317,16 @@ const char* r0hip_rv32im_witgen(uint32_t mode, const r0hip_raw_exec_buffers* buf
 namespace r0 {
 
 void check_injector(const uint32_t* index, size_t rows, const uint32_t* offsets, const uint32_t* values,
-                    size_t limit);
+                    size_t limit, size_t seg_rows);
 
 // SegmentProverImpl::prove_core from a preflight (circuit/rv32im/src/prove/hal/mod.rs:143-224):
 // WitnessGenerator::hal_generate_witness (witgen/mod.rs:135-176: globals, code and data
 // INVALID, the injector scattered into data, stepExec, zeroize), then the prove core with the
 // version word 2 and WitnessGenerator::accum on the device. `resident`: the global vector,
 // the injector and the preflight arrays are device pointers; otherwise host pointers.
-// inputs_ready (resident only): called with the stream after the INVALID fills and before the
-// first read of the inputs (the segment pipeline makes the stream wait for their upload there).
+// inputs_ready (resident only): called with the stream after the groups' fill (which reads no
+// input) and before the first read of the inputs (the segment pipeline makes the stream wait for
+// their upload there, so the fill runs while the trace still uploads).
 std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const uint32_t* global_in,
                                   const uint32_t* inj_index, size_t inj_rows, const uint32_t* inj_offsets,
                                   const uint32_t* inj_values, const r0hip_raw_preflight_trace* pf,
@@ -338,7 +344,8 @@ std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const 
   Span span("prove_segment_trace");
   DevBuf code(c->group_size(1) * n), data(data_cols * n), global(c->output_size), accum(c->group_size(0) * n);
   // the groups as WitnessGenerator::new / ::accum allocate them (INVALID), already zeroized where
-  // nothing reads INVALID, with the injector scattered in: one pass (rv32im_prover_groups_init)
+  // nothing reads INVALID (rv32im_prover_groups_fill), then the injector (rv32im_prover_inject)
+  rv32im_prover_groups_fill(s, data.p, code.p, accum.p, n, c->group_size(0));
   const uint32_t *idx = inj_index, *off = inj_offsets, *val = inj_values;
   const rvwg::PreflightCycle* cyc = static_cast<const rvwg::PreflightCycle*>(pf->cycles);
   const rvwg::MemoryTxn* txn = static_cast<const rvwg::MemoryTxn*>(pf->txns);
@@ -349,7 +356,7 @@ std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const 
   } else {
     R0_REQUIRE((pf->txns_len == 0 || pf->txns) && (pf->bigint_bytes_len == 0 || pf->bigint_bytes),
                "r0hip_prove_segment_trace: null trace array with a nonzero count");
-    check_injector(inj_index, inj_rows, inj_offsets, inj_values, data_cols * n);
+    check_injector(inj_index, inj_rows, inj_offsets, inj_values, data_cols * n, n);
     const size_t n_inj = inj_index[inj_rows];
     upload_async(global.p, global_in, global.words * 4);
     auto* d_idx = static_cast<uint32_t*>(scratch((inj_rows + 1) * 4, kSlotRvInjIndex));
@@ -369,12 +376,17 @@ std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const 
   }
   auto* ierr = static_cast<uint32_t*>(scratch(16, kSlotRvInitErr));
   HIP_OK(hipMemsetD32Async(ierr, 0u, 4, s));
-  rv32im_prover_groups_init(s, data.p, code.p, accum.p, n, c->group_size(0), idx, off, val, inj_rows, data.words, cyc,
-                            ierr);
+  rv32im_prover_inject(s, data.p, n, idx, off, val, inj_rows, data.words, cyc, ierr);
   {
     Span w("witgen");
+    // an injector entry outside its row's injected columns: the group as the reference prepares
+    // it (hal_generate_witness, witgen/mod.rs:146-162), every word INVALID and the injector scattered
+    auto reinit = [&] {
+      HIP_OK(hipMemsetD32Async(data.p, 0xFFFFFFFFu, data.words, s));
+      scatter(s, data.p, idx, off, val, inj_rows, data.words);
+    };
     rv32im_witgen_dev(s, mode, data.p, global.p, n, cyc, txn, pf->txns_len, big, pf->bigint_bytes_len,
-                      pf->table_split_cycle, uint32_t(n), true, ierr);
+                      pf->table_split_cycle, uint32_t(n), true, ierr, reinit);
   }
   eltwise_zeroize(s, global.p, global.words);  // the data group was zeroized by the witgen merge
   AccumStep acc{accum.p, n, false, h_bigint, n_bigint};
@@ -383,17 +395,23 @@ std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const 
 }
 
 // The host injector (Injector, witgen/mod.rs:329-378) before it is uploaded: a CSR index that
-// never decreases (entries of row c are [index[c], index[c + 1])) and offsets inside the data
-// group. O(rows + entries); the resident path's scatter bounds its reads and writes instead.
+// never decreases (entries of row c are [index[c], index[c + 1])), offsets inside the data group
+// and in the entry's own row (col * seg_rows + c: Injector::set writes only its row). O(rows +
+// entries); the resident path's inject pass bounds its reads and writes and reports other rows.
 void check_injector(const uint32_t* index, size_t rows, const uint32_t* offsets, const uint32_t* values,
-                    size_t limit) {
+                    size_t limit, size_t seg_rows) {
   for (size_t c = 0; c < rows; c++)
     R0_REQUIRE(index[c] <= index[c + 1], "r0hip_prove_segment_trace: injector index decreases at row " +
                                              std::to_string(c));
   const size_t n_inj = index[rows];
   R0_REQUIRE(n_inj == 0 || (offsets && values), "r0hip_prove_segment_trace: null injector arrays");
-  for (size_t i = 0; i < n_inj; i++)
-    R0_REQUIRE(offsets[i] < limit, "r0hip_prove_segment_trace: injector offset outside the data group");
+  for (size_t c = 0; c < rows; c++)
+    for (size_t i = index[c]; i < index[c + 1]; i++) {
+      R0_REQUIRE(offsets[i] < limit, "r0hip_prove_segment_trace: injector offset outside the data group");
+      R0_REQUIRE(offsets[i] % seg_rows == c, "r0hip_prove_segment_trace: injector entry of row " + std::to_string(c) +
+                                                 " sets word " + std::to_string(offsets[i]) +
+                                                 " of another row (Injector::set writes its own row)");
+    }
 }
 
 }  // namespace r0

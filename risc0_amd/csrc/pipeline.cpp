@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <chrono>
 #include <deque>
 #include <functional>
 #include <mutex>
@@ -40,7 +41,7 @@ std::vector<uint32_t> prove_trace(int suite, uint32_t po2, uint32_t mode, const 
                                   const r0hip_bigint_back* h_bigint, size_t n_bigint, bool resident,
                                   std::vector<uint32_t>* mix, const std::function<void(hipStream_t)>& inputs_ready);
 void check_injector(const uint32_t* index, size_t rows, const uint32_t* offsets, const uint32_t* values,
-                    size_t limit);
+                    size_t limit, size_t seg_rows);
 
 namespace {
 
@@ -110,6 +111,22 @@ struct Queue {
   }
 };
 
+// k provers: k - 1 threads and the calling thread, whose stream the process already holds, so
+// a call keeps k + 1 streams busy (the uploader's and the provers') and the runtime's default 4
+// hardware queues give each its own for k <= 3 (a shared queue runs its streams' kernels in
+// order). R0_PIPE_CALLER_PROVES=0: k prover threads (the calling thread only waits).
+template <typename F>
+void run_provers(size_t k, F& prover) {
+  static const bool caller = [] {
+    const char* e = getenv("R0_PIPE_CALLER_PROVES");
+    return !e || strtoul(e, nullptr, 10) != 0;
+  }();
+  std::vector<std::thread> threads;
+  for (size_t t = caller ? 1 : 0; t < k; t++) threads.emplace_back(prover);
+  if (caller) prover();  // returns at its stop token; never throws (errors are per job)
+  for (auto& t : threads) t.join();
+}
+
 char* dup_msg(const char* m) {
   size_t n = strlen(m) + 1;
   char* p = static_cast<char*>(malloc(n));
@@ -141,17 +158,22 @@ struct TraceSet {
 };
 
 // Trace jobs: the uploader copies job i's trace into a free trace set and hands the set to a
-// prover at once; the prover allocates and INVALID-fills its witness groups, then its stream
-// waits for the set's event before the scatter (prove_trace's inputs_ready), so the copies of
-// one segment overlap the proofs of the others. k + 1 sets, sized once for the largest job.
-const char* prove_trace_jobs(int suite, uint32_t po2, r0hip_segment_job* jobs, size_t njobs, size_t k) {
+// prover at once; the prover allocates its witness groups and queues their fill (which reads no
+// input), then waits on the host until the uploader has queued the set's copies and makes its
+// stream wait for the set's event before the injector pass (prove_trace's inputs_ready), so the
+// copies of one segment overlap the proofs of the others. k + 1 sets, sized once for the largest
+// job.
+// verify: each finished seal is checked by r0hip_verify_seal (the validity equation included) on
+// a host thread of its own while the GPU proves the next segments, as ProverImpl::
+// prove_segment_core verifies a receipt before it returns it (zkvm/src/host/server/prove/
+// prover_impl.rs:262-280); a seal that fails fails its job.
+const char* prove_trace_jobs(int suite, uint32_t po2, r0hip_trace_job* jobs, size_t njobs, size_t k, bool verify) {
   constexpr size_t kCycleWords = 9, kTxnWords = 5, kGlobalWords = 90;  // RawPreflightCycle 36 B, txn 20 B
   const size_t n = size_t(1) << po2;
   const size_t data_words = size_t(211) * n;
   size_t cap_inj = 1, cap_txn = 1, cap_big = 4;
   for (size_t i = 0; i < njobs; i++) {
-    const r0hip_trace_input* t = jobs[i].trace;
-    R0_REQUIRE(t, "r0hip_prove_segments: a call mixes trace jobs and witness jobs");
+    const r0hip_trace_input* t = &jobs[i].trace;
     if (t->h_inj_index && t->inj_rows <= n) cap_inj = std::max<size_t>(cap_inj, t->h_inj_index[t->inj_rows]);
     cap_txn = std::max<size_t>(cap_txn, t->preflight.txns_len);
     cap_big = std::max<size_t>(cap_big, t->preflight.bigint_bytes_len);
@@ -190,14 +212,14 @@ const char* prove_trace_jobs(int suite, uint32_t po2, r0hip_segment_job* jobs, s
       ready_q.put(s);  // the prover fills its groups while the trace uploads
       try {
         ensure_init();
-        const r0hip_trace_input& t = *jobs[i].trace;
+        const r0hip_trace_input& t = jobs[i].trace;
         const r0hip_raw_preflight_trace& pf = t.preflight;
         R0_REQUIRE(t.h_global && t.h_inj_index && pf.cycles, "trace job: null argument");
         R0_REQUIRE(t.inj_rows <= n, "trace job: injector longer than the segment");
         R0_REQUIRE((pf.txns_len == 0 || pf.txns) && (pf.bigint_bytes_len == 0 || pf.bigint_bytes),
                    "trace job: null trace array with a nonzero count");
         R0_REQUIRE(jobs[i].n_bigint == 0 || jobs[i].h_bigint, "trace job: h_bigint is NULL with n_bigint > 0");
-        check_injector(t.h_inj_index, t.inj_rows, t.h_inj_offsets, t.h_inj_values, data_words);
+        check_injector(t.h_inj_index, t.inj_rows, t.h_inj_offsets, t.h_inj_values, data_words, n);
         const size_t n_inj = t.h_inj_index[t.inj_rows];
         stage_reset();  // the previous job's staged copies have landed: the arena is free
         upload_async(b.glob.p, t.h_global, kGlobalWords * 4);
@@ -222,51 +244,101 @@ const char* prove_trace_jobs(int suite, uint32_t po2, r0hip_segment_job* jobs, s
     for (size_t t = 0; t < k; t++) ready_q.put(-1);
   });
 
-  std::vector<std::thread> provers;
-  for (size_t t = 0; t < k; t++) {
-    provers.emplace_back([&] {
+  // the receipt check: finished seals queue here (job index and seal) for the verifier thread
+  std::mutex vmu;
+  std::condition_variable vcv;
+  std::deque<std::pair<long, std::vector<uint32_t>>> vq;
+  std::thread verifier;
+  if (verify)
+    verifier = std::thread([&] {
       for (;;) {
-        long s = ready_q.get();
-        if (s < 0) return;
-        TraceSet& b = sets[s];
-        r0hip_segment_job& j = jobs[b.job];
-        const r0hip_trace_input& tr = *j.trace;
-        try {
-          ensure_init();
-          r0hip_raw_preflight_trace pf = tr.preflight;  // the set's device copies
-          pf.cycles = b.cycles.p;
-          pf.txns = pf.txns_len ? b.txns.p : nullptr;
-          pf.bigint_bytes = pf.bigint_bytes_len ? reinterpret_cast<const uint8_t*>(b.bigint.p) : nullptr;
-          std::vector<uint32_t> mix;
-          std::vector<uint32_t> seal = prove_trace(
-              suite, po2, tr.mode, b.glob.p, b.index.p, tr.inj_rows, b.offsets.p, b.values.p, &pf, j.h_bigint,
-              j.n_bigint, true, &mix, [&](hipStream_t st) {
-                b.wait_landed();
-                {
-                  std::lock_guard<std::mutex> lk(b.mu);
-                  if (j.error) throw std::runtime_error(j.error);
-                }
-                HIP_OK(hipStreamWaitEvent(st, b.ev, 0));
-              });
-          HIP_OK(hipStreamSynchronize(stream()));
-          j.seal_len = seal.size();
-          if (j.h_mix_out) memcpy(j.h_mix_out, mix.data(), mix.size() * 4);
-          R0_REQUIRE(!j.h_seal || seal.size() <= j.seal_cap, "seal buffer too small");
-          if (j.h_seal) memcpy(j.h_seal, seal.data(), seal.size() * 4);
-        } catch (const std::exception& e) {
-          {
-            std::lock_guard<std::mutex> lk(b.mu);
-            if (!j.error) j.error = dup_msg(e.what());
-          }
-          drain_after_error();  // kernels queued before the throw may still read this set
+        std::pair<long, std::vector<uint32_t>> item;
+        {
+          std::unique_lock<std::mutex> lk(vmu);
+          vcv.wait(lk, [&] { return !vq.empty(); });
+          item = std::move(vq.front());
+          vq.pop_front();
         }
-        b.wait_landed();  // the uploader is done with this job before the set is refilled
-        free_q.put(s);
+        if (item.first < 0) return;
+        r0hip_trace_job& j = jobs[item.first];
+        const auto t0 = std::chrono::steady_clock::now();
+        uint32_t got = 0;
+        const char* err = r0hip_verify_seal("rv32im", suite, item.second.data(), item.second.size(), nullptr, 0,
+                                            nullptr, &got);
+        j.verify_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (!err && got != po2) err = dup_msg("the seal is of another segment size");
+        std::lock_guard<std::mutex> lk(vmu);
+        if (err) {
+          if (!j.error) j.error = dup_msg((std::string("receipt verification failed: ") + err).c_str());
+          free(const_cast<char*>(err));
+        } else {
+          j.verified = 1;
+        }
       }
     });
-  }
+  auto to_verifier = [&](long job, std::vector<uint32_t> seal) {
+    {
+      std::lock_guard<std::mutex> lk(vmu);
+      vq.emplace_back(job, std::move(seal));
+    }
+    vcv.notify_one();
+  };
+
+  const long corrupt_job = [] {
+    const char* e = getenv("R0HIP_TESTING_CORRUPT_SEAL_JOB");
+    return e ? strtol(e, nullptr, 10) : -1L;
+  }();
+  auto prover = [&] {
+    for (;;) {
+      long s = ready_q.get();
+      if (s < 0) return;
+      TraceSet& b = sets[s];
+      const long job = long(b.job);
+      r0hip_trace_job& j = jobs[job];
+      const r0hip_trace_input& tr = j.trace;
+      try {
+        ensure_init();
+        r0hip_raw_preflight_trace pf = tr.preflight;  // the set's device copies
+        pf.cycles = b.cycles.p;
+        pf.txns = pf.txns_len ? b.txns.p : nullptr;
+        pf.bigint_bytes = pf.bigint_bytes_len ? reinterpret_cast<const uint8_t*>(b.bigint.p) : nullptr;
+        std::vector<uint32_t> mix;
+        std::vector<uint32_t> seal = prove_trace(
+            suite, po2, tr.mode, b.glob.p, b.index.p, tr.inj_rows, b.offsets.p, b.values.p, &pf, j.h_bigint,
+            j.n_bigint, true, &mix, [&](hipStream_t st) {
+              b.wait_landed();
+              {
+                std::lock_guard<std::mutex> lk(b.mu);
+                if (j.error) throw std::runtime_error(j.error);
+              }
+              HIP_OK(hipStreamWaitEvent(st, b.ev, 0));
+            });
+        HIP_OK(hipStreamSynchronize(stream()));
+        j.seal_len = seal.size();
+        if (j.h_mix_out) memcpy(j.h_mix_out, mix.data(), mix.size() * 4);
+        // TESTING ONLY (tests/test_rv32im_witgen_gpu.py): R0HIP_TESTING_CORRUPT_SEAL_JOB=i flips a
+        // bit of job i's first Merkle root word, so its receipt check must fail that job alone
+        if (job == corrupt_job && seal.size() > 92) seal[92] ^= 1u;
+        R0_REQUIRE(!j.h_seal || seal.size() <= j.seal_cap, "seal buffer too small");
+        if (j.h_seal) memcpy(j.h_seal, seal.data(), seal.size() * 4);
+        if (verify) to_verifier(job, std::move(seal));
+      } catch (const std::exception& e) {
+        {
+          std::lock_guard<std::mutex> lk(b.mu);
+          if (!j.error) j.error = dup_msg(e.what());
+        }
+        drain_after_error();  // kernels queued before the throw may still read this set
+      }
+      b.wait_landed();  // the uploader is done with this job before the set is refilled
+      free_q.put(s);
+    }
+  };
+  run_provers(k, prover);
   uploader.join();
-  for (auto& t : provers) t.join();
+  if (verify) {
+    to_verifier(-1, {});
+    verifier.join();
+  }
   for (size_t i = 0; i < njobs; i++)
     if (jobs[i].error) return dup_msg((std::string("segment ") + std::to_string(i) + ": " + jobs[i].error).c_str());
   return nullptr;
@@ -277,9 +349,9 @@ const char* prove_trace_jobs(int suite, uint32_t po2, r0hip_segment_job* jobs, s
 
 using namespace r0;
 
-extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint32_t po2, int write_version,
-                                            uint32_t version, r0hip_segment_job* jobs, size_t njobs,
-                                            uint32_t in_flight) {
+namespace {
+const char* prove_segments_impl(const char* circuit, int suite, uint32_t po2, int write_version, uint32_t version,
+                                r0hip_segment_job* jobs, size_t njobs, uint32_t in_flight) {
   try {
     const CircuitDef* c = find_circuit(circuit ? circuit : "");
     R0_REQUIRE(c, std::string("unknown circuit ") + (circuit ? circuit : "(null)"));
@@ -293,12 +365,6 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
       jobs[i].error = nullptr;
       jobs[i].seal_len = 0;
     }
-    if (jobs[0].trace) {
-      R0_REQUIRE(std::string(c->name) == "rv32im", "trace jobs are rv32im segments");
-      R0_REQUIRE(write_version && version == 2, "trace jobs write the rv32im seal version word 2");
-      return prove_trace_jobs(suite, po2, jobs, njobs, k);
-    }
-    for (size_t i = 0; i < njobs; i++) R0_REQUIRE(!jobs[i].trace, "a call mixes witness jobs and trace jobs");
     const bool device_accum_ok = std::string(c->name) == "rv32im";
     const size_t n = size_t(1) << po2;
     // group_sizes: accum 0, code 1, data 2 (the reference's register-group order)
@@ -390,51 +456,48 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
       for (size_t t = 0; t < k; t++) ready_q.put(-1);  // one stop token per prover
     });
 
-    std::vector<std::thread> provers;
-    for (size_t t = 0; t < k; t++) {
-      provers.emplace_back([&] {
-        for (;;) {
-          long s = ready_q.get();
-          if (s < 0) return;
-          BufSet& b = sets[s];
-          r0hip_segment_job& j = jobs[b.job];
-          // j.error is written by the uploader under b.mu while this job's copies are queued
-          auto failed = [&] {
-            std::lock_guard<std::mutex> lk(b.mu);
-            return j.error != nullptr;
-          };
-          if (!failed()) {
-            try {
-              ensure_init();
-              std::vector<uint32_t> mix;
-              const bool dev_accum = !j.h_accum;  // (rv32im only: checked by the uploader)
-              const AccumStep acc{b.g[2].p, n, true, j.h_bigint, j.n_bigint};
-              std::vector<uint32_t> seal =
-                  prove_segment(*c, suite, po2, b.g[0].p, b.g[1].p, dev_accum ? nullptr : b.g[2].p, b.g[3].p,
-                                write_version != 0, version, &mix, &b, dev_accum ? &acc : nullptr);
-              HIP_OK(hipStreamSynchronize(stream()));
-              if (!failed()) {  // an upload error leaves the proof meaningless: drop it
-                j.seal_len = seal.size();
-                if (j.h_mix_out) memcpy(j.h_mix_out, mix.data(), mix.size() * 4);
-                R0_REQUIRE(!j.h_seal || seal.size() <= j.seal_cap, "seal buffer too small");
-                if (j.h_seal) memcpy(j.h_seal, seal.data(), seal.size() * 4);
-              }
-            } catch (const std::exception& e) {
-              {
-                std::lock_guard<std::mutex> lk(b.mu);
-                if (!j.error) j.error = dup_msg(e.what());
-              }
-              // kernels queued before the throw may still read this buffer set: drain
-              // them before the uploader refills it
-              drain_after_error();
+    auto prover = [&] {
+      for (;;) {
+        long s = ready_q.get();
+        if (s < 0) return;
+        BufSet& b = sets[s];
+        r0hip_segment_job& j = jobs[b.job];
+        // j.error is written by the uploader under b.mu while this job's copies are queued
+        auto failed = [&] {
+          std::lock_guard<std::mutex> lk(b.mu);
+          return j.error != nullptr;
+        };
+        if (!failed()) {
+          try {
+            ensure_init();
+            std::vector<uint32_t> mix;
+            const bool dev_accum = !j.h_accum;  // (rv32im only: checked by the uploader)
+            const AccumStep acc{b.g[2].p, n, true, j.h_bigint, j.n_bigint};
+            std::vector<uint32_t> seal =
+                prove_segment(*c, suite, po2, b.g[0].p, b.g[1].p, dev_accum ? nullptr : b.g[2].p, b.g[3].p,
+                              write_version != 0, version, &mix, &b, dev_accum ? &acc : nullptr);
+            HIP_OK(hipStreamSynchronize(stream()));
+            if (!failed()) {  // an upload error leaves the proof meaningless: drop it
+              j.seal_len = seal.size();
+              if (j.h_mix_out) memcpy(j.h_mix_out, mix.data(), mix.size() * 4);
+              R0_REQUIRE(!j.h_seal || seal.size() <= j.seal_cap, "seal buffer too small");
+              if (j.h_seal) memcpy(j.h_seal, seal.data(), seal.size() * 4);
             }
+          } catch (const std::exception& e) {
+            {
+              std::lock_guard<std::mutex> lk(b.mu);
+              if (!j.error) j.error = dup_msg(e.what());
+            }
+            // kernels queued before the throw may still read this buffer set: drain
+            // them before the uploader refills it
+            drain_after_error();
           }
-          free_q.put(s);
         }
-      });
-    }
+        free_q.put(s);
+      }
+    };
+    run_provers(k, prover);
     uploader.join();
-    for (auto& t : provers) t.join();
     for (size_t i = 0; i < njobs; i++)
       if (jobs[i].error) return dup_msg((std::string("segment ") + std::to_string(i) + ": " + jobs[i].error).c_str());
     return nullptr;
@@ -443,4 +506,44 @@ extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint
   } catch (...) {
     return dup_msg("r0hip: unknown error");
   }
+}
+}  // namespace
+
+extern "C" const char* r0hip_prove_segments(const char* circuit, int suite, uint32_t po2, int write_version,
+                                            uint32_t version, r0hip_segment_job* jobs, size_t njobs,
+                                            uint32_t in_flight) {
+  const char* err = prove_segments_impl(circuit, suite, po2, write_version, version, jobs, njobs, in_flight);
+  // the buffer sets are freed; the calling thread (one of the provers) keeps no device memory
+  drain_after_error();
+  release_thread_memory();
+  return err;
+}
+
+extern "C" const char* r0hip_prove_trace_segments(int suite, uint32_t po2, r0hip_trace_job* jobs, size_t njobs,
+                                                  uint32_t in_flight, int verify) {
+  const char* err = nullptr;
+  try {
+    R0_REQUIRE(suite >= 0 && suite <= 2, "unknown hash suite");
+    R0_REQUIRE(po2 >= 2 && po2 <= 24, "po2 out of range");
+    R0_REQUIRE(njobs == 0 || jobs, "jobs is NULL");
+    ensure_init();
+    for (size_t i = 0; i < njobs; i++) {
+      jobs[i].error = nullptr;
+      jobs[i].seal_len = 0;
+      jobs[i].verified = 0;
+      jobs[i].verify_ms = 0;
+    }
+    if (njobs) {
+      const size_t k = std::max<size_t>(1, std::min<size_t>(in_flight ? in_flight : 2, njobs));
+      err = prove_trace_jobs(suite, po2, jobs, njobs, k, verify != 0);
+    }
+  } catch (const std::exception& e) {
+    err = dup_msg(e.what());
+  } catch (...) {
+    err = dup_msg("r0hip: unknown error");
+  }
+  // the trace sets are freed; the calling thread (one of the provers) keeps no device memory
+  drain_after_error();
+  release_thread_memory();
+  return err;
 }

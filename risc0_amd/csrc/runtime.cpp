@@ -55,6 +55,17 @@ struct ThreadCtx {
   std::multimap<size_t, void*> pool;  // free blocks by size, last used on `stream`
   Stage stage;
   std::vector<uint8_t*> stage_old;
+  // the idle pool and scratch blocks to the shared lists (caller holds g_mu; stream drained)
+  void hand_back_memory() {
+    for (auto& kv : pool) g_orphans.emplace(kv.first, kv.second);
+    for (auto& kv : scratch)
+      if (kv.second.p) {
+        g_scratch_orphans[kv.first].emplace(kv.second.bytes, kv.second.p);
+        g_mem_live.fetch_sub(kv.second.bytes, std::memory_order_relaxed);
+      }
+    pool.clear();
+    scratch.clear();
+  }
   ~ThreadCtx() {
     // A worker thread hands its stream and memory over when it exits — no HIP calls
     // here (thread-exit destructors run after tools' per-thread state is gone). Every
@@ -62,17 +73,10 @@ struct ThreadCtx {
     // thread's context dies in process teardown and is left alone.
     if (!stream || std::this_thread::get_id() == g_main_thread) return;
     std::lock_guard<std::mutex> lk(g_mu);
-    for (auto& kv : pool) g_orphans.emplace(kv.first, kv.second);
-    for (auto& kv : scratch)
-      if (kv.second.p) {
-        g_scratch_orphans[kv.first].emplace(kv.second.bytes, kv.second.p);
-        g_mem_live.fetch_sub(kv.second.bytes, std::memory_order_relaxed);
-      }
+    hand_back_memory();
     g_free_streams.push_back(stream);
     if (stage.base) g_free_stages.push_back(Stage{stage.base, stage.cap, 0});
     // superseded arenas in stage_old are left allocated (rare: only after growth)
-    pool.clear();
-    scratch.clear();
   }
 };
 thread_local ThreadCtx t_ctx;
@@ -159,6 +163,12 @@ hipStream_t stream() {
 
 void drain_after_error() noexcept {
   if (t_ctx.stream) (void)hipStreamSynchronize(t_ctx.stream);
+}
+
+void release_thread_memory() noexcept {
+  if (!t_ctx.stream) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  t_ctx.hand_back_memory();
 }
 
 const uint32_t* dev_table(const std::string& key, const std::function<std::vector<uint32_t>()>& gen) {

@@ -125,6 +125,12 @@ void* scratch(size_t bytes, int slot = kSlotDefault);
 // status), so no buffer is reused or handed to another thread while kernels still use it.
 // Only a thread that has a stream drains; it never creates one.
 void drain_after_error() noexcept;
+// At the end of every entry point, with this thread's stream drained: hand the thread's idle
+// pool and scratch blocks to the shared lists, where any thread's next request finds them (as
+// an exiting worker thread's are handed over). A caller's thread — one that proves and
+// returns, or the calling thread of r0hip_prove_segments, which runs a prover itself — then
+// keeps no device memory between calls.
+void release_thread_memory() noexcept;
 
 // Stream-ordered host->device upload through a pinned bump arena, so the caller's
 // host data may die immediately. The arena is recycled by stage_reset() (call only

@@ -53,10 +53,9 @@ constexpr uint32_t kErrLookupIndex = 0x20008u;   // tables.h:43-46
 constexpr uint32_t kErrBigint = 0x20009u;        // bigIntExtern past the trace's bytes
 constexpr uint32_t kErrDiffCount = 0x2000Au;     // getDiffCount past the trace's cycles
 constexpr uint32_t kErrMajor = 0x2000Bu;         // a cycle's major outside the 13 instruction arms
-// an injected word in a column the row's instruction arm does not take from the injector: the
-// generated arms assume each arm's injected columns (tools/gen_rv32im_witgen.py, Path) and would
-// not read or check it as the reference does
-constexpr uint32_t kErrInjectorCol = 0x2000Cu;
+// an injector entry of row r whose offset lies in another row (the reference's Injector::set
+// writes only its own row, witgen/mod.rs:352-377; the init pass writes a row per lane)
+constexpr uint32_t kErrInjectorRow = 0x2000Cu;
 
 struct Args {
   uint32_t* data;    // DATA x rows, column-major (MutableBufObj over Buffer<checked>)
@@ -335,32 +334,39 @@ const char* rv32im_witgen_message(uint32_t k);
 // the driver (rv32im_witgen.hip): both phases over cycles [0, last_cycle) with the preflight
 // arrays resident on the device; synchronises, throws on a failed check
 // zeroize (the prover's path): the data group is the prover's own, INVALID in the injected
-// columns but the injector's words (rv32im_prover_groups_init; its other words are never read),
-// and the merge writes 0 for INVALID words (eltwise_zeroize fused, as hal_generate_witness does
-// right after stepExec, witgen/mod.rs:166-169)
+// columns but the injector's words (rv32im_prover_groups_fill + rv32im_prover_inject; its other
+// words are never read), and the merge writes 0 for INVALID words (eltwise_zeroize fused, as
+// hal_generate_witness does right after stepExec, witgen/mod.rs:166-169). extra_err: the inject
+// pass's record (4 words): a failure there is raised; word 3 set (an entry outside its row's
+// injected columns) calls reinit, which must leave the group as the reference prepares it (all
+// INVALID, the injector scattered in), and the merge then reads every column back.
 void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
                        const rvwg::PreflightCycle* d_cycles, const rvwg::MemoryTxn* d_txns, size_t n_txns,
                        const uint8_t* d_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle,
-                       bool zeroize = false, const uint32_t* extra_err = nullptr);
-// The prover's groups before witness generation, in one pass over the rows (replacing the INVALID
-// fills of WitnessGenerator::new and ::accum, witgen/mod.rs:135-170, 178-186, and the injector's
-// scatter): data INVALID in the injected columns — the only ones any arm or the prover-mode merge
-// reads back (every other data word is written by the merge) — then the injector's entries
-// (offsets at or past `limit` skipped, reads clamped to index[inj_rows]); code 0; accum INVALID in
-// the machine columns the accumulation's phase 3 adds to, 0 elsewhere: its zeroize then has
-// nothing left to change (AccumStep::zeroed; every row is stepped)
-// Each injector entry is checked against its row's arm (the cycle's major in d_cycles): an entry
-// in a column the arm does not take from the injector records kErrInjectorCol in err (3 words,
-// zeroed by the caller), which rv32im_witgen_dev's extra_err reports.
-void rv32im_prover_groups_init(hipStream_t s, uint32_t* data, uint32_t* code, uint32_t* accum, size_t rows,
-                               size_t accum_cols, const uint32_t* index, const uint32_t* offsets,
-                               const uint32_t* values, size_t inj_rows, uint64_t limit,
-                               const rvwg::PreflightCycle* d_cycles, uint32_t* err);
+                       bool zeroize = false, const uint32_t* extra_err = nullptr,
+                       const std::function<void()>& reinit = {});
+// The prover's groups before witness generation (replacing the INVALID fills of
+// WitnessGenerator::new and ::accum, witgen/mod.rs:135-170, 178-186, and the injector's scatter).
+// fill, one pass over the rows with no input (queued before the trace lands): data INVALID in
+// the injected columns — the only ones any arm or the prover-mode merge reads back (every other
+// data word is written by the merge) —; code 0; accum INVALID in the machine columns the
+// accumulation's phase 3 adds to, 0 elsewhere: its zeroize then has nothing left to change
+// (AccumStep::zeroed; every row is stepped).
+void rv32im_prover_groups_fill(hipStream_t s, uint32_t* data, uint32_t* code, uint32_t* accum, size_t rows,
+                               size_t accum_cols);
+// inject: the injector's entries (offsets at or past `limit` skipped, reads clamped to
+// index[inj_rows]), one lane per row; an entry in another row records kErrInjectorRow in err, an
+// entry in a column its row's arm (the cycle's major) does not take from the injector sets err[3]
+// (err: 4 words, zeroed by the caller; rv32im_witgen_dev's extra_err).
+void rv32im_prover_inject(hipStream_t s, uint32_t* data, size_t rows, const uint32_t* index, const uint32_t* offsets,
+                          const uint32_t* values, size_t inj_rows, uint64_t limit, const rvwg::PreflightCycle* d_cycles,
+                          uint32_t* err);
 // the same from host preflight arrays (uploaded first), as RawPreflightTrace hands them over
 void rv32im_witgen(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
                    const rvwg::PreflightCycle* h_cycles, const rvwg::MemoryTxn* h_txns, size_t n_txns,
                    const uint8_t* h_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle,
-                   bool zeroize = false, const uint32_t* extra_err = nullptr);
+                   bool zeroize = false, const uint32_t* extra_err = nullptr,
+                   const std::function<void()>& reinit = {});
 // the host preflight cycles uploaded into this thread's witgen scratch (what rv32im_witgen does
 // first), for callers that need them on the device before witness generation
 const rvwg::PreflightCycle* rv32im_upload_cycles(const rvwg::PreflightCycle* h_cycles, size_t n);

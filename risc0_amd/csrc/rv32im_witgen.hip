@@ -22,6 +22,7 @@
 // 27-word read-back for the launch sizes, a radix sort). Checks that throw in the reference
 // record the lane's first failure, raised after the kernels drain.
 #include <cstdlib>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -54,9 +55,9 @@ std::string witgen_error(const uint32_t* e) {
     case kErrBigint: return "bigint bytes past the preflight's" + at;
     case kErrDiffCount: return "getDiffCount past the preflight's cycles" + at;
     case kErrMajor: return "cycle major " + std::to_string(detail) + " selects no instruction arm" + at;
-    case kErrInjectorCol:
-      return "injector sets col " + std::to_string(detail) + ", which this row's instruction arm does not take from "
-             "the injector" + at;
+    case kErrInjectorRow:
+      return "injector entry of row " + std::to_string(cycle) + " sets word " + std::to_string(detail) +
+             " of another row (Injector::set writes its own row)";
     default: return "witness generation error " + std::to_string(code) + at;
   }
 }
@@ -112,12 +113,14 @@ __global__ __launch_bounds__(kBucketThreads) void bin_pos_kernel(const uint32_t*
 // the data group from the arms' compact values, a column line at a time: word (col, row) is the
 // row's stored value if its arm stored one, else the data word as the injector left it (an
 // injected value or INVALID). Every word of rows [0, rows) is written, so each line of a column
-// goes out whole. prover: the data group is the prover's own (INVALID but where the injector
-// wrote), so only injected columns are read back, and INVALID becomes 0 (the zeroize).
+// goes out whole. prover: the data group is the prover's own, INVALID in the injected columns but
+// where the injector wrote, so only those are read back, and INVALID becomes 0 (the zeroize).
+// full (the public witgen, or a prover whose injector sets words outside its rows' injected
+// columns, re-initialised for it): every column is read back.
 __global__ __launch_bounds__(kMergeThreads) void merge_kernel(uint32_t* data, uint32_t rows, uint32_t ncycles,
                                                              const uint32_t* cbuf, const uint8_t* keys,
                                                              const uint32_t* pos, const int16_t* slot_of, BinTable T,
-                                                             bool prover, bool xcd_tiles, uint32_t* err) {
+                                                             bool prover, bool full, bool xcd_tiles, uint32_t* err) {
   constexpr uint32_t kMaskWords = (rvwg::kDataCols + 31) / 32;
   __shared__ int16_t slot[(rvwg::kMajors + 1) * rvwg::kDataCols];
   __shared__ uint32_t msk[kMaskWords][kMergeThreads];  // this thread's row: its arm's stored-slot bits
@@ -158,10 +161,12 @@ __global__ __launch_bounds__(kMergeThreads) void merge_kernel(uint32_t* data, ui
     // the stored value and the data word the row keeps otherwise, loaded side by side (the
     // read-back no longer waits on the compact load's result)
     const uint32_t c = stored ? cb[size_t(slot) * n + i] : rvwg::kInvalid;
-    const uint32_t d = !prover || (e & rvwg::kInjectedCol) ? *p : rvwg::kInvalid;
-    // the caller's data group (the public witgen) holds a word the arm does not take from the
-    // injector: the arms never read or checked it (the prover's injector is checked at init)
-    if (!prover && stepped && !(e & rvwg::kInjectedCol) && d != rvwg::kInvalid && atomicCAS(err, 0u, rvwg::kErrInjectorCol) == 0u) {
+    const uint32_t d = full || (e & rvwg::kInjectedCol) ? *p : rvwg::kInvalid;
+    // a word set before the arm ran in a column the arm stores but does not take from the
+    // injector (so never compared in the arm): Buffer::set's check (buffers.h:30-42) fails only
+    // on another value; a word in a column the arm does not store is kept, as there
+    if (full && stepped && stored && !(e & rvwg::kInjectedCol) && d != rvwg::kInvalid && d != c &&
+        atomicCAS(err, 0u, rvwg::kErrInconsistent) == 0u) {
       err[1] = r;
       err[2] = col;
     }
@@ -171,55 +176,62 @@ __global__ __launch_bounds__(kMergeThreads) void merge_kernel(uint32_t* data, ui
   }
 }
 
-// one lane per row: the injected columns INVALID, the row's injector entries, code and accum 0
+// one lane per row: the injected columns INVALID, code 0, accum INVALID in [acc_inv_begin,
+// acc_inv_end) and 0 elsewhere (needs no input: queued before the trace has landed)
 struct InjectedCols {
   uint32_t n;
   uint8_t col[rvwg::kDataCols];
   uint32_t arm_mask[rvwg::kMajors][(rvwg::kDataCols + 31) / 32];  // kInjectedCol per arm, as bits
 };
-__global__ __launch_bounds__(kMergeThreads) void prover_groups_init_kernel(
-    uint32_t* data, uint32_t* code, uint32_t* accum, uint32_t rows, uint32_t accum_cols, InjectedCols U,
-    const uint32_t* index, const uint32_t* offsets, const uint32_t* values, uint32_t inj_rows, uint64_t limit,
-    uint32_t acc_inv_begin, uint32_t acc_inv_end, const rvwg::PreflightCycle* cycles, uint32_t row_shift,
-    uint32_t* err) {
+__global__ __launch_bounds__(kMergeThreads) void prover_groups_fill_kernel(uint32_t* data, uint32_t* code,
+                                                                          uint32_t* accum, uint32_t rows,
+                                                                          uint32_t accum_cols, InjectedCols U,
+                                                                          uint32_t acc_inv_begin,
+                                                                          uint32_t acc_inv_end) {
   const uint32_t r = blockIdx.x * kMergeThreads + threadIdx.x;
   if (r >= rows) return;
   for (uint32_t k = 0; k < U.n; k++) data[uint64_t(U.col[k]) * rows + r] = rvwg::kInvalid;
   code[r] = 0u;
   for (uint32_t c = 0; c < accum_cols; c++)
     accum[uint64_t(c) * rows + r] = c >= acc_inv_begin && c < acc_inv_end ? rvwg::kInvalid : 0u;
-  if (r < inj_rows) {
-    const uint32_t end = min(index[r + 1], index[inj_rows]);
-    const uint32_t arm = cycles[r].major;  // a major past the arms fails in the bucket kernel
-    for (uint32_t i = index[r]; i < end; i++) {
-      const uint32_t off = offsets[i];
-      if (off >= limit) continue;
-      data[off] = values[i];
-      const uint32_t col = off >> row_shift;
-      if (arm < rvwg::kMajors && !((U.arm_mask[arm][col >> 5] >> (col & 31)) & 1u) &&
-          atomicCAS(err, 0u, rvwg::kErrInjectorCol) == 0u) {
+}
+
+// one lane per injector row: its entries (Injector::set writes only its own row, witgen/mod.rs:
+// 352-377; an entry of another row is refused). err[3] != 0 marks an entry in a column the row's
+// arm does not take from the injector: the prover then re-initialises the group whole
+// (rv32im_witgen_dev's reinit) so the merge can read every column back.
+__global__ __launch_bounds__(kMergeThreads) void prover_inject_kernel(uint32_t* data, uint32_t rows,
+                                                                     InjectedCols U, const uint32_t* index,
+                                                                     const uint32_t* offsets, const uint32_t* values,
+                                                                     uint32_t inj_rows, uint64_t limit,
+                                                                     const rvwg::PreflightCycle* cycles,
+                                                                     uint32_t row_shift, uint32_t* err) {
+  const uint32_t r = blockIdx.x * kMergeThreads + threadIdx.x;
+  if (r >= inj_rows) return;
+  const uint32_t end = min(index[r + 1], index[inj_rows]);
+  const uint32_t arm = cycles[r].major;  // a major past the arms fails in the bucket kernel
+  for (uint32_t i = index[r]; i < end; i++) {
+    const uint32_t off = offsets[i];
+    if (off >= limit) continue;
+    if ((off & (rows - 1)) != r) {
+      if (atomicCAS(err, 0u, rvwg::kErrInjectorRow) == 0u) {
         err[1] = r;
-        err[2] = col;
+        err[2] = off;
       }
+      continue;
     }
+    data[off] = values[i];
+    const uint32_t col = off >> row_shift;
+    if (arm < rvwg::kMajors && !((U.arm_mask[arm][col >> 5] >> (col & 31)) & 1u)) atomicOr(err + 3, 1u);
   }
 }
 
 }  // namespace
 
-void rv32im_prover_groups_init(hipStream_t s, uint32_t* data, uint32_t* code, uint32_t* accum, size_t rows,
-                               size_t accum_cols, const uint32_t* index, const uint32_t* offsets,
-                               const uint32_t* values, size_t inj_rows, uint64_t limit,
-                               const rvwg::PreflightCycle* d_cycles, uint32_t* err) {
+namespace {
+// the data columns any arm takes from the injector, and each arm's (the slot table's kInjectedCol)
+const InjectedCols& injected_cols() {
   using namespace rvwg;
-  R0_REQUIRE(rows >= 4 && rows <= (size_t(1) << 24) && (rows & (rows - 1)) == 0 && inj_rows <= rows,
-             "rv32im_prover_groups_init: bad shape");
-  // accum: the machine columns phase 3 adds the previous row's totals to (kUserAccumSplit = 23 up
-  // to the last group, rv32im-sys/kernels/cxx/ffi.cpp:341-356) stay INVALID as the reference
-  // leaves the cells stepAccum does not write (INVALID + total is what it stores there); every
-  // other accum cell is written by the step or is INVALID only to be zeroized, so it starts 0
-  R0_REQUIRE(accum_cols == 103, "rv32im_prover_groups_init: the rv32im accum group has 103 columns");
-  const uint32_t acc_inv_begin = 23, acc_inv_end = 23 + 4 * ((103 - 23) / 4 - 1);
   static const InjectedCols U = [] {
     InjectedCols u{};
     const int16_t* t = rv32im_witgen_slot_table();
@@ -234,18 +246,46 @@ void rv32im_prover_groups_init(hipStream_t s, uint32_t* data, uint32_t* code, ui
     }
     return u;
   }();
+  return U;
+}
+}  // namespace
+
+void rv32im_prover_groups_fill(hipStream_t s, uint32_t* data, uint32_t* code, uint32_t* accum, size_t rows,
+                               size_t accum_cols) {
+  using namespace rvwg;
+  R0_REQUIRE(rows >= 4 && rows <= (size_t(1) << 24) && (rows & (rows - 1)) == 0,
+             "rv32im_prover_groups_fill: bad shape");
+  // accum: the machine columns phase 3 adds the previous row's totals to (kUserAccumSplit = 23 up
+  // to the last group, rv32im-sys/kernels/cxx/ffi.cpp:341-356) stay INVALID as the reference
+  // leaves the cells stepAccum does not write (INVALID + total is what it stores there); every
+  // other accum cell is written by the step or is INVALID only to be zeroized, so it starts 0
+  R0_REQUIRE(accum_cols == 103, "rv32im_prover_groups_fill: the rv32im accum group has 103 columns");
+  const uint32_t acc_inv_begin = 23, acc_inv_end = 23 + 4 * ((103 - 23) / 4 - 1);
+  const InjectedCols& U = injected_cols();
   KScope ks("rv32im_groups_init", double(rows) * 4.0 * (U.n + 1 + accum_cols));
-  hipLaunchKernelGGL(prover_groups_init_kernel, dim3(uint32_t((rows + kMergeThreads - 1) / kMergeThreads)),
-                     dim3(kMergeThreads), 0, s, data, code, accum, uint32_t(rows), uint32_t(accum_cols), U, index,
-                     offsets, values, uint32_t(inj_rows), limit, acc_inv_begin, acc_inv_end, d_cycles,
-                     uint32_t(__builtin_ctzll(rows)), err);
+  hipLaunchKernelGGL(prover_groups_fill_kernel, dim3(uint32_t((rows + kMergeThreads - 1) / kMergeThreads)),
+                     dim3(kMergeThreads), 0, s, data, code, accum, uint32_t(rows), uint32_t(accum_cols), U,
+                     acc_inv_begin, acc_inv_end);
+  HIP_OK(hipGetLastError());
+}
+
+void rv32im_prover_inject(hipStream_t s, uint32_t* data, size_t rows, const uint32_t* index, const uint32_t* offsets,
+                          const uint32_t* values, size_t inj_rows, uint64_t limit, const rvwg::PreflightCycle* d_cycles,
+                          uint32_t* err) {
+  R0_REQUIRE(rows >= 4 && rows <= (size_t(1) << 24) && (rows & (rows - 1)) == 0 && inj_rows <= rows,
+             "rv32im_prover_inject: bad shape");
+  if (inj_rows == 0) return;
+  KScope ks("rv32im_groups_init", double(inj_rows) * 8.0);
+  hipLaunchKernelGGL(prover_inject_kernel, dim3(uint32_t((inj_rows + kMergeThreads - 1) / kMergeThreads)),
+                     dim3(kMergeThreads), 0, s, data, uint32_t(rows), injected_cols(), index, offsets, values,
+                     uint32_t(inj_rows), limit, d_cycles, uint32_t(__builtin_ctzll(rows)), err);
   HIP_OK(hipGetLastError());
 }
 
 void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
                        const rvwg::PreflightCycle* d_cycles, const rvwg::MemoryTxn* d_txns, size_t n_txns,
                        const uint8_t* d_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle,
-                       bool zeroize, const uint32_t* extra_err) {
+                       bool zeroize, const uint32_t* extra_err, const std::function<void()>& reinit) {
   using namespace rvwg;
   R0_REQUIRE(mode <= 2, "rv32im_witgen: mode must be 0 (parallel), 1 (forward) or 2 (reverse)");
   R0_REQUIRE(rows >= 4 && (rows & (rows - 1)) == 0 && rows <= (size_t(1) << 24),
@@ -300,16 +340,27 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
     const char* e = std::getenv("R0_RVWG_MERGE_XCD");
     return !(e && e[0] == '0');
   }();
-  uint32_t h[4 + kBins];
+  uint32_t h[4 + kBins], h_init[4] = {0, 0, 0, 0};
   {
     KScope ks("rv32im_witgen_bucket", double(last_cycle) * 2 * sizeof(PreflightCycle));
     hipLaunchKernelGGL(bucket_count_kernel, dim3(g), dim3(kBucketThreads), 0, s, A, table_split, counts, keys, vals,
                        minor_bits);
     HIP_OK(hipGetLastError());
     HIP_OK(hipMemcpyAsync(h, A.err, sizeof(h), hipMemcpyDeviceToHost, s));  // err[0..2], pad, counts
+    if (extra_err) HIP_OK(hipMemcpyAsync(h_init, extra_err, sizeof(h_init), hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
   }
+  R0_REQUIRE(h_init[0] == 0, "rv32im witgen: " + witgen_error(h_init));
   R0_REQUIRE(h[0] == 0, "rv32im witgen: " + witgen_error(h));
+  // the prover's injector set a word in a column its row's arm does not take from the injector:
+  // the group is re-initialised whole (INVALID, the injector scattered in, as the reference
+  // prepares it) and the merge reads every column back and checks it as Buffer::set does
+  bool full = !zeroize;
+  if (zeroize && h_init[3]) {
+    R0_REQUIRE(static_cast<bool>(reinit), "rv32im witgen: injector outside the arms' columns and no re-initialisation");
+    reinit();
+    full = true;
+  }
   const uint32_t* cnt = h + 4;  // counts start at A.err + 4
   BinTable T{};
   T.minor_bits = minor_bits;
@@ -350,14 +401,13 @@ void rv32im_witgen_dev(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* g
     upload_async(d_slot, rv32im_witgen_slot_table(), slot_bytes);
     KScope ks("rv32im_witgen_merge", double(rows) * kDataCols * 8.0 + double(cwords) * 4.0);
     hipLaunchKernelGGL(merge_kernel, dim3(uint32_t((rows + kMergeThreads - 1) / kMergeThreads)), dim3(kMergeThreads), 0,
-                       s, data, uint32_t(rows), last_cycle, cbuf, keys, pos, d_slot, T, zeroize, merge_xcd, A.err);
+                       s, data, uint32_t(rows), last_cycle, cbuf, keys, pos, d_slot, T, zeroize, full, merge_xcd,
+                       A.err);
     HIP_OK(hipGetLastError());
   }
-  uint32_t h_err[3] = {0, 0, 0}, h_extra[3] = {0, 0, 0};
+  uint32_t h_err[3] = {0, 0, 0};
   HIP_OK(hipMemcpyAsync(h_err, A.err, 12, hipMemcpyDeviceToHost, s));
-  if (extra_err) HIP_OK(hipMemcpyAsync(h_extra, extra_err, 12, hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
-  R0_REQUIRE(h_extra[0] == 0, "rv32im witgen: " + witgen_error(h_extra));
   R0_REQUIRE(h_err[0] == 0, "rv32im witgen: " + witgen_error(h_err));
 }
 
@@ -370,7 +420,7 @@ const rvwg::PreflightCycle* rv32im_upload_cycles(const rvwg::PreflightCycle* h_c
 void rv32im_witgen(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* global, size_t rows,
                    const rvwg::PreflightCycle* h_cycles, const rvwg::MemoryTxn* h_txns, size_t n_txns,
                    const uint8_t* h_bigint, size_t n_bigint, uint32_t table_split, uint32_t last_cycle, bool zeroize,
-                   const uint32_t* extra_err) {
+                   const uint32_t* extra_err, const std::function<void()>& reinit) {
   using namespace rvwg;
   R0_REQUIRE(last_cycle <= rows && last_cycle <= (size_t(1) << 24), "rv32im_witgen: more cycles than rows");
   R0_REQUIRE((last_cycle == 0 || h_cycles) && (n_txns == 0 || h_txns) && (n_bigint == 0 || h_bigint),
@@ -382,7 +432,7 @@ void rv32im_witgen(hipStream_t s, uint32_t mode, uint32_t* data, uint32_t* globa
   upload_async(d_txns, h_txns, n_txns * sizeof(MemoryTxn));
   upload_async(d_bigint, h_bigint, n_bigint);
   rv32im_witgen_dev(s, mode, data, global, rows, d_cycles, n_txns ? d_txns : nullptr, n_txns,
-                    n_bigint ? d_bigint : nullptr, n_bigint, table_split, last_cycle, zeroize, extra_err);
+                    n_bigint ? d_bigint : nullptr, n_bigint, table_split, last_cycle, zeroize, extra_err, reinit);
 }
 
 }  // namespace r0

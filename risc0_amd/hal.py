@@ -58,6 +58,7 @@ def _declare(L):
         "r0hip_rv32im_accum": [vp, vp, vp, vp, sz, sz, sz],
         "r0hip_recursion_accum": [vp, vp, vp, vp, vp, sz, sz],
         "r0hip_prove_segments": [C.c_char_p, C.c_int, C.c_uint32, C.c_int, C.c_uint32, C.c_void_p, sz, C.c_uint32],
+        "r0hip_prove_trace_segments": [C.c_int, C.c_uint32, C.c_void_p, sz, C.c_uint32, C.c_int],
         "r0hip_verify_seal": [C.c_char_p, C.c_int, u32p, sz, u32p, sz, u32p, C.POINTER(C.c_uint32)],
         "r0hip_testing_verify_seal_structure": [C.c_char_p, C.c_int, u32p, sz, C.POINTER(C.c_uint32)],
         "r0hip_poly_ext": [C.c_char_p, u32p, u32p, u32p, u32p, u32p],
@@ -561,8 +562,14 @@ class SegmentJob(C.Structure):
     """struct r0hip_segment_job (include/r0hip.h)"""
     _fields_ = [("h_code", C.c_void_p), ("h_data", C.c_void_p), ("h_accum", C.c_void_p), ("h_global", C.c_void_p),
                 ("h_bigint", C.c_void_p), ("n_bigint", C.c_size_t), ("h_seal", C.c_void_p),
+                ("seal_cap", C.c_size_t), ("seal_len", C.c_size_t), ("h_mix_out", C.c_void_p), ("error", C.c_void_p)]
+
+
+class TraceJobStruct(C.Structure):
+    """struct r0hip_trace_job (include/r0hip.h)"""
+    _fields_ = [("trace", TraceInput), ("h_bigint", C.c_void_p), ("n_bigint", C.c_size_t), ("h_seal", C.c_void_p),
                 ("seal_cap", C.c_size_t), ("seal_len", C.c_size_t), ("h_mix_out", C.c_void_p), ("error", C.c_void_p),
-                ("trace", C.c_void_p)]
+                ("verified", C.c_int), ("verify_ms", C.c_double)]
 
 
 class TraceJob:
@@ -622,26 +629,39 @@ class _HostBlock:
             self.ptr = None
 
 
-def prove_trace_segments(hal, po2, traces, in_flight=2, seal_cap=1 << 22):
-    """The native segment pipeline with trace jobs (r0hip_prove_segments, job.trace): each
-    TraceJob is one rv32im prove_core from its preflight trace; an uploader copies the traces
-    into in_flight + 1 device trace sets while in_flight provers run. Returns [(seal, mix)] in
-    job order."""
-    jobs = (SegmentJob * len(traces))()
+def prove_trace_segments(hal, po2, traces, in_flight=2, seal_cap=1 << 22, verify=True, per_job=False):
+    """The GPU worker unit (r0hip_prove_trace_segments): each TraceJob is one rv32im prove_core
+    from its preflight trace; an uploader copies the traces into in_flight + 1 device trace sets
+    while in_flight provers run, and (verify) every seal is checked by the native verifier, the
+    validity equation included, on a host thread beside the proofs. Returns [(seal, mix)] in job
+    order and raises on any failed job; per_job=True returns [(seal, mix, error or None,
+    verify_ms)] instead, without raising for a job's own failure."""
+    jobs = (TraceJobStruct * len(traces))()
     seals, mixes, keep = [], [], []
     for j, t in zip(jobs, traces):
         keep.append(t)
-        j.trace = C.cast(C.pointer(t.struct), C.c_void_p).value
+        j.trace = t.struct
         if t.backs is not None:
             j.h_bigint, j.n_bigint = C.cast(t.backs, C.c_void_p).value, len(t.backs)
         seals.append(np.zeros(seal_cap, dtype=np.uint32))
         mixes.append(np.zeros(36, dtype=np.uint32))
         j.h_seal, j.seal_cap, j.h_mix_out = seals[-1].ctypes.data, seal_cap, mixes[-1].ctypes.data
-    err = lib().r0hip_prove_segments(b"rv32im", hal.suite, po2, 1, 2, C.cast(jobs, C.c_void_p), len(traces), in_flight)
+    err = lib().r0hip_prove_trace_segments(hal.suite, po2, C.cast(jobs, C.c_void_p), len(traces), in_flight,
+                                           int(bool(verify)))
+    errors = []
     for j in jobs:
+        errors.append(C.cast(j.error, C.c_char_p).value.decode() if j.error else None)
         if j.error:
             libc_free(j.error)
+    if per_job:
+        if err and not any(errors):
+            check(err)  # a failure of the call itself, not of a job
+        elif err:
+            libc_free(err)
+        return [(seal[: j.seal_len].copy(), mix, e, j.verify_ms) for j, seal, mix, e in zip(jobs, seals, mixes, errors)]
     check(err)
+    if verify:
+        assert all(j.verified for j in jobs)
     return [(seal[: j.seal_len].copy(), mix) for j, seal, mix in zip(jobs, seals, mixes)]
 
 

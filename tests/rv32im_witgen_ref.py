@@ -56,13 +56,16 @@ def injector_arrays(trace, lay=None):
     return trace.injector_arrays(lay)
 
 
-def prove_from_trace(trace, suite, oracle, mode=MODE_SEQ_FORWARD):
+def prove_from_trace(trace, suite, oracle, mode=MODE_SEQ_FORWARD, data_patch=()):
     """the reference's prove_core from a preflight on the CPU (SegmentProverImpl::prove_core,
     prove/hal/mod.rs:143-224): the compiled reference witgen, zeroize, the oracle prover with
     the compiled reference accumulation run on the drawn mix (oracle_prove_segment_cb), INVALID
-    accum words zeroized. Returns (seal, mix, data, global, accum)."""
+    accum words zeroized. data_patch: (offset, word) pairs set in the data group after the
+    injector (extra injector entries). Returns (seal, mix, data, global, accum)."""
     rows = 1 << trace.po2
     data, glob, cyc, tx = inputs(trace)
+    for off, word in data_patch:
+        data[off] = word
     d, g = run(data, glob, cyc, tx, trace.table_split_cycle, rows, mode, trace.bigint_array())
     d = np.where(d == INVALID, 0, d).astype(np.uint32)
     g = np.where(g == INVALID, 0, g).astype(np.uint32)

@@ -732,11 +732,10 @@ def test_steady_state_proving_makes_no_hipmalloc(oracle):
     globs = [dev(h, glob) for _ in range(2)]
     version = 2 if case["circuit"] == "rv32im" else None
     seals = {}
-    # start from a clean pool: blocks other tests' threads left (other sizes) would be
-    # matched up to 25% larger in whatever order threads race for them. Those threads hand
-    # their blocks back from thread-exit destructors, after their joins returned: wait for
-    # that first, or blocks of other sizes land in the pool mid-test
-    time.sleep(1.0)
+    # start from a clean pool: blocks other tests' calls left (other sizes) would be matched
+    # up to 25% larger in whatever order threads race for them. Every entry point hands its
+    # thread's idle blocks back to the shared pool before it returns (release_thread_memory,
+    # runtime.cpp), so nothing lands in the pool after the call that used it has returned
     r.trim()
 
     def batch(tag):
@@ -747,13 +746,9 @@ def test_steady_state_proving_makes_no_hipmalloc(oracle):
             t.start()
         for t in ts:
             t.join()
-        # a thread hands its blocks back in its C++ thread_local destructor, which runs as the
-        # OS thread exits — after Thread.join() has returned — so the next batch's threads could
-        # otherwise start before the blocks are back and allocate (a test race, not a leak)
-        time.sleep(0.2)
 
     # warm until a whole batch allocates nothing: some slots are asked small and then grown
-    # within a proof, and blocks go back to a shared pool at thread exit, so which thread
+    # within a proof, and blocks go back to a shared pool at the end of each call, so which thread
     # finds which block depends on the race; once the pool holds blocks of every size both
     # interleavings need, proving allocates no more (a leak would keep allocating here)
     # (three batches in a row, since one or two interleavings that happen to allocate nothing
@@ -774,6 +769,8 @@ def test_steady_state_proving_makes_no_hipmalloc(oracle):
     os.write(2, b"steady batch ends\n")
     after = r.mem_stats()
     assert after["mallocs"] == before["mallocs"], (before, after)
+    # no thread keeps a proof's blocks past its call: live bytes are the test's own buffers again
+    assert after["live"] == before["live"], (before, after)
     assert after["peak_live"] > after["live"] >= 0
     assert after["reserved"] >= after["peak_live"]
     for i in range(2):

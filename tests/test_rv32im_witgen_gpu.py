@@ -228,7 +228,7 @@ def _trace_job(r, t, pinned=False):
 
 
 def test_prove_segments_trace_jobs_match_single(hal):
-    """the segment pipeline's trace jobs (r0hip_segment_job.trace: an uploader stages each
+    """the segment pipeline's trace jobs (r0hip_prove_trace_segments: an uploader stages each
     preflight trace into one of in_flight + 1 device trace sets while the provers run, as r0vm's
     GPU queue does): six distinct po2=14 segments — loop guests of different lengths, a random
     loop body, a BigInt ecall trace; page-locked and pageable inputs — over 2 provers and 3 sets
@@ -252,7 +252,7 @@ def test_prove_segments_trace_jobs_match_single(hal):
 
 def test_prove_segments_trace_job_errors(hal):
     """a trace job whose injector index decreases fails with the host check's message (the other
-    jobs still prove), a call mixing trace and witness jobs is refused, and the next call is clean"""
+    jobs still prove), and the next call is clean"""
     import risc0_amd as r
     t = T.loop_s_trace(14, 100, seed=3)
     good = _trace_job(r, t)
@@ -264,6 +264,41 @@ def test_prove_segments_trace_job_errors(hal):
     ref = r.prove_segment_trace(hal, 14, good.glob, good.index, good.offsets, good.values, good.cycles, good.txns,
                                 t.table_split_cycle)
     assert np.array_equal(seal, ref[0])
+
+
+def test_prove_trace_segments_verification_fails_the_job(hal, monkeypatch):
+    """r0hip_prove_trace_segments checks every seal with the native verifier (validity equation
+    included) on a host thread beside the proofs, as ProverImpl::prove_segment_core verifies a
+    receipt before it returns it (prover_impl.rs:262-280): every job of a clean call is verified;
+    a job whose seal fails the check (a bit flipped in its first Merkle root by the testing hook
+    R0HIP_TESTING_CORRUPT_SEAL_JOB) reports "receipt verification failed" and the other jobs still
+    return their verified seals"""
+    import risc0_amd as r
+    traces = [T.loop_s_trace(14, 150 + 31 * i, seed=70 + i) for i in range(4)]
+    jobs = [_trace_job(r, t) for t in traces]
+    clean = r.prove_trace_segments(hal, 14, jobs, in_flight=2, per_job=True)
+    assert all(e is None and ms > 0 for _, _, e, ms in clean)
+    monkeypatch.setenv("R0HIP_TESTING_CORRUPT_SEAL_JOB", "2")
+    got = r.prove_trace_segments(hal, 14, jobs, in_flight=2, per_job=True)
+    monkeypatch.delenv("R0HIP_TESTING_CORRUPT_SEAL_JOB")
+    for i, ((seal, mix, err, _), (cseal, cmix, _, _)) in enumerate(zip(got, clean)):
+        if i == 2:
+            assert err and "receipt verification failed" in err, err
+            assert not np.array_equal(seal, cseal)
+        else:
+            assert err is None and np.array_equal(seal, cseal) and np.array_equal(mix, cmix)
+    with pytest.raises(r.R0HipError, match="segment 2: receipt verification failed"):
+        monkeypatch.setenv("R0HIP_TESTING_CORRUPT_SEAL_JOB", "2")
+        try:
+            r.prove_trace_segments(hal, 14, jobs, in_flight=2)
+        finally:
+            monkeypatch.delenv("R0HIP_TESTING_CORRUPT_SEAL_JOB")
+    # without the check the flipped seal is returned as proved (what verify=1 guards against)
+    monkeypatch.setenv("R0HIP_TESTING_CORRUPT_SEAL_JOB", "2")
+    unchecked = r.prove_trace_segments(hal, 14, jobs, in_flight=2, verify=False)
+    monkeypatch.delenv("R0HIP_TESTING_CORRUPT_SEAL_JOB")
+    with pytest.raises(r.R0HipError):
+        r.verify_seal("rv32im", hal.suite, unchecked[2][0], check_validity=True)
 
 
 def test_prove_segment_trace_pinned_inputs_match_pageable(hal):
@@ -327,29 +362,57 @@ def test_loop_s_trace_po2_24_proves_and_verifies(hal):
     r.trim()
 
 
-def test_injector_outside_the_arms_columns_fails(hal):
-    """the generated arms take each arm's injected columns from the injector: an
-    injected word in a column the row's arm does not take — which the reference would read or
-    check — is refused, in the prover's init pass and in the public witgen's merge, and the
-    next call is clean"""
-    import risc0_amd as r
-    t = T.loop_s_trace(14, 200, seed=5)
-    cyc, tx = t.arrays()
-    lay = W.layout()
-    rows = 1 << 14
-    row = int(np.flatnonzero((cyc["state"] == T.DECODE) & (cyc["major"] == 0))[5])
-    col = lay["sha2_u32"][0]
-    idx, off, val = W.injector_arrays(t)
-    at = int(idx[row + 1])  # one more entry at the end of the row
-    off2 = np.insert(off, at, col * rows + row)
-    val2 = np.insert(val, at, W.encode(1))
+def _with_entry(idx, off, val, row, offset, word):
+    """the injector with one more entry at the end of `row` (Injector::set order)"""
+    at = int(idx[row + 1])
     idx2 = idx.copy()
     idx2[row + 1:] += 1
-    with pytest.raises(r.R0HipError, match=f"injector sets col {col}"):
-        r.prove_segment_trace(hal, 14, W.global_words(t), idx2, off2, val2, cyc, tx, t.table_split_cycle)
+    return idx2, np.insert(off, at, offset), np.insert(val, at, word)
+
+
+def test_injector_words_outside_the_arms_columns_match_reference(hal, oracle):
+    """a word set before the arms run in a column the row's arm does not take from the
+    injector is treated as the reference's Buffer::set treats it (buffers.h:30-42): kept when the
+    arm does not store the column, accepted when the arm stores the same value, "Inconsistent set"
+    when it stores another. The public witgen's data group equals the compiled reference's word for
+    word; the prover (an injector entry there) equals the CPU path's seal; the next call is clean."""
+    import risc0_amd as r
+    po2, rows = 14, 1 << 14
+    t = T.loop_s_trace(po2, 200, seed=5)
+    cyc, tx = t.arrays()
+    lay = W.layout()
     data, glob, _, _ = W.inputs(t)
-    data[col * rows + row] = W.encode(1)
-    with pytest.raises(r.R0HipError, match=f"injector sets col {col}"):
-        gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle)
-    seal, _ = r.prove_segment_trace(hal, 14, W.global_words(t), idx, off, val, cyc, tx, t.table_split_cycle)
-    assert r.verify_seal("rv32im", hal.suite, seal, check_validity=True) == 14
+    ref_d, ref_g = W.run(data, glob, cyc, tx, t.table_split_cycle, rows)
+    row = int(np.flatnonzero((cyc["state"] == T.DECODE) & (cyc["major"] == 0))[5])
+    keep_col = lay["sha2_u32"][0]  # the arm neither reads nor writes it: a set word is kept
+    assert ref_d[keep_col * rows + row] == W.INVALID
+    # a column the row's arm writes that the injector left INVALID
+    stored = [c for c in range(W.DATA_COLS) if data[c * rows + row] == W.INVALID and ref_d[c * rows + row] != W.INVALID]
+    same_col = stored[len(stored) // 2]
+    same = int(ref_d[same_col * rows + row])
+    other = (same + 1) % T.P  # another canonical word
+    for col, word, fails in ((keep_col, W.encode(1), False), (same_col, same, False), (same_col, other, True)):
+        d2 = data.copy()
+        d2[col * rows + row] = word
+        if fails:
+            with pytest.raises(RuntimeError, match="Inconsistent set"):
+                W.run(d2, glob, cyc, tx, t.table_split_cycle, rows)
+            with pytest.raises(r.R0HipError, match="Inconsistent set"):
+                gpu_witgen(hal, d2, glob, cyc, tx, t.table_split_cycle)
+        else:
+            rd, rg = W.run(d2, glob, cyc, tx, t.table_split_cycle, rows)
+            gd, gg = gpu_witgen(hal, d2, glob, cyc, tx, t.table_split_cycle)
+            assert np.array_equal(gd, rd) and np.array_equal(gg, rg), (col, int((gd != rd).sum()))
+    idx, off, val = W.injector_arrays(t)
+    # the prover: an injector entry in a column the arm does not take (kept, then zeroized-in)
+    patch = [(keep_col * rows + row, int(W.encode(1)))]
+    ref_seal, ref_mix, _, _, _ = W.prove_from_trace(t, oracle.POSEIDON2, oracle, data_patch=patch)
+    idx2, off2, val2 = _with_entry(idx, off, val, row, *patch[0])
+    seal, mix = r.prove_segment_trace(hal, po2, W.global_words(t), idx2, off2, val2, cyc, tx, t.table_split_cycle)
+    assert np.array_equal(mix, ref_mix) and np.array_equal(seal, ref_seal)
+    # an entry of another row is refused on the host (Injector::set writes its own row)
+    idx3, off3, val3 = _with_entry(idx, off, val, row, keep_col * rows + row + 1, int(W.encode(1)))
+    with pytest.raises(r.R0HipError, match="of another row"):
+        r.prove_segment_trace(hal, po2, W.global_words(t), idx3, off3, val3, cyc, tx, t.table_split_cycle)
+    seal, _ = r.prove_segment_trace(hal, po2, W.global_words(t), idx, off, val, cyc, tx, t.table_split_cycle)
+    assert r.verify_seal("rv32im", hal.suite, seal, check_validity=True) == po2
