@@ -64,6 +64,12 @@ def parse():
                     help="segments of the leg that runs the rv32im accumulation inside the prover on the "
                          "resident witness (r0hip_prove_segment_accum), as the reference's prove_core does; "
                          "reported beside value as with_accumulation; 0 = skip")
+    ap.add_argument("--per-op-steps", type=int, default=3,
+                    help="trace mode: segments of the per_op_abi leg (rank 0): trace 0 proved by the reference prover "
+                         "over the per-op r0hip_* symbols only (integration/hal_prover.cpp), as a Rust HipHal would "
+                         "drive them; 0 = skip")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="trace mode: skip the receipt check of each seal in the pipeline (A/B runs only)")
     ap.add_argument("--cpu-po2", type=int, default=None,
                     help="segment size of the CPU baseline proof (default: the bench's own po2, at most 20)")
     ap.add_argument("--inflight", type=int, default=None,
@@ -248,7 +254,7 @@ def main():
             print(json.dumps({label + "_phases_ms": phases, "seal_words": int(last["seal"].size)}), file=sys.stderr)
         return t, last["seal"], last["mix"]
 
-    resident = None
+    resident = per_op = None
     if trace_mode:
         batch = [tjobs[i % len(tjobs)] for i in range(args.steps)]
         out = {}
@@ -256,7 +262,7 @@ def main():
         def pipeline(jobs_):
             # every seal checked by the native verifier beside the proofs (the worker unit returns
             # only receipts that verified, prover_impl.rs:262-280); a failed check fails the bench
-            res = r.prove_trace_segments(hal, args.po2, jobs_, in_flight=k, per_job=True)
+            res = r.prove_trace_segments(hal, args.po2, jobs_, in_flight=k, per_job=True, verify=not args.no_verify)
             bad = [e for _, _, e, _ in res if e]
             if bad:
                 raise RuntimeError(f"{len(bad)} of {len(res)} segments failed: {bad[0]}")
@@ -281,6 +287,8 @@ def main():
                                 "from k host threads): the round-4 headline, no H2D"}
         if not args.no_prove_only:
             t_w, seal_w, _ = timed_leg(prove_witness, "prove_only")
+        if args.per_op_steps > 0 and rank == 0:
+            per_op = per_op_leg(hal, args, tjobs[0], seal, mix)
     elif program_mode:
         import itertools
         counter = itertools.count()
@@ -383,7 +391,7 @@ def main():
                        **({"guest": args.guest, "distinct_traces_per_rank": len(traces),
                            "distinct_seals_rank0": seals_distinct,
                            "h2d_bytes_per_segment": int(tjobs[0].h2d_bytes()),
-                           "receipts_verified": True, "verify_ms_per_segment": round(verify_ms, 2),
+                           "receipts_verified": not args.no_verify, "verify_ms_per_segment": round(verify_ms, 2),
                            "ms_one_segment_unpipelined": round(1000.0 * t_one, 1)} if trace_mode else {}),
                        **({"programs_per_rank": len(progs), "seal_valid_rank0": bool(program_valid)}
                           if program_mode else {}),
@@ -399,6 +407,8 @@ def main():
             line["end_to_end"] = e2e
         if resident:
             line["resident_trace"] = resident
+        if per_op:
+            line["per_op_abi"] = per_op
         if acc_leg:
             line["with_accumulation"] = acc_leg
         print(json.dumps(line))
@@ -408,6 +418,31 @@ def main():
         # full-size oracle parity failed: the line above carries both digests
         print("bench: GPU seal differs from the CPU oracle's on the same input", file=sys.stderr)
         sys.exit(1)
+
+
+def per_op_leg(hal, args, job, pipeline_seal, pipeline_mix):
+    """The drop-in path's own number: trace 0 proved by the reference prover over ONLY the per-op
+    r0hip_* symbols (integration/hal_prover.cpp: the injector scatter, r0hip_rv32im_witgen, the
+    Prover's make_coeffs / commit_group / finalize / fri_prove and the accumulation, one
+    synchronous call per Hal method, Merkle openings one device-to-host copy per node as with
+    has_unified_memory() = false), what a Rust HipHal behind risc0_zkp::hal::Hal delivers; one
+    segment at a time, from the trace in host memory. Its seal must equal the pipeline's."""
+    sys.path.insert(0, os.path.join(ROOT, "integration"))
+    import halprover
+    halprover.prove_trace(hal, args.po2, job)  # warm the calling thread's pool and the driver
+    phases, seal = {}, None
+    t0 = time.perf_counter()
+    for _ in range(args.per_op_steps):
+        seal, mix = halprover.prove_trace(hal, args.po2, job)
+        for k_, v in halprover.last_profile().items():
+            phases[k_] = phases.get(k_, 0.0) + v / args.per_op_steps
+    t = time.perf_counter() - t0
+    return {"value": round(args.per_op_steps * (1 << args.po2) / t, 1), "unit": "cycles/s",
+            "ms_per_step": round(1000.0 * t / args.per_op_steps, 3), "steps": args.per_op_steps,
+            "seal_equal": bool(np.array_equal(seal, pipeline_seal)), "mix_equal": bool(np.array_equal(mix, pipeline_mix)),
+            "host_phases_ms": {k_: round(v, 2) for k_, v in phases.items()},
+            "note": "trace 0 through the reference prover over the per-op C ABI only (integration/hal_prover.cpp, "
+                    "libr0hip_halprover.so), one segment at a time; seal compared with the pipeline's seal of trace 0"}
 
 
 HBM_PEAK_GBS = 8000.0

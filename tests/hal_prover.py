@@ -288,11 +288,12 @@ class Prover:
                 pos = group
 
 
-def prove_segment(oracle, hal, circuit, po2, code, data, accum, glob):
+def prove_segment(oracle, hal, circuit, po2, code, data, accum, glob, accumulate=None):
     """rv32im prove_core (circuit/rv32im/src/prove/hal/mod.rs:143-224) / recursion
     (circuit/recursion/src/prove/mod.rs:160-230) over device witness buffers. The mix is
-    drawn from the transcript after code and data are committed; `accum` is taken as
-    given (the accumulation witness generation stays the caller's). Returns (seal, mix)."""
+    drawn from the transcript after code and data are committed; `accum` is taken as given,
+    or filled by accumulate(mix_buf, mix) between the mix draw and the accum commit (the
+    circuit HAL's accumulation, witgen/mod.rs:178-221). Returns (seal, mix)."""
     p = Prover(oracle, hal, circuit)
     if circuit == "rv32im":
         p.iop.write([2])  # RV32IM_SEAL_VERSION
@@ -309,5 +310,7 @@ def prove_segment(oracle, hal, circuit, po2, code, data, accum, glob):
     p.commit_group(2, data)
     mix = np.array([p.iop.random_elem() for _ in range(p.taps.d["mix_size"])], np.uint32)
     mix_buf = hal.copy_from_elem("mix", mix)
+    if accumulate is not None:
+        accumulate(mix_buf, mix)
     p.commit_group(0, accum)
     return p.finalize(mix_buf, glob), mix
