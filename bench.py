@@ -51,6 +51,10 @@ def parse():
                     help="trace mode: loop_s = the datasheet's benchmark guest (risc0/zkvm/examples/loop.s under the "
                          "v1compat kernel, datasheet.rs iteration counts); random_loop = a random 32-instruction "
                          "RV32IM body repeated until the segment suspends")
+    ap.add_argument("--session", type=int, default=None,
+                    help="trace mode, configs[3]: ONE loop.s session cut into this many consecutive segments "
+                         "(tests/rv32im_trace.LoopSession); segment i goes to rank i mod N, every segment is proved "
+                         "once in the timed region (steps = the rank's segments)")
     ap.add_argument("--traces", type=int, default=None,
                     help="trace mode: distinct preflight traces per rank, cycled over the timed segments "
                          "(default 4 up to po2=22, 1 above)")
@@ -179,7 +183,15 @@ def main():
         import rv32im_trace as T  # the input generator: a restated preflight (test infrastructure, no oracle)
         ntr = args.traces if args.traces is not None else (4 if args.po2 <= 22 else 1)
         t0 = time.perf_counter()
-        for i in range(max(1, ntr)):
+        if args.session:
+            # configs[3]: this rank's segments of one session, built in parallel worker processes
+            # from the session's state at each (the executor's pass fast-forwards the others)
+            mine = segments_for_rank(rank, world, args.session)
+            args.steps = len(mine)
+            tjobs, trace0 = session_jobs(r, args, mine)
+            traces = [trace0] + [None] * (len(tjobs) - 1)
+            ntr = 0
+        for i in range(max(1, ntr) if not args.session else 0):
             seed = 0x5249534330 + 64 * rank + i
             if args.guest == "loop_s":
                 # the datasheet's iteration count, shortened by a few iterations per trace so the
@@ -201,8 +213,8 @@ def main():
                              bigint=bi if len(bi) else None)
         bigint_records = trace.bigint_records() or None
         del cyc, tx, idx, off, val
-        print(f"rank {rank}: {len(traces)} {args.guest} traces built in {time.perf_counter() - t0:.1f} s (trace 0: "
-              f"{trace.table_split_cycle} rows before the tables, {len(trace.arrays()[1])} memory transactions, "
+        print(f"rank {rank}: {len(tjobs)} {args.guest} traces built in {time.perf_counter() - t0:.1f} s (trace 0: "
+              f"{tjobs[0].table_split} rows before the tables, {tjobs[0].txns.size} memory transactions, "
               f"{tjobs[0].h2d_bytes() / 1e6:.0f} MB to upload)", file=sys.stderr)
 
     progs = []
@@ -309,7 +321,8 @@ def main():
     # ranks that had to share a device (segments.narrow_visible_devices, or the rehearsal switch)
     shared = gather_results({rank: os.environ.get("R0_RANKS_SHARE_DEVICES") == "1"
                              or os.environ.get("R0_BENCH_SHARE_GPUS") == "1"}, dist)
-    cycles_total = world * args.steps * (1 << args.po2)
+    # a session's segments split unevenly when N does not divide it: the whole session counts
+    cycles_total = (args.session if args.session else world * args.steps) * (1 << args.po2)
     value = cycles_total / t
     ms_per_step = 1000.0 * t / args.steps
     prove_only = None
@@ -352,7 +365,12 @@ def main():
                     "(RecursionProverImpl::prove, r0hip_prove_recursion)"
                     if program_mode else
                     f"{args.circuit} segment po2={args.po2}, {args.hashfn} hashfn, witness resident in HBM -> seal on host")
-        if trace_mode and args.guest == "loop_s":
+        if trace_mode and args.session:
+            data = (f"synthetic: ONE run of the datasheet's loop guest (risc0/zkvm/examples/loop.s under a restated "
+                    f"v1compat kernel) cut into {args.session} consecutive po2={args.po2} segments where the executor "
+                    "cuts them (tests/rv32im_trace.LoopSession: each resumes from the previous one's final memory and "
+                    "root); segment i on rank i mod N, each proved once")
+        elif trace_mode and args.guest == "loop_s":
             data = (f"synthetic: the datasheet's loop guest (risc0/zkvm/examples/loop.s under a restated v1compat kernel; "
                     f"{T.loop_s_iterations(args.po2)} iterations less 37 per trace, datasheet.rs:42-58), preflight restated "
                     f"from the reference executor (tests/rv32im_trace.py); {len(traces)} distinct seeded traces per rank, "
@@ -388,6 +406,7 @@ def main():
                        "hip_hw_queues_per_process": int(os.environ.get("GPU_MAX_HW_QUEUES") or 4),
                        "parallelism": f"segment-per-gpu x{world}",
                        "seal_sha256_by_rank": [digests[i] for i in range(world)],
+                       **({"session_segments": args.session} if args.session else {}),
                        **({"guest": args.guest, "distinct_traces_per_rank": len(traces),
                            "distinct_seals_rank0": seals_distinct,
                            "h2d_bytes_per_segment": int(tjobs[0].h2d_bytes()),
@@ -418,6 +437,59 @@ def main():
         # full-size oracle parity failed: the line above carries both digests
         print("bench: GPU seal differs from the CPU oracle's on the same input", file=sys.stderr)
         sys.exit(1)
+
+
+def session_jobs(r, args, mine):
+    """configs[3]'s input for this rank: segments `mine` of ONE loop.s session of args.session
+    segments (tests/rv32im_trace.LoopSession). The executor's pass fast-forwards the session here
+    (a fraction of a second per segment); this rank's first segment is built in this process (its
+    Trace feeds the CPU baseline), the others in worker processes from the session's state at each.
+    Returns (TraceJobs in page-locked memory, the first segment's Trace)."""
+    import concurrent.futures as cf
+    import multiprocessing as mp
+    import rv32im_trace as T
+    it = T.loop_s_session_iterations(args.po2, args.session)
+    seed = 0x5249534330
+    S = T.LoopSession(args.po2, it, seed=seed)
+    states, tr0 = {}, None
+    t0 = time.perf_counter()
+    for k in range(max(mine) + 1):
+        if k == mine[0]:
+            tr0 = S._advance(build=True)
+            continue
+        if k in mine:
+            states[k] = S.state()
+        S._advance(build=False)
+    assert S.terminated == (max(mine) == args.session - 1), "the session does not end at its last segment"
+    print(f"session of {args.session} segments: fast-forwarded to segment {max(mine)} in "
+          f"{time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
+
+    def job(g, idx, off, val, cyc, tx, split, bi, recs):
+        return r.TraceJob(*(r.pinned_copy(a) for a in (g, idx, off, val, cyc, tx)), split, bigint=bi,
+                          bigint_records=recs)
+    cyc, tx = tr0.arrays()
+    jobs = {mine[0]: job(tr0.global_words(), *tr0.injector_arrays(), cyc, tx, tr0.table_split_cycle,
+                         tr0.bigint_array(), tr0.bigint_records())}
+    workers = max(1, min(8, len(states)))
+    if states:
+        with cf.ProcessPoolExecutor(workers, mp_context=mp.get_context("spawn"), initializer=_session_worker_init,
+                                    initargs=(os.path.join(ROOT, "tests"),)) as ex:
+            futs = {ex.submit(_build_segment, args.po2, it, seed, st): k for k, st in states.items()}
+            for n, f in enumerate(cf.as_completed(futs)):
+                out = f.result()
+                jobs[futs[f]] = job(*out[:9])
+                if n % 8 == 7:
+                    print(f"  {n + 1}/{len(states)} segments built", file=sys.stderr, flush=True)
+    return [jobs[k] for k in mine], tr0
+
+
+def _session_worker_init(tests_dir):
+    sys.path.insert(0, tests_dir)
+
+
+def _build_segment(po2, iterations, seed, state):
+    import rv32im_trace as T
+    return T.build_session_segment(po2, iterations, seed, state)
 
 
 def per_op_leg(hal, args, job, pipeline_seal, pipeline_mix):

@@ -66,6 +66,7 @@ uint32_t verify_seal(const CircuitDef& c, int suite, const uint32_t* seal, size_
     len--;
   }
   ReadIOP iop(seal, len, suite);
+  iop.defer = true;  // openings hashed after the transcript, on several threads (check_pending)
   uint32_t psi[16], ci[16];
   for (int i = 0; i < 16; i++) {
     psi[i] = fp_encode(uint8_t(PROOF_SYSTEM_INFO[i]));

@@ -7,11 +7,13 @@
 //   FRI               risc0/zkp/src/verify/fri.rs:36-155
 // No HIP: compiles with g++ as well as hipcc.
 #pragma once
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "transcript.h"
@@ -58,12 +60,25 @@ Digest hash_pair(int suite, const Digest& a, const Digest& b) {
   return p2_hash_words(both, 16);
 }
 
+struct MerkleVerifier;
+// A Merkle opening read from the seal whose hashes are checked later (ReadIOP::defer): the
+// transcript never depends on a hash of an opening, so the query loop reads and checks the
+// arithmetic in order, and the openings' hash paths run afterwards on several threads.
+struct PendingOpening {
+  const MerkleVerifier* tree;
+  const uint32_t* row;   // cols field words
+  const uint32_t* path;  // 8 words per level above the top layer
+  size_t idx;
+};
+
 // read_iop.rs: a cursor over the seal plus the Fiat-Shamir RNG
 struct ReadIOP {
   const uint32_t* words;
   size_t size, pos = 0;
   int suite;
   std::unique_ptr<Rng> rng;
+  bool defer = false;  // Merkle openings go to `pending` instead of being hashed at once
+  std::vector<PendingOpening> pending;
   ReadIOP(const uint32_t* w, size_t n, int s) : words(w), size(n), suite(s), rng(make_rng(s)) {}
   const uint32_t* read(size_t n) {
     if (n > size - pos) throw VerifyError("seal too short");
@@ -106,25 +121,77 @@ struct MerkleVerifier {
     iop.commit(root);
   }
 
-  // opens row `idx`: the column values, checked against the committed tree
+  // opens row `idx`: the column values, checked against the committed tree (now, or with
+  // iop.defer in check_pending)
   const uint32_t* verify(ReadIOP& iop, size_t idx) const {
     if (idx >= rows) throw VerifyError("merkle query out of range");
     const uint32_t* out = iop.read_elems(cols);
-    Digest cur = hash_elems(iop.suite, out, cols);
+    size_t levels = 0;
+    for (size_t i = idx + rows; i >= 2 * top_size; i >>= 1) levels++;
+    const uint32_t* path = iop.read(8 * levels);
+    if (iop.defer)
+      iop.pending.push_back(PendingOpening{this, out, path, idx});
+    else
+      check(iop.suite, out, path, idx);
+    return out;
+  }
+  void check(int suite, const uint32_t* out, const uint32_t* path, size_t idx) const {
+    Digest cur = hash_elems(suite, out, cols);
     idx += rows;
     while (idx >= 2 * top_size) {
       const bool low = idx & 1;
-      Digest other = digest_of(iop.read(8));
+      Digest other = digest_of(path);
+      path += 8;
       idx >>= 1;
-      cur = low ? hash_pair(iop.suite, other, cur) : hash_pair(iop.suite, cur, other);
+      cur = low ? hash_pair(suite, other, cur) : hash_pair(suite, cur, other);
     }
     const Digest& present = idx >= top_size ? top[idx - top_size] : rest[idx];
     if (!same(present, cur)) throw VerifyError("merkle path mismatch");
-    return out;
   }
 };
 
+// the deferred openings' hash paths on up to `threads` host threads; the first failure (in
+// opening order) is thrown
+inline void check_pending(ReadIOP& iop, unsigned threads) {
+  const size_t n = iop.pending.size();
+  if (n == 0) return;
+  threads = unsigned(std::max<size_t>(1, std::min<size_t>(threads, n)));
+  std::vector<std::string> err(threads);
+  std::vector<size_t> err_at(threads, SIZE_MAX);
+  auto work = [&](unsigned t) {
+    for (size_t i = t; i < n; i += threads) {
+      const PendingOpening& p = iop.pending[i];
+      try {
+        p.tree->check(iop.suite, p.row, p.path, p.idx);
+      } catch (const std::exception& e) {
+        err[t] = e.what();
+        err_at[t] = i;
+        return;
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (unsigned t = 1; t < threads; t++) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+  size_t first = SIZE_MAX;
+  unsigned which = 0;
+  for (unsigned t = 0; t < threads; t++)
+    if (err_at[t] < first) first = err_at[t], which = t;
+  if (first != SIZE_MAX) throw VerifyError(err[which]);
+}
+
 FpExt load_ext(const uint32_t* w) { return FpExt{{w[0], w[1], w[2], w[3]}}; }
+
+// host threads for the deferred Merkle openings: R0HIP_VERIFY_THREADS, else up to 8 of the cores
+inline unsigned verify_threads() {
+  static const unsigned n = [] {
+    const char* e = std::getenv("R0HIP_VERIFY_THREADS");
+    if (e) return unsigned(std::max(1L, std::strtol(e, nullptr, 10)));
+    return std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  }();
+  return n;
+}
 
 // The tap-set view (taps.rs) the verifier needs: taps as {offset, back, group, combo, skip}
 struct TapView {
@@ -203,6 +270,7 @@ void fri_verify(ReadIOP& iop, size_t degree, Inner inner) {
     FpExt x = fe_from_fp(fp_pow(gen, pos));
     if (!fe_eq(poly_eval(final_poly.data(), degree, x), goal)) throw VerifyError("FRI final polynomial mismatch");
   }
+  check_pending(iop, verify_threads());  // while the rounds' verifiers are alive
 }
 
 // verify_validity (mod.rs:292-474) then fri_verify and verify_complete (read_iop.rs:66-71),

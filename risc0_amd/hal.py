@@ -584,7 +584,9 @@ class TraceJob:
             else np.ascontiguousarray(a, dtype=np.uint32)
         self.glob, self.index, self.offsets, self.values = u(glob), u(inj_index), u(inj_offsets), u(inj_values)
         self.cycles, self.txns = np.ascontiguousarray(cycles), np.ascontiguousarray(txns)
+        self.table_split = table_split
         self.bigint = None if bigint is None or not len(bigint) else np.ascontiguousarray(bigint, dtype=np.uint8)
+        self.records = bigint_records
         self.backs = bigint_backs(bigint_records)
         pf = RawPreflightTrace(self.cycles.ctypes.data, self.txns.ctypes.data if self.txns.nbytes else None,
                                None if self.bigint is None else self.bigint.ctypes.data, self.txns.nbytes // 20,

@@ -458,7 +458,7 @@ class Trace:
     def __init__(self, po2, program, *, base_pc=0x10000, data=None, regs=None, seed=1, max_user_cycles=None,
                  read_nodes=True, discover_cycles=None, kernel=None, kernel_pc=KERNEL_START, machine_regs=None,
                  read_record=(), write_record=(), bigint_nondet=None, boot_kernel=False, zero_digests=False,
-                 fast_loop=None):
+                 fast_loop=None, image=None, tree=None, discover_only=False):
         """program: user code at base_pc. kernel: machine-mode code at kernel_pc, entered by a
         user `ecall` through ECALL_DISPATCH_ADDR (r0vm.rs:342-352); it leaves with `mret` or
         a machine ecall (terminate, host read/write, Poseidon2). read_record / write_record:
@@ -471,43 +471,55 @@ class Trace:
         digests start zero (a first segment) instead of seeded words. fast_loop: (head_pc,
         iterations_left(trace)) — a user loop whose iterations produce the same rows and
         transactions up to an affine change per iteration; once three iterations agree, the
-        rest (bar the last two) are emitted as numpy blocks (_bulk_loop) instead of stepped."""
+        rest (bar the last two) are emitted as numpy blocks (_bulk_loop) instead of stepped.
+        Continuations (LoopSession): image — the whole memory image the segment resumes from (the
+        previous segment's final memory, suspend pc and mode included), in place of program /
+        kernel / data / regs; tree — the session's Merkle node digests (node -> 8 words), which give
+        the off-path digests and are advanced to the segment's post-state, so a segment's root is
+        the previous segment's post root; discover_only — run the executor's pass alone (final
+        memory, page sets, tree), no preflight rows."""
         self.po2 = po2
         self.bigint_nondet = bigint_nondet
         self.fast_loop = fast_loop
         self.rng = np.random.default_rng(seed)
         # image: code, data, registers, suspend state, input/output digests
         mem = {}
-        for i, w in enumerate(program):
-            mem[base_pc // 4 + i] = w
-        for i, w in enumerate(kernel or ()):
-            mem[kernel_pc // 4 + i] = w
-        if kernel and not boot_kernel:
-            mem[ECALL_DISPATCH_WADDR] = kernel_pc
-        for a, w in (data or {}).items():
-            mem[a // 4] = w
-        regs = regs or {}
-        for r in range(REG_MAX):
-            mem[USER_REGS_WADDR + r] = regs.get(r, 0) if r else 0
-        for r, v in (machine_regs or {}).items():
-            mem[MACHINE_REGS_WADDR + r] = v
+        if image is None:
+            for i, w in enumerate(program):
+                mem[base_pc // 4 + i] = w
+            for i, w in enumerate(kernel or ()):
+                mem[kernel_pc // 4 + i] = w
+            if kernel and not boot_kernel:
+                mem[ECALL_DISPATCH_WADDR] = kernel_pc
+            for a, w in (data or {}).items():
+                mem[a // 4] = w
+            regs = regs or {}
+            for r in range(REG_MAX):
+                mem[USER_REGS_WADDR + r] = regs.get(r, 0) if r else 0
+            for r, v in (machine_regs or {}).items():
+                mem[MACHINE_REGS_WADDR + r] = v
+            if boot_kernel:
+                mem[USER_START_WADDR] = base_pc
+                mem[SUSPEND_PC_WADDR] = kernel_pc
+                mem[SUSPEND_MODE_WADDR] = 1
+            else:
+                mem[SUSPEND_PC_WADDR] = base_pc
+                mem[SUSPEND_MODE_WADDR] = 0
+        else:
+            mem = dict(image)  # the previous segment's final memory: it resumes where that one suspended
         self.read_record = [list(x) for x in read_record]
         self.write_record = list(write_record)
-        if boot_kernel:
-            mem[USER_START_WADDR] = base_pc
-            mem[SUSPEND_PC_WADDR] = kernel_pc
-            mem[SUSPEND_MODE_WADDR] = 1
-        else:
-            mem[SUSPEND_PC_WADDR] = base_pc
-            mem[SUSPEND_MODE_WADDR] = 0
         self.input_words = [int(x) for x in self.rng.integers(0, 1 << 32, 8, dtype=np.uint64)]
         for i in range(8):
-            mem[GLOBAL_OUTPUT_WADDR + i] = int(self.rng.integers(0, 1 << 32))
+            w = int(self.rng.integers(0, 1 << 32))
+            if image is None:
+                mem[GLOBAL_OUTPUT_WADDR + i] = w
         self.nonce = [int(x) for x in self.rng.integers(0, 1 << 32, 8, dtype=np.uint64)]
         if zero_digests:
             self.input_words, self.nonce = [0] * 8, [0] * 8
             for i in range(8):
-                del mem[GLOBAL_OUTPUT_WADDR + i]
+                if image is None:
+                    del mem[GLOBAL_OUTPUT_WADDR + i]
         self.rand_z = [int(x) for x in self.rng.integers(0, P, 4)]
         self.program_end = base_pc + 4 * len(program)
         # pass 1 (the executor's run that fixes the segment's partial image): the pages the
@@ -525,13 +537,18 @@ class Trace:
         anc = lambda pages: sorted({n for p in pages for n in ancestors(MEMORY_PAGES + p)})
         page_memory = {}
         digest = {}
+        continuing = bool(tree)  # a continuation: the session's tree holds the last post-state
         for p in touched:
             digest[MEMORY_PAGES + p] = page_digest([mem.get(p * 256 + i, 0) for i in range(256)])
         nodes_in = anc(touched)
         for n in sorted(nodes_in, reverse=True):
             for c in (2 * n, 2 * n + 1):
                 if c not in digest:
-                    digest[c] = [int(x) for x in self.rng.integers(0, P, 8)]
+                    if tree is None:
+                        digest[c] = [int(x) for x in self.rng.integers(0, P, 8)]
+                    else:  # the session's digest of that node (first seen: an arbitrary one, kept)
+                        digest[c] = tree.setdefault(c, [int(x) for x in
+                                                        np.random.default_rng([0x7EE, c]).integers(0, P, 8)])
             digest[n] = node_hash(digest[2 * n + 1], digest[2 * n])
         for n, d in digest.items():
             for i, w in enumerate(d):
@@ -542,10 +559,27 @@ class Trace:
         self.write_pages = dirty
         self.write_nodes = anc(dirty)
         assert self.write_nodes, "a segment pages out at least the registers' page"
+        if tree is not None:
+            if continuing:  # a continuation loads the root the session's last segment stored
+                assert self.root == tree[1], "the segment's pre-state root is not the session's"
+            # the post-state: dirty pages from the final memory, their ancestors re-hashed
+            post = dict(digest)
+            for p_ in dirty:
+                post[MEMORY_PAGES + p_] = page_digest([self.mem.get(p_ * 256 + i, 0) for i in range(256)])
+            for n in reversed(self.write_nodes):
+                post[n] = node_hash(post[2 * n + 1], post[2 * n])
+            self.post_root = post[1]
+            tree.update(post)
+        self.final_mem = self.mem
+        if discover_only:
+            return
         # pass 2: the preflight proper
         self.reset(mem, page_memory)
         self.discover = False
         self.build()
+        if tree is not None:
+            assert [self.page_memory[digest_waddr(1) + i] for i in range(8)] == self.post_root, \
+                "the segment's stored root differs from the session's post-state"
 
     def reset(self, mem, page_memory):
         # rows and transactions: Python lists while stepping; numpy blocks (_flush, bulk loop
@@ -1855,3 +1889,100 @@ def loop_s_trace(po2, iterations=None, seed=1, fast=True):
     return Trace(po2, code, base_pc=LOOP_S_TEXT, data=data, seed=seed, kernel=kernel, boot_kernel=True,
                  zero_digests=True, read_record=[n.to_bytes(4, "little"), (4).to_bytes(4, "little") + bytes(4)],
                  fast_loop=(head, left) if fast else None)
+
+
+def paging_rows(tr):
+    """the rows of a segment besides its body's user cycles: load root and nonce, read the
+    nodes and pages, resume and suspend, write the pages and nodes, store the root
+    (Trace.build; Poseidon2 costs 13 rows per node, 322 per page)"""
+    return 11 + 13 * (len(tr.read_nodes) + len(tr.write_nodes)) + 322 * (len(tr.read_pages) + len(tr.write_pages))
+
+
+class LoopSession:
+    """configs[3]'s input (BASELINE.json: big-loop guest, many po2=20 segments): ONE run of the
+    datasheet's loop guest (loop.s under the v1compat kernel, `iterations` loop iterations) cut
+    into consecutive segments of 2^po2 rows where the executor cuts it (execute/executor.rs:
+    213-301): a segment suspends once its user cycles would leave no room for its paging and the
+    reserved table cycles, and the next segment resumes from its final memory image (suspend pc
+    and mode, user registers, the loop counter) with its pages loaded from the session's Merkle
+    tree, whose root it continues from. Test infrastructure, like the rest of this module.
+
+    segment(k) builds segment k's Trace; segments before it are fast-forwarded with the
+    executor's pass alone (no preflight rows), so a rank can build only its own segments."""
+
+    MARGIN = 16  # rows left free below the limit (an instruction that ends a segment can take several)
+
+    def __init__(self, po2, iterations, seed=1):
+        self.po2, self.iterations, self.seed = po2, iterations, seed
+        self.code, self.data, self.head, _count = loop_s_program()
+        self.kernel = v1compat_kernel()
+        self.tree = {}
+        self.image = None  # the next segment's starting memory (None: the boot)
+        self.next_k = 0
+        self.terminated = False
+        self.roots = []  # (pre, post) root per segment passed
+
+    def _kwargs(self, k, build):
+        n = self.iterations
+        left = lambda tr: n - tr.mem.get(USER_REGS_WADDR + REG_A4, 0)
+        kw = dict(base_pc=LOOP_S_TEXT, seed=self.seed * 100003 + k, zero_digests=True, tree=self.tree,
+                  fast_loop=(self.head, left), discover_only=not build)
+        if self.image is None:
+            kw.update(data=self.data, kernel=self.kernel, boot_kernel=True,
+                      read_record=[n.to_bytes(4, "little"), (4).to_bytes(4, "little") + bytes(4)])
+        else:
+            kw.update(image=self.image)
+        return kw
+
+    def _advance(self, build):
+        assert not self.terminated, "the session has ended"
+        k = self.next_k
+        limit = 1 << self.po2
+        # the executor's split: the page sets of the longest segment that could run (a scratch
+        # tree: this pass must not advance the session), then the user cycles that leave room
+        probe = Trace(self.po2, self.code, max_user_cycles=limit, **{**self._kwargs(k, False), "tree": dict(self.tree)})
+        users = limit - RESERVED_CYCLES - paging_rows(probe) - self.MARGIN
+        tr = Trace(self.po2, self.code, max_user_cycles=users, **self._kwargs(k, build))
+        if build:
+            assert tr.table_split_cycle + RESERVED_CYCLES <= limit
+        self.roots.append((tr.root, tr.post_root))
+        self.image = tr.final_mem
+        self.terminated = bool(tr.terminated)
+        self.next_k = k + 1
+        return tr
+
+    def state(self):
+        """where the session stands (the next segment, its starting image and the tree): what a
+        worker needs to build that segment (build_session_segment)"""
+        return (self.next_k, self.image, {n: list(d) for n, d in self.tree.items()}, self.terminated)
+
+    def segment(self, k):
+        """segment k's Trace (k at or after the next unbuilt segment)"""
+        assert k >= self.next_k, "segments are built in order"
+        while self.next_k < k:
+            self._advance(build=False)
+        return self._advance(build=True)
+
+    def __iter__(self):
+        while not self.terminated:
+            yield self._advance(build=True)
+
+
+def loop_s_session_iterations(po2, segments):
+    """loop iterations that fill `segments` segments of 2^po2 rows and end in the last one"""
+    per = (1 << po2) // 2 - 4096  # two user cycles per iteration (addi, bltu), less the paging
+    return per * (segments - 1) + per // 2
+
+
+def build_session_segment(po2, iterations, seed, state):
+    """segment state[0] of a LoopSession from its state() (another process may build it): the
+    Trace's preflight as the segment pipeline takes it — (global words, injector index, offsets,
+    values, cycles, txns, table split, bigint bytes, bigint records, terminated)"""
+    S = LoopSession(po2, iterations, seed)
+    S.next_k, S.image, S.tree, S.terminated = state[0], state[1], {n: list(d) for n, d in state[2].items()}, state[3]
+    tr = S._advance(build=True)
+    cyc, tx = tr.arrays()
+    idx, off, val = tr.injector_arrays()
+    return (tr.global_words(), idx, off, val, cyc, tx, tr.table_split_cycle, tr.bigint_array(), tr.bigint_records(),
+            bool(tr.terminated))
+

@@ -416,3 +416,29 @@ def test_injector_words_outside_the_arms_columns_match_reference(hal, oracle):
         r.prove_segment_trace(hal, po2, W.global_words(t), idx3, off3, val3, cyc, tx, t.table_split_cycle)
     seal, _ = r.prove_segment_trace(hal, po2, W.global_words(t), idx, off, val, cyc, tx, t.table_split_cycle)
     assert r.verify_seal("rv32im", hal.suite, seal, check_validity=True) == po2
+
+
+def test_loop_s_session_segments_match_reference_and_verify(hal):
+    """configs[3]'s input: ONE loop.s session cut into consecutive po2=20
+    segments where the executor cuts it (rv32im_trace.LoopSession): each segment after the first
+    resumes mid-loop from the previous one's final memory with its pages loaded, and its pre-state
+    root is the previous post-state root. Segments 0, 1 and the last: the GPU witness equals the
+    compiled reference witgen's word for word, and the three seals (one r0hip_prove_trace_segments
+    call, receipts checked) pass r0hip_verify_seal with the validity equation."""
+    import risc0_amd as r
+    po2, K = 20, 3
+    S = T.LoopSession(po2, T.loop_s_session_iterations(po2, K), seed=11)
+    traces = list(S)
+    assert len(traces) == K and traces[-1].terminated and not traces[0].terminated
+    for a, b in zip(traces, traces[1:]):
+        assert b.root == a.post_root
+    for t in traces:
+        data, glob, cyc, tx = W.inputs(t)
+        ref_d, ref_g = W.run(data, glob, cyc, tx, t.table_split_cycle, 1 << po2, W.MODE_PARALLEL)
+        d, g = gpu_witgen(hal, data, glob, cyc, tx, t.table_split_cycle)
+        assert np.array_equal(d, ref_d) and np.array_equal(g, ref_g)
+    got = r.prove_trace_segments(hal, po2, [_trace_job(r, t) for t in traces], in_flight=2)
+    assert len({s.tobytes() for s, _ in got}) == K
+    for seal, _ in got:
+        assert r.verify_seal("rv32im", hal.suite, seal, check_validity=True) == po2
+
