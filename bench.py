@@ -839,6 +839,14 @@ def pmc_traffic(family, calls, args):
     return int((d["read_bytes"] + d["write_bytes"]) / calls), os.path.relpath(path, ROOT)
 
 
+# how oracle/Makefile builds the CPU baseline's code: the reference's own C++ (poly_fp, the
+# rv32im and recursion witness generation and accumulation) at the level its cargo build gives
+# it, the oracle's restated CpuHal/Prover at -O3; both for the build host's x86-64 baseline ISA
+REF_BUILD = ("oracle/_ref: g++ -O3 -ffunction-sections -fdata-sections -fno-var-tracking -g0 -std=c++17 (cc::Build "
+             "under cargo's release profile: risc0/build_kernel/src/lib.rs:141-151, Cargo.toml:86-87); "
+             "liboracle.so: g++ -O3 -std=c++17; every core the process may use (`cores`)")
+
+
 def host_cores():
     """CPUs this process may use on the box: the affinity mask, capped by the cgroup CPU
     quota (cgroup v2 cpu.max or v1 cfs_quota/period) when one is set."""
@@ -920,7 +928,7 @@ def cpu_baseline_trace(args, trace, gpu_seal, gpu_mix):
                 "sample": f"one rv32im segment at po2={trace.po2} ({args.hashfn}) from the bench's own preflight trace, "
                           f"{t:.1f} s wall: the reference's compiled witgen and accumulation (oracle/_ref) and the "
                           "oracle prover with the reference's compiled poly_fp",
-                "seconds_by_hal_op": ops,
+                "seconds_by_hal_op": ops, "build": REF_BUILD,
                 "seal_equal": bool(np.array_equal(cseal, gpu_seal)) if compare else None,
                 "mix_equal": bool(np.array_equal(cmix, gpu_mix)) if compare else None,
                 "oracle_seal_sha256": dig(cseal), "gpu_seal_sha256": dig(gpu_seal),
@@ -981,7 +989,7 @@ def cpu_baseline_program(args, p, gpu_seal, gpu_mix):
         return {"value": round(n / t, 1), "unit": "cycles/s", "cores": int(oracle.num_threads()), "kind": "port",
                 "sample": f"one recursion segment at po2={po2} ({args.hashfn}) from rank 0's program 0, {t:.1f} s wall: "
                           "the reference's compiled recursion witgen and accumulation (oracle/_ref) and the oracle prover",
-                "seconds_by_hal_op": ops,
+                "seconds_by_hal_op": ops, "build": REF_BUILD,
                 "seal_equal": bool(np.array_equal(cseal, gpu_seal)), "mix_equal": bool(np.array_equal(cmix, gpu_mix)),
                 "oracle_seal_sha256": dig(cseal), "gpu_seal_sha256": dig(gpu_seal),
                 "parity_note": "CPU recursion prove of rank 0's program 0 against the GPU seal of the same program"}

@@ -106,10 +106,10 @@ const char* r0hip_memset32(void* d_dst, uint32_t value, size_t count) {
   return wrap([&] { HIP_OK(hipMemsetD32Async(d_dst, int(value), count, stream())); });
 }
 const char* r0hip_memcpy_h2d(void* d_dst, const void* h_src, size_t bytes) {
-  return wrap([&] { HIP_OK(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, stream())); });
+  return wrap([&] { upload(d_dst, h_src, bytes); });
 }
 const char* r0hip_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes) {
-  return wrap([&] { HIP_OK(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, stream())); });
+  return wrap([&] { download(h_dst, d_src, bytes); });
 }
 const char* r0hip_memcpy_d2d(void* d_dst, const void* d_src, size_t bytes) {
   return wrap([&] { HIP_OK(hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, stream())); });

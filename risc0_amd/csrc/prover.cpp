@@ -45,11 +45,7 @@ size_t log2_exact(size_t v) {
 }
 
 // host copies through a stream-ordered D2H followed by a sync
-void d2h(void* h, const void* d, size_t bytes) {
-  hipStream_t s = stream();
-  HIP_OK(hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, s));
-  HIP_OK(hipStreamSynchronize(s));
-}
+void d2h(void* h, const void* d, size_t bytes) { download(h, d, bytes); }
 template <typename T>
 uint32_t* upload(const std::vector<T>& v, int slot) {
   size_t bytes = v.size() * sizeof(T);

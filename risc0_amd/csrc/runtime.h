@@ -140,6 +140,11 @@ void release_thread_memory() noexcept;
 // drain this thread's stream (or stage_reset) before returning to the caller.
 void upload_async(void* d_dst, const void* h_src, size_t bytes);
 void stage_reset();
+// Device-to-host copy in stream order, complete on return (this thread's stream is drained):
+// small copies into pageable memory bounce through the page-locked arena.
+void download(void* h_dst, const void* d_src, size_t bytes);
+// The same host-to-device (small pageable sources bounce through the arena), complete on return.
+void upload(void* d_dst, const void* h_src, size_t bytes);
 
 // Optional kernel-level timing (HIP events on the library stream around each
 // launcher), with the launcher's algorithmic HBM bytes and modmul-equivalent count

@@ -44,3 +44,18 @@ def test_rust_hal_implements_every_hal_method():
                "hash_fold", "gather_sample", "scatter", "prefix_products", "combos_prepare", "combos_divide"]
     for m in methods:
         assert re.search(r"fn " + m + r"\b", rs), m
+
+
+def test_rust_recursion_circuit_hal_binds_the_recursion_entry_points():
+    """recursion_circuit_hal_hip.rs (circuit/recursion/src/prove/hal/hip.rs, beside the
+    reference's cuda.rs) implements the recursion circuit's three HAL traits over the C ABI"""
+    rs = open(os.path.join(ROOT, "integration", "rust", "recursion_circuit_hal_hip.rs")).read()
+    for trait in ("CircuitWitnessGenerator", "CircuitAccumulator", "CircuitHal"):
+        assert re.search(r"impl<HS: HipHash> " + trait + r"<HipHal<HS>> for HipRecursionCircuitHal<HS>", rs), trait
+    for sym in ("r0hip_recursion_witgen", "r0hip_recursion_accum", "r0hip_eval_check"):
+        assert re.search(sym + r"\(", rs), sym
+    for suite in ("HipHashPoseidon2", "HipHashPoseidon254", "HipHashSha256"):
+        assert suite in rs
+    # the rv32im circuit HAL no longer carries it as comments
+    rv = open(os.path.join(ROOT, "integration", "rust", "circuit_hal_hip.rs")).read()
+    assert "HipRecursionCircuitHal" not in rv.replace("recursion_circuit_hal_hip.rs", "")
