@@ -3,11 +3,12 @@
 
 A step proves one rv32im segment of 2^po2 cycles on one GPU the way the reference's
 prove_core does (circuit/rv32im/src/prove/hal/mod.rs:143-224), from the segment's
-preflight trace: the trace (the datasheet's loop guest, restated preflight) starts in
-page-locked host memory, and the native segment pipeline (r0hip_prove_segments trace jobs)
-uploads it, generates the witness, accumulates and proves to the seal (Vec<u32>) on the
-host, with in_flight segments on the GPU and the next trace uploading, as r0vm's GPU worker
-queue runs segments. --witness times the prove core alone on a resident synthetic witness.
+preflight trace: the trace (a segment of one run of the datasheet's loop guest, restated
+preflight, cut into consecutive segments where the executor cuts them) starts in page-locked
+host memory, and the native segment pipeline (r0hip_prove_trace_segments) uploads it,
+generates the witness, accumulates, proves to the seal (Vec<u32>) and checks the receipt on
+the host, with in_flight segments on the GPU and the next trace uploading, as r0vm's GPU
+worker queue runs segments. --witness times the prove core alone on a resident synthetic witness.
 Multi-GPU: one process per GPU, whole segments sharded per rank, no data-path
 collective (gloo only for the barriers, the max-time reduce and the host-side gather of
 seal digests). The ranks come from torch.distributed.run, or — when `--gpus N` is given
@@ -54,7 +55,10 @@ def parse():
     ap.add_argument("--session", type=int, default=None,
                     help="trace mode, configs[3]: ONE loop.s session cut into this many consecutive segments "
                          "(tests/rv32im_trace.LoopSession); segment i goes to rank i mod N, every segment is proved "
-                         "once in the timed region (steps = the rank's segments)")
+                         "once in the timed region (steps = the rank's segments). Default for the loop guest up to "
+                         "po2=22: N x --steps segments")
+    ap.add_argument("--no-session", action="store_true",
+                    help="trace mode: cycle --traces distinct single-segment traces per rank instead (the round-5 form)")
     ap.add_argument("--traces", type=int, default=None,
                     help="trace mode: distinct preflight traces per rank, cycled over the timed segments "
                          "(default 4 up to po2=22, 1 above)")
@@ -162,6 +166,10 @@ def main():
     # groups are only read and are shared
     globs = [dg] + [hal.copy_from_elem("global", glob) for _ in range(k - 1)]
     trace_mode = args.circuit == "rv32im" and not args.witness
+    if trace_mode and args.guest == "loop_s" and not args.no_session and args.session is None and args.po2 <= 22:
+        # the default workload: N x steps consecutive segments of one loop.s run, segment i on
+        # rank i mod N (configs[1] per segment, configs[3] across the ranks)
+        args.session = world * args.steps
     # recursion: a whole proof from the program and its preflight (RecursionProverImpl::prove,
     # circuit/recursion/src/prove/mod.rs:160-230: witness generation, ZK noise, accumulation,
     # prove), the lift/join shape with random programs (the lift/join .zkr files are not in the
@@ -358,7 +366,8 @@ def main():
     if rank == 0:
         workload = (f"{args.circuit} segment po2={args.po2}, {args.hashfn} hashfn, from its preflight trace in page-locked "
                     "host memory: upload -> witness generation -> accumulation -> seal on host (the reference's "
-                    "prove_core), through the native segment pipeline (r0hip_prove_segments trace jobs)"
+                    "prove_core), through the native segment pipeline (r0hip_prove_trace_segments), each receipt "
+                    "checked by the native verifier before it is returned"
                     if trace_mode else
                     f"recursion segment po2={args.po2}, {args.hashfn} hashfn, from the program (control group resident) "
                     "and its preflight in host memory: witness generation -> ZK noise -> accumulation -> seal on host "
