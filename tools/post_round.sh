@@ -14,8 +14,10 @@ python3 tools/rocprof_families.py "$(f stats '*kernel_stats.csv')" $NS > profile
 cp "$(f stats '*kernel_stats.csv')" profiles/${R}_rocprof_kernel_stats.csv
 python3 tools/pmc_summary.py "$(f valu '*counter_collection.csv')" profiles/${R}_pmc_valu.json > profiles/${R}_pmc_valu.txt
 python3 tools/pmc_traffic.py "$(f fetch '*counter_collection.csv')" "$(f write '*counter_collection.csv')" $NP > profiles/${R}_pmc_traffic.json
+# eval_check's instruction mix on this tree's objects (bench.py's roofline.eval_check_issue)
+python3 tools/ec_inst_mix.py rv32im profiles/${R}_pmc_valu.json > profiles/${R}_ec_inst_mix.json
 # the library the counters were taken on (bench.py compares it with the one it loads)
-[ -f $O/lib_sha256_16 ] && python3 tools/pmc_stamp.py $(cat $O/lib_sha256_16) profiles/${R}_pmc_valu.json profiles/${R}_pmc_traffic.json
+[ -f $O/lib_sha256_16 ] && python3 tools/pmc_stamp.py $(cat $O/lib_sha256_16) profiles/${R}_pmc_valu.json profiles/${R}_pmc_traffic.json profiles/${R}_ec_inst_mix.json
 cp $O/bench.json profiles/${R}_bench.json
 cp $O/pytest_gpu.log profiles/${R}_pytest_gpu.log
 head -30 profiles/${R}_rocprof_families.txt
