@@ -36,8 +36,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     # a multiple of the segments in flight; enough segments that the pipeline's fill and drain
-    # (the first trace's upload, the last segments finishing alone) are a small share
-    ap.add_argument("--steps", type=int, default=12)
+    # (the first trace's upload, the last segments finishing alone: ~20 ms per run) are a small
+    # share — 3% of 12 segments, 1.5% of 24
+    ap.add_argument("--steps", type=int, default=24)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--po2", type=int, default=20)
     ap.add_argument("--circuit", default="rv32im")
@@ -283,11 +284,12 @@ def main():
             # every seal checked by the native verifier beside the proofs (the worker unit returns
             # only receipts that verified, prover_impl.rs:262-280); a failed check fails the bench
             res = r.prove_trace_segments(hal, args.po2, jobs_, in_flight=k, per_job=True, verify=not args.no_verify)
-            bad = [e for _, _, e, _ in res if e]
+            bad = [e for _, _, e, _, _ in res if e]
             if bad:
                 raise RuntimeError(f"{len(bad)} of {len(res)} segments failed: {bad[0]}")
-            out["res"] = [(sl, m) for sl, m, _, _ in res]
-            out["verify_ms"] = [v for _, _, _, v in res]
+            out["res"] = [(sl, m) for sl, m, _, _, _ in res]
+            out["verify_ms"] = [v for _, _, _, v, _ in res]
+            out["prove_ms"] = [pm for _, _, _, _, pm in res]
         pipeline([tjobs[i % len(tjobs)] for i in range(max(args.warmup, k + 1))])  # warm every set, thread, pool
         _t, t = timed_segments(pipeline, [batch], 0, hal.synchronize, dist)
         seal, mix = out["res"][0]  # job 0 proved trace 0
@@ -296,6 +298,11 @@ def main():
         t0 = time.perf_counter()
         pipeline([tjobs[0]])
         t_one = time.perf_counter() - t0
+        # the one segment's latency, split: the prover's share (upload wait, witness generation,
+        # accumulation, proof, seal to host), the receipt check after it, the rest (call set-up:
+        # trace sets, threads; the Python wrapper)
+        one_split = {"prove_ms": round(out["prove_ms"][0], 2), "verify_ms": round(out["verify_ms"][0], 2),
+                     "other_ms": round(1000.0 * t_one - out["prove_ms"][0] - out["verify_ms"][0], 2)}
         rsteps = args.steps if args.resident_steps is None else args.resident_steps
         if rsteps > 0:
             t_r, seal_r, _ = timed_leg(lambda slot: r.prove_segment_trace_resident(hal, rt, bigint_records=bigint_records),
@@ -420,7 +427,8 @@ def main():
                            "distinct_seals_rank0": seals_distinct,
                            "h2d_bytes_per_segment": int(tjobs[0].h2d_bytes()),
                            "receipts_verified": not args.no_verify, "verify_ms_per_segment": round(verify_ms, 2),
-                           "ms_one_segment_unpipelined": round(1000.0 * t_one, 1)} if trace_mode else {}),
+                           "ms_one_segment_unpipelined": round(1000.0 * t_one, 1),
+                           "one_segment_split": one_split} if trace_mode else {}),
                        **({"programs_per_rank": len(progs), "seal_valid_rank0": bool(program_valid)}
                           if program_mode else {}),
                        "ranks_share_devices": any(shared[i] for i in range(world))},

@@ -352,6 +352,8 @@ typedef struct r0hip_trace_job {
   const char* error;                  /* out: NULL or a malloc'd message (free() it) */
   int verified;                       /* out: 1 when the seal passed r0hip_verify_seal */
   double verify_ms;                   /* out: host milliseconds of that check */
+  double prove_ms;                    /* out: host milliseconds from a prover taking the job to its
+                                         seal in host memory (the wait for its upload included) */
 } r0hip_trace_job;
 const char* r0hip_prove_trace_segments(int suite, uint32_t po2, r0hip_trace_job* jobs, size_t njobs,
                                        uint32_t in_flight, int verify);

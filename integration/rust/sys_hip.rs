@@ -78,6 +78,7 @@ pub struct R0HipTraceJob {
     pub error: *const c_char,
     pub verified: c_int,
     pub verify_ms: f64,
+    pub prove_ms: f64,
 }
 
 #[link(name = "r0hip")]

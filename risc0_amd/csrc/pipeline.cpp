@@ -296,6 +296,7 @@ const char* prove_trace_jobs(int suite, uint32_t po2, r0hip_trace_job* jobs, siz
       const long job = long(b.job);
       r0hip_trace_job& j = jobs[job];
       const r0hip_trace_input& tr = j.trace;
+      const auto t0 = std::chrono::steady_clock::now();
       try {
         ensure_init();
         r0hip_raw_preflight_trace pf = tr.preflight;  // the set's device copies
@@ -314,6 +315,7 @@ const char* prove_trace_jobs(int suite, uint32_t po2, r0hip_trace_job* jobs, siz
               HIP_OK(hipStreamWaitEvent(st, b.ev, 0));
             });
         HIP_OK(hipStreamSynchronize(stream()));
+        j.prove_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         j.seal_len = seal.size();
         if (j.h_mix_out) memcpy(j.h_mix_out, mix.data(), mix.size() * 4);
         // TESTING ONLY (tests/test_rv32im_witgen_gpu.py): R0HIP_TESTING_CORRUPT_SEAL_JOB=i flips a
@@ -532,6 +534,7 @@ extern "C" const char* r0hip_prove_trace_segments(int suite, uint32_t po2, r0hip
       jobs[i].seal_len = 0;
       jobs[i].verified = 0;
       jobs[i].verify_ms = 0;
+      jobs[i].prove_ms = 0;
     }
     if (njobs) {
       const size_t k = std::max<size_t>(1, std::min<size_t>(in_flight ? in_flight : 2, njobs));

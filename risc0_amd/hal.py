@@ -569,7 +569,7 @@ class TraceJobStruct(C.Structure):
     """struct r0hip_trace_job (include/r0hip.h)"""
     _fields_ = [("trace", TraceInput), ("h_bigint", C.c_void_p), ("n_bigint", C.c_size_t), ("h_seal", C.c_void_p),
                 ("seal_cap", C.c_size_t), ("seal_len", C.c_size_t), ("h_mix_out", C.c_void_p), ("error", C.c_void_p),
-                ("verified", C.c_int), ("verify_ms", C.c_double)]
+                ("verified", C.c_int), ("verify_ms", C.c_double), ("prove_ms", C.c_double)]
 
 
 class TraceJob:
@@ -637,7 +637,8 @@ def prove_trace_segments(hal, po2, traces, in_flight=2, seal_cap=1 << 22, verify
     while in_flight provers run, and (verify) every seal is checked by the native verifier, the
     validity equation included, on a host thread beside the proofs. Returns [(seal, mix)] in job
     order and raises on any failed job; per_job=True returns [(seal, mix, error or None,
-    verify_ms)] instead, without raising for a job's own failure."""
+    verify_ms, prove_ms)] instead, without raising for a job's own failure (prove_ms: from a
+    prover taking the job to its seal in host memory)."""
     jobs = (TraceJobStruct * len(traces))()
     seals, mixes, keep = [], [], []
     for j, t in zip(jobs, traces):
@@ -660,7 +661,7 @@ def prove_trace_segments(hal, po2, traces, in_flight=2, seal_cap=1 << 22, verify
             check(err)  # a failure of the call itself, not of a job
         elif err:
             libc_free(err)
-        return [(seal[: j.seal_len].copy(), mix, e, j.verify_ms) for j, seal, mix, e in zip(jobs, seals, mixes, errors)]
+        return [(seal[: j.seal_len].copy(), mix, e, j.verify_ms, j.prove_ms) for j, seal, mix, e in zip(jobs, seals, mixes, errors)]
     check(err)
     if verify:
         assert all(j.verified for j in jobs)

@@ -277,11 +277,11 @@ def test_prove_trace_segments_verification_fails_the_job(hal, monkeypatch):
     traces = [T.loop_s_trace(14, 150 + 31 * i, seed=70 + i) for i in range(4)]
     jobs = [_trace_job(r, t) for t in traces]
     clean = r.prove_trace_segments(hal, 14, jobs, in_flight=2, per_job=True)
-    assert all(e is None and ms > 0 for _, _, e, ms in clean)
+    assert all(e is None and ms > 0 and pms > 0 for _, _, e, ms, pms in clean)
     monkeypatch.setenv("R0HIP_TESTING_CORRUPT_SEAL_JOB", "2")
     got = r.prove_trace_segments(hal, 14, jobs, in_flight=2, per_job=True)
     monkeypatch.delenv("R0HIP_TESTING_CORRUPT_SEAL_JOB")
-    for i, ((seal, mix, err, _), (cseal, cmix, _, _)) in enumerate(zip(got, clean)):
+    for i, ((seal, mix, err, _, _), (cseal, cmix, _, _, _)) in enumerate(zip(got, clean)):
         if i == 2:
             assert err and "receipt verification failed" in err, err
             assert not np.array_equal(seal, cseal)

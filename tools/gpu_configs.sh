@@ -9,7 +9,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/$TAG; mkdir -p $O
 run() {  # name, timeout, bench args...
   local n=$1 t=$2; shift 2
-  timeout -k 10 $t python3 -u bench.py --e2e-steps 0 --accum-steps 0 "$@" > $O/$n.json 2> $O/$n.err || { tail -20 $O/$n.err; exit 1; }
+  timeout -k 10 $t python3 -u bench.py --e2e-steps 0 --accum-steps 0 --per-op-steps 0 "$@" > $O/$n.json 2> $O/$n.err || { tail -20 $O/$n.err; exit 1; }
   python3 -c "import json; d=json.load(open('$O/$n.json')); c=d.get('cpu_baseline') or {}; print('$n', d['value'], d['ms_per_step'], 'seal_equal', c.get('seal_equal'))"
 }
 run po2_24 600 --po2 24 --steps 2 --warmup 1 --no-cpu-baseline --resident-steps 0
