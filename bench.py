@@ -513,8 +513,9 @@ def per_op_leg(hal, args, job, pipeline_seal, pipeline_mix):
     """The drop-in path's own number: trace 0 proved by the reference prover over ONLY the per-op
     r0hip_* symbols (integration/hal_prover.cpp: the injector scatter, r0hip_rv32im_witgen, the
     Prover's make_coeffs / commit_group / finalize / fri_prove and the accumulation, one
-    synchronous call per Hal method, Merkle openings one device-to-host copy per node as with
-    has_unified_memory() = false), what a Rust HipHal behind risc0_zkp::hal::Hal delivers; one
+    synchronous call per Hal method, has_unified_memory() = false, the node reads of Merkle openings
+    from the HAL buffer's host mirror of each node heap), what a Rust HipHal behind
+    risc0_zkp::hal::Hal delivers; one
     segment at a time, from the trace in host memory. Its seal must equal the pipeline's."""
     sys.path.insert(0, os.path.join(ROOT, "integration"))
     import halprover

@@ -48,20 +48,46 @@ size_t lg(size_t n) {
 struct Buf {
   uint32_t* p = nullptr;
   size_t words = 0;
+  // get_at through a page-locked host mirror of the whole buffer (hal_hip.rs BufferImpl::
+  // get_at on a Merkle node heap): one device-to-host copy at the first read after the buffer
+  // was last written (written()), then host loads. The Prover writes a node heap only while it
+  // builds the tree (hash_rows, hash_fold), so a tree's ~50 x 17 openings cost one bulk copy
+  // (268 MB at po2=20, ~5 ms) instead of one synchronous 13 us copy per node.
+  mutable uint32_t* host = nullptr;
+  mutable bool host_ok = false;
   Buf() = default;
   explicit Buf(size_t n) : words(n) {
     void* d = nullptr;
     ok(r0hip_alloc(&d, (n ? n : 1) * 4));
     p = static_cast<uint32_t*>(d);
   }
-  Buf(Buf&& o) noexcept : p(o.p), words(o.words) { o.p = nullptr; }
+  Buf(Buf&& o) noexcept : p(o.p), words(o.words), host(o.host), host_ok(o.host_ok) {
+    o.p = nullptr;
+    o.host = nullptr;
+  }
   Buf& operator=(Buf&& o) noexcept {
     std::swap(p, o.p);
     std::swap(words, o.words);
+    std::swap(host, o.host);
+    std::swap(host_ok, o.host_ok);
     return *this;
   }
   ~Buf() {
     if (p) free(const_cast<char*>(r0hip_free(p)));  // a drop never fails the proof
+    if (host) free(const_cast<char*>(r0hip_host_free(host)));
+  }
+  void written() { host_ok = false; }
+  const uint32_t* at(size_t off) const {
+    if (!host_ok) {
+      if (!host) {
+        void* h = nullptr;
+        ok(r0hip_host_alloc(&h, words * 4));
+        host = static_cast<uint32_t*>(h);
+      }
+      ok(r0hip_memcpy_d2h(host, p, words * 4));
+      host_ok = true;
+    }
+    return host + off;
   }
   static Buf from(const uint32_t* h, size_t n) {
     Buf b(n);
@@ -106,12 +132,11 @@ struct Merkle {
     top_size = size_t(1) << top_layer;
     ok(r0hip_hash_rows(suite, nodes.p + rows * 8, matrix->p, rows, cols));
     for (size_t i = layers; i-- > 0;) ok(r0hip_hash_fold(suite, nodes.p, (size_t(1) << i) * 2, size_t(1) << i));
-    auto h = nodes.to_host(8, 8);  // get_at(1)
-    memcpy(root.w, h.data(), 32);
+    nodes.written();
+    memcpy(root.w, nodes.at(8), 32);  // get_at(1)
   }
   void commit(WriteIOP& iop) const {
-    auto top = nodes.to_host(top_size * 8, top_size * 8);
-    iop.write(top.data(), top.size());
+    iop.write(nodes.at(top_size * 8), top_size * 8);  // the top layer's get_at reads
     iop.commit(root);
   }
   // prove/merkle.rs:108-140: gather_sample, then one get_at per node up the tree
@@ -124,8 +149,7 @@ struct Merkle {
     while (idx >= 2 * top_size) {
       const size_t low = idx % 2;
       idx /= 2;
-      auto other = nodes.to_host((2 * idx + (1 - low)) * 8, 8);
-      iop.write(other.data(), 8);
+      iop.write(nodes.at((2 * idx + (1 - low)) * 8), 8);
     }
   }
 };

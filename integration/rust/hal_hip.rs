@@ -11,7 +11,9 @@
 //   * every call is synchronous on return (include/r0hip.h), exactly what the Prover
 //     assumes of `view`/`get_at` after a kernel;
 //   * `has_unified_memory()` is false: Merkle openings go through `gather_sample`
-//     (prove/merkle.rs:111-129);
+//     (prove/merkle.rs:111-129); `get_at` on a Merkle node heap reads a page-locked host
+//     mirror of the heap, filled by one bulk copy at the first read after the tree was built
+//     (a tree's ~50 x 17 node reads would otherwise be one synchronous copy each);
 //   * combos_prepare / combos_divide are overridden with the device versions, as cuda.rs:
 //     986-1048 does (one batched call for every chunk instead of one per divisor).
 //
@@ -19,7 +21,7 @@
 // driven over the same C symbols from Python, produces the golden seals:
 // tests/hal_prover.py + tests/test_gpu_parity.py::test_per_op_abi_prover_matches_golden_seal.
 
-use std::{cell::RefCell, ffi::CStr, marker::PhantomData, os::raw::c_void, rc::Rc, sync::OnceLock};
+use std::{cell::{Cell, RefCell}, ffi::CStr, marker::PhantomData, os::raw::c_void, rc::Rc, sync::OnceLock};
 
 use parking_lot::{ReentrantMutex, ReentrantMutexGuard};
 use risc0_core::{
@@ -65,6 +67,13 @@ struct DeviceAlloc {
     name: &'static str,
     ptr: *mut c_void,
     bytes: usize,
+    /// Merkle node heaps (marked by hash_fold): get_at reads `mirror`, a page-locked copy of the
+    /// whole allocation made at the first read after the last write (`mirror_ok`). The only Hal
+    /// methods that write a Buffer<Digest> are hash_rows and hash_fold, plus view_mut; all three
+    /// clear `mirror_ok`.
+    mirrored: Cell<bool>,
+    mirror: Cell<*mut c_void>,
+    mirror_ok: Cell<bool>,
 }
 
 impl DeviceAlloc {
@@ -74,7 +83,22 @@ impl DeviceAlloc {
         ffi_wrap(|| unsafe { r0hip_alloc(&mut ptr, bytes) })
             .unwrap_or_else(|e| panic!("allocation failed on {name}: {bytes} bytes: {e}"));
         tracker().lock().unwrap().alloc(bytes);
-        Self { name, ptr, bytes }
+        Self { name, ptr, bytes, mirrored: Cell::new(false), mirror: Cell::new(std::ptr::null_mut()),
+               mirror_ok: Cell::new(false) }
+    }
+
+    /// the host mirror, refreshed if the device copy was written since
+    fn host(&self) -> *const u8 {
+        if !self.mirror_ok.get() {
+            if self.mirror.get().is_null() {
+                let mut h = std::ptr::null_mut();
+                check(unsafe { r0hip_host_alloc(&mut h, self.bytes) });
+                self.mirror.set(h);
+            }
+            check(unsafe { r0hip_memcpy_d2h(self.mirror.get(), self.ptr, self.bytes) });
+            self.mirror_ok.set(true);
+        }
+        self.mirror.get() as *const u8
     }
 }
 
@@ -82,6 +106,9 @@ impl Drop for DeviceAlloc {
     fn drop(&mut self) {
         tracker().lock().unwrap().free(self.bytes);
         unsafe { r0hip_free(self.ptr) };
+        if !self.mirror.get().is_null() {
+            unsafe { r0hip_host_free(self.mirror.get()) };
+        }
     }
 }
 
@@ -125,6 +152,16 @@ impl<T> BufferImpl<T> {
         unsafe { (self.dev_void() as *mut u8).add(idx * std::mem::size_of::<T>()) as *mut u32 }
     }
 
+    /// a Hal method wrote this buffer's device memory; `node_heap`: it is a Merkle node heap
+    /// (hash_fold), whose get_at reads go through the host mirror
+    fn written(&self, node_heap: bool) {
+        let a = self.alloc.borrow();
+        a.mirror_ok.set(false);
+        if node_heap {
+            a.mirrored.set(true);
+        }
+    }
+
     fn read(&self, offset: usize, len: usize) -> Vec<T> {
         let mut out = Vec::<T>::with_capacity(len);
         let bytes = len * std::mem::size_of::<T>();
@@ -152,6 +189,12 @@ impl<T: Clone> Buffer<T> for BufferImpl<T> {
 
     fn get_at(&self, idx: usize) -> T {
         assert!(idx < self.size);
+        let a = self.alloc.borrow();
+        if a.mirrored.get() {
+            let at = (self.offset + idx) * std::mem::size_of::<T>();
+            return unsafe { std::ptr::read_unaligned(a.host().add(at) as *const T) };
+        }
+        drop(a);
         self.read(idx, 1).pop().unwrap()
     }
 
@@ -164,6 +207,7 @@ impl<T: Clone> Buffer<T> for BufferImpl<T> {
         scope!("view_mut");
         let mut host = self.read(0, self.size);
         f(&mut host);
+        self.written(false);
         let bytes = std::mem::size_of_val(host.as_slice());
         if bytes > 0 {
             check(unsafe { r0hip_memcpy_h2d(self.dev_void(), host.as_ptr() as *const c_void, bytes) });
@@ -440,11 +484,13 @@ impl<HS: HipHash> Hal for HipHal<HS> {
         let rows = output.size();
         assert_eq!(matrix.size() % rows, 0);
         check(unsafe { r0hip_hash_rows(HS::SUITE, output.dev(), matrix.dev(), rows, matrix.size() / rows) });
+        output.written(false);
     }
 
     fn hash_fold(&self, io: &Self::Buffer<Digest>, input_size: usize, output_size: usize) {
         assert_eq!(input_size, 2 * output_size);
         check(unsafe { r0hip_hash_fold(HS::SUITE, io.dev(), input_size, output_size) });
+        io.written(true);
     }
 
     fn gather_sample(

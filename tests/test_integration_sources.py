@@ -59,3 +59,26 @@ def test_rust_recursion_circuit_hal_binds_the_recursion_entry_points():
     # the rv32im circuit HAL no longer carries it as comments
     rv = open(os.path.join(ROOT, "integration", "rust", "circuit_hal_hip.rs")).read()
     assert "HipRecursionCircuitHal" not in rv.replace("recursion_circuit_hal_hip.rs", "")
+
+
+def test_rust_hal_node_heap_mirror_is_invalidated_by_every_digest_write():
+    """hal_hip.rs answers get_at on a Merkle node heap from a host mirror (one bulk copy per
+    tree instead of one synchronous copy per node). The Hal methods that write a Buffer<Digest>
+    are hash_rows and hash_fold (hal/mod.rs:55-258), plus Buffer::view_mut: each must clear the
+    mirror, and hash_fold marks the allocation as a node heap."""
+    rs = open(os.path.join(ROOT, "integration", "rust", "hal_hip.rs")).read()
+
+    def body(name):
+        m = re.search(r"fn " + name + r"\b[^{]*\{", rs)
+        assert m, name
+        depth, i = 1, m.end()
+        while depth:
+            depth += {"{": 1, "}": -1}.get(rs[i], 0)
+            i += 1
+        return rs[m.end():i]
+    assert "io.written(true)" in body("hash_fold")
+    assert "output.written(false)" in body("hash_rows")
+    assert "self.written(false)" in body("view_mut")
+    # no other Hal method takes a Buffer<Digest>
+    sigs = re.findall(r"fn (\w+)\([^)]*Buffer<Digest>", rs)
+    assert set(sigs) <= {"hash_rows", "hash_fold", "alloc_digest", "copy_from_digest"}, sigs
