@@ -44,6 +44,16 @@ const char* r0hip_host_alloc(void** h_ptr, size_t bytes);
 const char* r0hip_host_free(void* h_ptr);
 const char* r0hip_synchronize(void);
 void r0hip_free_error(const char* err);
+/* A device-to-host copy that runs beside the caller's later calls, for a HAL's host mirrors
+ * (hal_hip.rs: a Merkle node heap, read node by node by MerkleTreeProver::prove, merkle.rs:
+ * 108-140). The copy goes on a process-wide copy stream; d_src is read as the caller's earlier
+ * calls left it (every call is complete on return), and must not be written or freed until the
+ * copy finished. *h_copy = a handle for r0hip_copy_finish, or NULL when the copy is already
+ * done (bytes == 0, or h_dst is not r0hip_host_alloc memory: then it is copied before return).
+ * r0hip_copy_finish: *done = 1 when the bytes are in h_dst (the handle is then released; a
+ * NULL handle is done), 0 if not yet (only with block == 0). */
+const char* r0hip_memcpy_d2h_start(void* h_dst, const void* d_src, size_t bytes, void** h_copy);
+const char* r0hip_copy_finish(void* h_copy, int block, int* done);
 
 /* ---- NTT family (sppark_batch_* in sys/src/cuda.rs:22-46; CPU semantics cpu.rs:305-408) ----
  * Inputs must be canonical field words (< p), as every buffer the Hal hands over is: the first

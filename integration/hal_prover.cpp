@@ -49,45 +49,74 @@ struct Buf {
   uint32_t* p = nullptr;
   size_t words = 0;
   // get_at through a page-locked host mirror of the whole buffer (hal_hip.rs BufferImpl::
-  // get_at on a Merkle node heap): one device-to-host copy at the first read after the buffer
-  // was last written (written()), then host loads. The Prover writes a node heap only while it
-  // builds the tree (hash_rows, hash_fold), so a tree's ~50 x 17 openings cost one bulk copy
-  // (268 MB at po2=20, ~5 ms) instead of one synchronous 13 us copy per node.
+  // get_at on a Merkle node heap). hash_fold's root layer starts one device-to-host copy of the
+  // heap beside the Prover's next calls (mirror_start: r0hip_memcpy_d2h_start); get_at reads the
+  // mirror once it has landed and reads the one node synchronously until then (the root and top
+  // layer right after the build). The Prover writes a node heap only while it builds the tree
+  // (hash_rows, hash_fold), so a tree's ~50 x 17 openings cost one overlapped bulk copy (268 MB
+  // at po2=20, ~5 ms of PCIe) instead of one synchronous 13 us copy per node.
   mutable uint32_t* host = nullptr;
   mutable bool host_ok = false;
+  mutable void* pending = nullptr;  // the mirror's copy in flight
   Buf() = default;
   explicit Buf(size_t n) : words(n) {
     void* d = nullptr;
     ok(r0hip_alloc(&d, (n ? n : 1) * 4));
     p = static_cast<uint32_t*>(d);
   }
-  Buf(Buf&& o) noexcept : p(o.p), words(o.words), host(o.host), host_ok(o.host_ok) {
+  Buf(Buf&& o) noexcept : p(o.p), words(o.words), host(o.host), host_ok(o.host_ok), pending(o.pending) {
     o.p = nullptr;
     o.host = nullptr;
+    o.pending = nullptr;
   }
   Buf& operator=(Buf&& o) noexcept {
     std::swap(p, o.p);
     std::swap(words, o.words);
     std::swap(host, o.host);
     std::swap(host_ok, o.host_ok);
+    std::swap(pending, o.pending);
     return *this;
   }
   ~Buf() {
+    settle();
     if (p) free(const_cast<char*>(r0hip_free(p)));  // a drop never fails the proof
     if (host) free(const_cast<char*>(r0hip_host_free(host)));
   }
-  void written() { host_ok = false; }
-  const uint32_t* at(size_t off) const {
-    if (!host_ok) {
-      if (!host) {
-        void* h = nullptr;
-        ok(r0hip_host_alloc(&h, words * 4));
-        host = static_cast<uint32_t*>(h);
-      }
-      ok(r0hip_memcpy_d2h(host, p, words * 4));
-      host_ok = true;
+  // wait out a mirror copy in flight (before the buffer is written or freed)
+  void settle() const noexcept {
+    if (!pending) return;
+    int done = 0;
+    free(const_cast<char*>(r0hip_copy_finish(pending, 1, &done)));
+    pending = nullptr;
+  }
+  void written() {
+    settle();
+    host_ok = false;
+  }
+  void mirror_start() {
+    written();
+    if (!host) {
+      void* h = nullptr;
+      ok(r0hip_host_alloc(&h, words * 4));
+      host = static_cast<uint32_t*>(h);
     }
-    return host + off;
+    void* c = nullptr;
+    ok(r0hip_memcpy_d2h_start(host, p, words * 4, &c));
+    pending = c;
+    host_ok = true;  // valid once `pending` has finished
+  }
+  // n words at off: from the landed mirror, else one synchronous copy
+  const uint32_t* at(size_t off, size_t n, uint32_t* one) const {
+    if (host_ok && pending) {
+      int done = 0;
+      void* c = pending;
+      pending = nullptr;  // finish releases the handle when done; keep it otherwise
+      ok(r0hip_copy_finish(c, 0, &done));
+      if (!done) pending = c;
+    }
+    if (host_ok && !pending) return host + off;
+    ok(r0hip_memcpy_d2h(one, p + off, n * 4));
+    return one;
   }
   static Buf from(const uint32_t* h, size_t n) {
     Buf b(n);
@@ -132,11 +161,13 @@ struct Merkle {
     top_size = size_t(1) << top_layer;
     ok(r0hip_hash_rows(suite, nodes.p + rows * 8, matrix->p, rows, cols));
     for (size_t i = layers; i-- > 0;) ok(r0hip_hash_fold(suite, nodes.p, (size_t(1) << i) * 2, size_t(1) << i));
-    nodes.written();
-    memcpy(root.w, nodes.at(8), 32);  // get_at(1)
+    nodes.mirror_start();
+    uint32_t one[8];
+    memcpy(root.w, nodes.at(8, 8, one), 32);  // get_at(1)
   }
   void commit(WriteIOP& iop) const {
-    iop.write(nodes.at(top_size * 8), top_size * 8);  // the top layer's get_at reads
+    std::vector<uint32_t> top(top_size * 8);  // nodes.slice(top_size, top_size).view
+    iop.write(nodes.at(top_size * 8, top.size(), top.data()), top.size());
     iop.commit(root);
   }
   // prove/merkle.rs:108-140: gather_sample, then one get_at per node up the tree
@@ -149,7 +180,8 @@ struct Merkle {
     while (idx >= 2 * top_size) {
       const size_t low = idx % 2;
       idx /= 2;
-      iop.write(nodes.at((2 * idx + (1 - low)) * 8), 8);
+      uint32_t one[8];
+      iop.write(nodes.at((2 * idx + (1 - low)) * 8, 8, one), 8);
     }
   }
 };

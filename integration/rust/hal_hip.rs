@@ -12,8 +12,9 @@
 //     assumes of `view`/`get_at` after a kernel;
 //   * `has_unified_memory()` is false: Merkle openings go through `gather_sample`
 //     (prove/merkle.rs:111-129); `get_at` on a Merkle node heap reads a page-locked host
-//     mirror of the heap, filled by one bulk copy at the first read after the tree was built
-//     (a tree's ~50 x 17 node reads would otherwise be one synchronous copy each);
+//     mirror of the heap, copied beside the next calls once hash_fold has built the root
+//     (r0hip_memcpy_d2h_start; a tree's ~50 x 17 node reads would otherwise be one synchronous
+//     copy each);
 //   * combos_prepare / combos_divide are overridden with the device versions, as cuda.rs:
 //     986-1048 does (one batched call for every chunk instead of one per divisor).
 //
@@ -67,13 +68,14 @@ struct DeviceAlloc {
     name: &'static str,
     ptr: *mut c_void,
     bytes: usize,
-    /// Merkle node heaps (marked by hash_fold): get_at reads `mirror`, a page-locked copy of the
-    /// whole allocation made at the first read after the last write (`mirror_ok`). The only Hal
-    /// methods that write a Buffer<Digest> are hash_rows and hash_fold, plus view_mut; all three
-    /// clear `mirror_ok`.
-    mirrored: Cell<bool>,
+    /// Merkle node heaps: hash_fold's root layer starts a copy of the whole allocation into
+    /// `mirror` (page-locked) beside the Prover's next calls (`pending`); get_at reads the mirror
+    /// once that copy has landed and one element synchronously until then. The only Hal methods
+    /// that write a Buffer<Digest> are hash_rows and hash_fold, plus view_mut; all three settle
+    /// the copy and clear `mirror_ok`.
     mirror: Cell<*mut c_void>,
     mirror_ok: Cell<bool>,
+    pending: Cell<*mut c_void>,
 }
 
 impl DeviceAlloc {
@@ -83,27 +85,60 @@ impl DeviceAlloc {
         ffi_wrap(|| unsafe { r0hip_alloc(&mut ptr, bytes) })
             .unwrap_or_else(|e| panic!("allocation failed on {name}: {bytes} bytes: {e}"));
         tracker().lock().unwrap().alloc(bytes);
-        Self { name, ptr, bytes, mirrored: Cell::new(false), mirror: Cell::new(std::ptr::null_mut()),
-               mirror_ok: Cell::new(false) }
+        Self { name, ptr, bytes, mirror: Cell::new(std::ptr::null_mut()), mirror_ok: Cell::new(false),
+               pending: Cell::new(std::ptr::null_mut()) }
     }
 
-    /// the host mirror, refreshed if the device copy was written since
-    fn host(&self) -> *const u8 {
-        if !self.mirror_ok.get() {
-            if self.mirror.get().is_null() {
-                let mut h = std::ptr::null_mut();
-                check(unsafe { r0hip_host_alloc(&mut h, self.bytes) });
-                self.mirror.set(h);
-            }
-            check(unsafe { r0hip_memcpy_d2h(self.mirror.get(), self.ptr, self.bytes) });
-            self.mirror_ok.set(true);
+    /// wait out a mirror copy in flight (before the allocation is written or freed)
+    fn settle(&self) {
+        let c = self.pending.replace(std::ptr::null_mut());
+        if !c.is_null() {
+            let mut done = 0;
+            check(unsafe { r0hip_copy_finish(c, 1, &mut done) });
         }
-        self.mirror.get() as *const u8
+    }
+
+    /// the device copy was written: the mirror is stale
+    fn written(&self) {
+        self.settle();
+        self.mirror_ok.set(false);
+    }
+
+    /// hash_fold built the root: copy the heap to the host beside the next calls
+    fn mirror_start(&self) {
+        self.written();
+        if self.mirror.get().is_null() {
+            let mut h = std::ptr::null_mut();
+            check(unsafe { r0hip_host_alloc(&mut h, self.bytes) });
+            self.mirror.set(h);
+        }
+        let mut c = std::ptr::null_mut();
+        check(unsafe { r0hip_memcpy_d2h_start(self.mirror.get(), self.ptr, self.bytes, &mut c) });
+        self.pending.set(c);
+        self.mirror_ok.set(true);
+    }
+
+    /// the mirror if its copy has landed
+    fn host(&self) -> Option<*const u8> {
+        if !self.mirror_ok.get() {
+            return None;
+        }
+        let c = self.pending.get();
+        if !c.is_null() {
+            let mut done = 0;
+            check(unsafe { r0hip_copy_finish(c, 0, &mut done) });
+            if done == 0 {
+                return None;
+            }
+            self.pending.set(std::ptr::null_mut());
+        }
+        Some(self.mirror.get() as *const u8)
     }
 }
 
 impl Drop for DeviceAlloc {
     fn drop(&mut self) {
+        self.settle();
         tracker().lock().unwrap().free(self.bytes);
         unsafe { r0hip_free(self.ptr) };
         if !self.mirror.get().is_null() {
@@ -152,13 +187,14 @@ impl<T> BufferImpl<T> {
         unsafe { (self.dev_void() as *mut u8).add(idx * std::mem::size_of::<T>()) as *mut u32 }
     }
 
-    /// a Hal method wrote this buffer's device memory; `node_heap`: it is a Merkle node heap
-    /// (hash_fold), whose get_at reads go through the host mirror
-    fn written(&self, node_heap: bool) {
+    /// a Hal method wrote this buffer's device memory; `root`: hash_fold wrote a node heap's
+    /// root layer, so the heap's host mirror starts copying
+    fn written(&self, root: bool) {
         let a = self.alloc.borrow();
-        a.mirror_ok.set(false);
-        if node_heap {
-            a.mirrored.set(true);
+        if root {
+            a.mirror_start();
+        } else {
+            a.written();
         }
     }
 
@@ -190,9 +226,9 @@ impl<T: Clone> Buffer<T> for BufferImpl<T> {
     fn get_at(&self, idx: usize) -> T {
         assert!(idx < self.size);
         let a = self.alloc.borrow();
-        if a.mirrored.get() {
+        if let Some(h) = a.host() {
             let at = (self.offset + idx) * std::mem::size_of::<T>();
-            return unsafe { std::ptr::read_unaligned(a.host().add(at) as *const T) };
+            return unsafe { std::ptr::read_unaligned(h.add(at) as *const T) };
         }
         drop(a);
         self.read(idx, 1).pop().unwrap()
@@ -490,7 +526,7 @@ impl<HS: HipHash> Hal for HipHal<HS> {
     fn hash_fold(&self, io: &Self::Buffer<Digest>, input_size: usize, output_size: usize) {
         assert_eq!(input_size, 2 * output_size);
         check(unsafe { r0hip_hash_fold(HS::SUITE, io.dev(), input_size, output_size) });
-        io.written(true);
+        io.written(output_size == 1);
     }
 
     fn gather_sample(

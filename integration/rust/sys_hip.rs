@@ -96,6 +96,10 @@ unsafe extern "C" {
     pub fn r0hip_host_free(h_ptr: *mut c_void) -> *const c_char;
     pub fn r0hip_synchronize() -> *const c_char;
     pub fn r0hip_free_error(err: *const c_char);
+    // a device-to-host copy beside later calls (the HAL's node-heap mirrors, hal_hip.rs)
+    pub fn r0hip_memcpy_d2h_start(h_dst: *mut c_void, d_src: *const c_void, bytes: usize,
+                                  h_copy: *mut *mut c_void) -> *const c_char;
+    pub fn r0hip_copy_finish(h_copy: *mut c_void, block: c_int, done: *mut c_int) -> *const c_char;
 
     // ---- NTT family (sppark_batch_expand/NTT/iNTT/zk_shift, cuda_batch_bit_reverse) ----
     pub fn r0hip_batch_expand_into_evaluate_ntt(

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <stdexcept>
 #include <vector>
 
@@ -122,6 +123,50 @@ const char* r0hip_host_free(void* h_ptr) {
 }
 const char* r0hip_synchronize(void) {
   return wrap([] {});
+}
+
+namespace {
+struct PendingCopy {  // r0hip_memcpy_d2h_start's handle: the copy's completion on the copy stream
+  hipEvent_t ev = nullptr;
+  ~PendingCopy() {
+    if (ev) (void)hipEventDestroy(ev);
+  }
+};
+}  // namespace
+
+const char* r0hip_memcpy_d2h_start(void* h_dst, const void* d_src, size_t bytes, void** h_copy) {
+  return wrap([&] {
+    R0_REQUIRE(h_copy, "r0hip_memcpy_d2h_start: h_copy is NULL");
+    *h_copy = nullptr;
+    if (!bytes) return;
+    R0_REQUIRE(h_dst && d_src, "r0hip_memcpy_d2h_start: null pointer");
+    if (!host_pinned(h_dst, bytes)) {  // pageable: copied now, as r0hip_memcpy_d2h
+      download(h_dst, d_src, bytes);
+      return;
+    }
+    auto pc = std::make_unique<PendingCopy>();
+    HIP_OK(hipEventCreateWithFlags(&pc->ev, hipEventDisableTiming));
+    const hipStream_t cs = copy_stream();
+    HIP_OK(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, cs));
+    HIP_OK(hipEventRecord(pc->ev, cs));
+    *h_copy = pc.release();
+  });
+}
+const char* r0hip_copy_finish(void* h_copy, int block, int* done) {
+  return wrap_nosync([&] {
+    int fin = 1;
+    if (h_copy) {
+      auto* pc = static_cast<PendingCopy*>(h_copy);
+      const hipError_t e = block ? hipEventSynchronize(pc->ev) : hipEventQuery(pc->ev);
+      if (e == hipErrorNotReady) {
+        fin = 0;
+      } else {
+        delete pc;  // the handle is spent either way
+        HIP_OK(e);
+      }
+    }
+    if (done) *done = fin;
+  });
 }
 void r0hip_free_error(const char* err) { free(const_cast<char*>(err)); }
 

@@ -161,6 +161,16 @@ hipStream_t stream() {
   return t_ctx.stream;
 }
 
+hipStream_t copy_stream() {
+  ensure_init();
+  static hipStream_t s = [] {
+    hipStream_t c = nullptr;
+    HIP_OK(hipStreamCreateWithFlags(&c, hipStreamNonBlocking));
+    return c;
+  }();
+  return s;
+}
+
 void drain_after_error() noexcept {
   if (t_ctx.stream) (void)hipStreamSynchronize(t_ctx.stream);
 }
@@ -236,7 +246,6 @@ void* scratch(size_t bytes, int slot) {
 }
 
 // ---- pinned staging for async uploads (per thread) ---------------------------
-bool host_pinned(const void* p, size_t bytes);
 
 namespace {
 // `bytes` of this thread's page-locked arena (a new, larger arena when it is full; the old one

@@ -33,6 +33,11 @@ namespace r0 {
 // Per-process stream on the current device (created by r0hip_init / lazily).
 hipStream_t stream();
 void ensure_init();
+// One process-wide stream for copies that run beside every thread's work
+// (r0hip_memcpy_d2h_start).
+hipStream_t copy_stream();
+// [p, p + bytes) lies inside one live r0hip_host_alloc block
+bool host_pinned(const void* p, size_t bytes);
 
 // Constant tables kept resident in HBM for the life of the process, keyed by a
 // string; `gen` runs on the host once per key.

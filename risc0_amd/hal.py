@@ -53,6 +53,8 @@ def _declare(L):
         "r0hip_memcpy_d2d": [vp, vp, sz],
         "r0hip_host_alloc": [C.POINTER(vp), sz],
         "r0hip_host_free": [vp],
+        "r0hip_memcpy_d2h_start": [vp, vp, sz, C.POINTER(vp)],
+        "r0hip_copy_finish": [vp, C.c_int, C.POINTER(C.c_int)],
         "r0hip_fill_uniform": [vp, sz, C.c_uint64],
         "r0hip_rv32im_accum_finalize": [vp, sz, sz, sz],
         "r0hip_rv32im_accum": [vp, vp, vp, vp, sz, sz, sz],

@@ -1192,3 +1192,47 @@ def test_prove_recursion_from_program(hal, hal_sha, oracle, suite, po2):
         ref_seal, ref_mix, _ = oracle.prove_segment("recursion", s, po2, ctrl, data, acc, glob)
         assert np.array_equal(mix, ref_mix)
         assert np.array_equal(seal, ref_seal)
+
+
+@pytest.mark.gpu
+def test_async_mirror_copy(hal):
+    """r0hip_memcpy_d2h_start / r0hip_copy_finish (the HAL's node-heap mirrors): a copy into
+    page-locked memory runs beside later calls and lands word for word, polled (block = 0) or
+    waited; a pageable destination and an empty copy are done on return (NULL handle)."""
+    import ctypes
+    import risc0_amd as r
+    lib = r.lib()
+    n = 1 << 24  # 64 MB: long enough to still be in flight at the first poll
+    src = np.random.default_rng(7).integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    d = hal.copy_from_elem("src", src)
+    h = ctypes.c_void_p()
+    r.check(lib.r0hip_host_alloc(ctypes.byref(h), n * 4))
+    try:
+        arr = np.ctypeslib.as_array(ctypes.cast(h, ctypes.POINTER(ctypes.c_uint32)), shape=(n,))
+        arr[:] = 0
+        for block in (0, 1):
+            c, done = ctypes.c_void_p(), ctypes.c_int(-1)
+            r.check(lib.r0hip_memcpy_d2h_start(h, d.ptr, n * 4, ctypes.byref(c)))
+            assert c.value
+            r.check(lib.r0hip_eltwise_zeroize_elem(hal.alloc_elem("other", 1 << 20).ptr, 1 << 20))  # a later call
+            polls = 0
+            while True:
+                r.check(lib.r0hip_copy_finish(c, block, ctypes.byref(done)))
+                if done.value:
+                    break
+                polls += 1
+                assert polls < 10**7
+            assert np.array_equal(arr, src)
+            arr[:] = 0
+        # pageable destination: copied before return, no handle
+        page = np.zeros(n, dtype=np.uint32)
+        c = ctypes.c_void_p(1)
+        r.check(lib.r0hip_memcpy_d2h_start(page.ctypes.data, d.ptr, n * 4, ctypes.byref(c)))
+        assert c.value is None and np.array_equal(page, src)
+        r.check(lib.r0hip_memcpy_d2h_start(h, d.ptr, 0, ctypes.byref(c)))
+        assert c.value is None
+        done = ctypes.c_int(-1)
+        r.check(lib.r0hip_copy_finish(None, 0, ctypes.byref(done)))
+        assert done.value == 1
+    finally:
+        r.check(lib.r0hip_host_free(h))
