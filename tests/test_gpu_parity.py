@@ -1236,3 +1236,51 @@ def test_async_mirror_copy(hal):
         assert done.value == 1
     finally:
         r.check(lib.r0hip_host_free(h))
+
+
+@pytest.mark.gpu
+def test_empty_inputs_are_no_ops(hal):
+    """Every per-op entry point takes a zero count as the reference CPU HAL does (an empty loop,
+    hal/cpu.rs:263-651): it returns success and writes nothing — no zero-sized grid reaches the
+    runtime (a HIP launch of 0 workgroups is an error) and no word of the buffers changes."""
+    import ctypes
+    import risc0_amd as r
+    lib = r.lib()
+    sentinel = np.full(4096, 0x1234567, dtype=np.uint32)
+    a, b, c = (hal.copy_from_elem(n, sentinel) for n in ("a", "b", "c"))
+    u32 = ctypes.POINTER(ctypes.c_uint32)
+    fe = (ctypes.c_uint32 * 4)(1, 2, 3, 4)
+    which = (ctypes.c_uint32 * 1)(0)
+    host = np.zeros(4, dtype=np.uint32)
+    calls = {
+        "memset32": lambda: lib.r0hip_memset32(a.ptr, 7, 0),
+        "memcpy_h2d": lambda: lib.r0hip_memcpy_h2d(a.ptr, host.ctypes.data, 0),
+        "memcpy_d2h": lambda: lib.r0hip_memcpy_d2h(host.ctypes.data, a.ptr, 0),
+        "memcpy_d2d": lambda: lib.r0hip_memcpy_d2d(a.ptr, b.ptr, 0),
+        "expand_evaluate": lambda: lib.r0hip_batch_expand_into_evaluate_ntt(a.ptr, b.ptr, 0, 6, 2),
+        "interpolate": lambda: lib.r0hip_batch_interpolate_ntt(a.ptr, 0, 6),
+        "zk_shift": lambda: lib.r0hip_zk_shift(a.ptr, 0, 6),
+        "bit_reverse": lambda: lib.r0hip_batch_bit_reverse(a.ptr, 0, 6),
+        "evaluate_any": lambda: lib.r0hip_batch_evaluate_any(a.ptr, b.ptr, 1, 6, c.ptr, c.ptr, 0),
+        "mix_poly_coeffs": lambda: lib.r0hip_mix_poly_coeffs(a.ptr, b.ptr, ctypes.cast(which, u32),
+                                                             ctypes.cast(fe, u32), ctypes.cast(fe, u32), 0, 64),
+        "fri_fold": lambda: lib.r0hip_fri_fold(a.ptr, b.ptr, ctypes.cast(fe, u32), 0),
+        "add_elem": lambda: lib.r0hip_eltwise_add_elem(a.ptr, b.ptr, c.ptr, 0),
+        "copy_elem": lambda: lib.r0hip_eltwise_copy_elem(a.ptr, b.ptr, 0),
+        "zeroize": lambda: lib.r0hip_eltwise_zeroize_elem(a.ptr, 0),
+        "sum_extelem": lambda: lib.r0hip_eltwise_sum_extelem(a.ptr, b.ptr, 5, 0),
+        "gather_sample": lambda: lib.r0hip_gather_sample(a.ptr, b.ptr, 3, 0, 64),
+        "prefix_products": lambda: lib.r0hip_prefix_products(a.ptr, 0),
+        "hash_rows": lambda: lib.r0hip_hash_rows(0, a.ptr, b.ptr, 0, 16),
+        "hash_fold": lambda: lib.r0hip_hash_fold(0, a.ptr, 0, 0),
+        "hash_rows_sha": lambda: lib.r0hip_hash_rows(1, a.ptr, b.ptr, 0, 16),
+        "hash_fold_sha": lambda: lib.r0hip_hash_fold(1, a.ptr, 0, 0),
+    }
+    for name, call in calls.items():
+        r.check(call())
+        for buf in (a, b, c):
+            assert np.array_equal(buf.to_numpy(), sentinel), name
+    # a CSR scatter over zero cycles (index holds its one entry, 0)
+    idx = hal.copy_from_elem("idx", np.zeros(1, dtype=np.uint32))
+    r.check(lib.r0hip_scatter(a.ptr, idx.ptr, b.ptr, c.ptr, 0))
+    assert np.array_equal(a.to_numpy(), sentinel)
