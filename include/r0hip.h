@@ -120,6 +120,12 @@ const char* r0hip_fill_uniform(uint32_t* d_out, size_t count, uint64_t seed);
 const char* r0hip_hash_rows(int suite, uint32_t* d_out, const uint32_t* d_matrix, size_t rows, size_t cols);
 /* io[output_size + i] = H(io[input_size + 2i], io[input_size + 2i + 1]) (cpu.rs:569-581) */
 const char* r0hip_hash_fold(int suite, uint32_t* d_io, size_t input_size, size_t output_size);
+/* A whole tree in one call: MerkleTreeProver::new's hash_rows into nodes[rows..2rows) and
+ * hash_fold of every layer down to the root at nodes[1] (prove/merkle.rs:54-81); d_nodes
+ * holds 2*rows digests, rows a power of two. Same words as those calls; the fused form knows
+ * each layer's height, so Poseidon2 layers over all-zero rows store the zero-subtree digests
+ * instead of hashing them. */
+const char* r0hip_merkle_tree(int suite, uint32_t* d_nodes, const uint32_t* d_matrix, size_t rows, size_t cols);
 
 /* ---- circuits (risc0_circuit_{rv32im,recursion}_cuda_eval_check) ---- */
 /* circuit: "rv32im" | "recursion". groups[g] = evaluated register group g (accum=0, code=1, data=2),

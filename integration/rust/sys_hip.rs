@@ -184,6 +184,8 @@ unsafe extern "C" {
     pub fn r0hip_hash_rows(suite: c_int, d_out: *mut u32, d_matrix: *const u32, rows: usize, cols: usize)
         -> *const c_char;
     pub fn r0hip_hash_fold(suite: c_int, d_io: *mut u32, input_size: usize, output_size: usize) -> *const c_char;
+    pub fn r0hip_merkle_tree(suite: c_int, d_nodes: *mut u32, d_matrix: *const u32, rows: usize, cols: usize)
+        -> *const c_char;
 
     // ---- circuits ----
     pub fn r0hip_eval_check(

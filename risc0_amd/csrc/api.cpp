@@ -573,6 +573,13 @@ const char* r0hip_hash_fold(int suite, uint32_t* d_io, size_t input_size, size_t
     hash_fold(stream(), suite, d_io, input_size, output_size);
   });
 }
+const char* r0hip_merkle_tree(int suite, uint32_t* d_nodes, const uint32_t* d_matrix, size_t rows, size_t cols) {
+  return wrap([&] {
+    R0_REQUIRE(suite >= 0 && suite <= 2, "unknown hash suite");
+    R0_REQUIRE(rows > 0 && (rows & (rows - 1)) == 0, "merkle_tree: rows must be a power of two");
+    merkle_tree(stream(), suite, d_nodes, d_matrix, rows, cols);
+  });
+}
 
 const char* r0hip_eval_check(const char* circuit, uint32_t* d_check, const uint32_t* const* d_groups,
                              const uint32_t* d_mix, const uint32_t* d_global, const uint32_t* h_poly_mix,

@@ -14,6 +14,9 @@
 #include "poseidon254.h"
 #include "runtime.h"
 
+#include <map>
+#include <mutex>
+
 namespace r0 {
 namespace {
 
@@ -26,13 +29,38 @@ __device__ __forceinline__ void store_digest(uint32_t* out, const uint32_t* d) {
   o[1] = make_uint4(d[4], d[5], d[6], d[7]);
 }
 
+// ---- zero subtrees (Poseidon2) ---------------------------------------------------------
+// An all-zero row hashes to a constant of the hash (Z_0: the permutation of the zero state
+// for rows of <= 16 columns), and a node whose two children are both Z_k is
+// Z_{k+1} = hash_pair(Z_k, Z_k): the empty-subtree digests of a sparse Merkle tree.
+// rv32im's code group is one column of zeros in every proof (the reference allocates it
+// zero-filled and zeroizes it: rv32im/src/prove/witgen/mod.rs:152,168), so its leaves and
+// every layer above them are these constants. A wave whose rows (or child pairs) all match
+// stores the constant and skips the permutation; any other wave hashes as before, so the
+// words are the same for every input (the host computes the chain with the same
+// permutation, poseidon2_mix).
+struct P2Zero {
+  uint32_t in[8];   // Z_k: the digest both children must equal (fold kernels)
+  uint32_t out[8];  // Z_{k+1} (fold kernels) or Z_0 (row kernels)
+  uint32_t on;
+};
+__device__ __forceinline__ bool wave_all(bool p) { return __ballot(!p) == 0; }
+__device__ __forceinline__ bool eq_digest(uint4 a, uint4 b, const uint32_t* z) {
+  return ((a.x ^ z[0]) | (a.y ^ z[1]) | (a.z ^ z[2]) | (a.w ^ z[3]) | (b.x ^ z[4]) | (b.y ^ z[5]) | (b.z ^ z[6]) |
+          (b.w ^ z[7])) == 0;
+}
+// z[q] for a lane-dependent q < 4 as selects (no dynamic indexing of a kernel argument)
+__device__ __forceinline__ uint32_t sel4(const uint32_t* z, uint32_t q) {
+  return q == 0 ? z[0] : q == 1 ? z[1] : q == 2 ? z[2] : z[3];
+}
+
 // FIRST/LAST: a column range of a longer row (hash_rows_range) starts from the capacity
 // cells 16..23 saved in `state` and ends by saving them there (overwrite-mode sponge: the
 // rate cells are replaced by the next block, so the capacity is the whole carried state)
 template <bool FIRST, bool LAST>
 __global__ __launch_bounds__(kThreads) void p2_rows_kernel(uint32_t* out, uint32_t* state,
                                                          const uint32_t* __restrict__ m, uint64_t rows,
-                                                         uint32_t cols) {
+                                                         uint32_t cols, P2Zero z) {
   uint64_t row = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (row >= rows) return;
   uint32_t c[24];
@@ -61,6 +89,15 @@ __global__ __launch_bounds__(kThreads) void p2_rows_kernel(uint32_t* out, uint32
     }
   };
   load(0);
+  if (FIRST && LAST && nblk == 1 && z.on) {  // one block: a zero row hashes to Z_0
+    uint32_t any = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) any |= nxt[i];
+    if (wave_all(any == 0)) {
+      store_digest(out + row * 8, z.out);
+      return;
+    }
+  }
   for (uint32_t b = 0; b < nblk; b++) {
 #pragma unroll
     for (int i = 0; i < 16; i++) c[i] = nxt[i];
@@ -72,12 +109,16 @@ __global__ __launch_bounds__(kThreads) void p2_rows_kernel(uint32_t* out, uint32
 }
 
 __global__ __launch_bounds__(kThreads) void p2_fold_kernel(uint32_t* io, uint64_t in_off, uint64_t out_off,
-                                                         uint64_t n) {
+                                                         uint64_t n, P2Zero z) {
   uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (i >= n) return;
   const uint4* src = reinterpret_cast<const uint4*>(io + (in_off + 2 * i) * 8);
   uint32_t c[24];
   uint4 a = src[0], b = src[1], d = src[2], e = src[3];
+  if (z.on && wave_all(eq_digest(a, b, z.in) && eq_digest(d, e, z.in))) {
+    store_digest(io + (out_off + i) * 8, z.out);
+    return;
+  }
   c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w; c[4] = b.x; c[5] = b.y; c[6] = b.z; c[7] = b.w;
   c[8] = d.x; c[9] = d.y; c[10] = d.z; c[11] = d.w; c[12] = e.x; c[13] = e.y; c[14] = e.z; c[15] = e.w;
 #pragma unroll
@@ -90,7 +131,7 @@ __global__ __launch_bounds__(kThreads) void p2_fold_kernel(uint32_t* io, uint64_
 // two child digests are loaded before the first permutation, so those loads are in flight
 // while it runs (one node per lane waits for its loads with nothing to overlap them).
 __global__ __launch_bounds__(kThreads) void p2_fold2_kernel(uint32_t* io, uint64_t in_off, uint64_t out_off,
-                                                          uint64_t n) {
+                                                          uint64_t n, P2Zero z) {
   const uint64_t m = (n + 1) / 2;
   const uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (i >= m) return;
@@ -104,13 +145,21 @@ __global__ __launch_bounds__(kThreads) void p2_fold2_kernel(uint32_t* io, uint64
     a2 = s2[0], b2 = s2[1], d2 = s2[2], e2 = s2[3];
   }
   uint32_t c[24];
-  c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w; c[4] = b.x; c[5] = b.y; c[6] = b.z; c[7] = b.w;
-  c[8] = d.x; c[9] = d.y; c[10] = d.z; c[11] = d.w; c[12] = e.x; c[13] = e.y; c[14] = e.z; c[15] = e.w;
+  if (z.on && wave_all(eq_digest(a, b, z.in) && eq_digest(d, e, z.in))) {
+    store_digest(io + (out_off + i) * 8, z.out);
+  } else {
+    c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w; c[4] = b.x; c[5] = b.y; c[6] = b.z; c[7] = b.w;
+    c[8] = d.x; c[9] = d.y; c[10] = d.z; c[11] = d.w; c[12] = e.x; c[13] = e.y; c[14] = e.z; c[15] = e.w;
 #pragma unroll
-  for (int k = 16; k < 24; k++) c[k] = 0;
-  poseidon2_mix(c);
-  store_digest(io + (out_off + i) * 8, c);
+    for (int k = 16; k < 24; k++) c[k] = 0;
+    poseidon2_mix(c);
+    store_digest(io + (out_off + i) * 8, c);
+  }
   if (!two) return;
+  if (z.on && wave_all(eq_digest(a2, b2, z.in) && eq_digest(d2, e2, z.in))) {
+    store_digest(io + (out_off + j) * 8, z.out);
+    return;
+  }
   c[0] = a2.x; c[1] = a2.y; c[2] = a2.z; c[3] = a2.w; c[4] = b2.x; c[5] = b2.y; c[6] = b2.z; c[7] = b2.w;
   c[8] = d2.x; c[9] = d2.y; c[10] = d2.z; c[11] = d2.w; c[12] = e2.x; c[13] = e2.y; c[14] = e2.z; c[15] = e2.w;
 #pragma unroll
@@ -122,8 +171,14 @@ __global__ __launch_bounds__(kThreads) void p2_fold2_kernel(uint32_t* io, uint64
 // Small layers: four lanes per node (poseidon2_mix_quad), so a layer of n nodes keeps 4n
 // lanes busy. Lane q loads cells 4j + q (j < 4) of the two child digests and stores
 // digest words q and 4 + q.
+// Lane q's words of Z_k are z[q] and z[4 + q] (left child words 0, 1; right 2, 3).
+__device__ __forceinline__ bool quad_zero(const uint32_t* c, const uint32_t* zin, uint32_t q) {
+  const uint32_t z0 = sel4(zin, q), z1 = sel4(zin + 4, q);
+  return ((c[0] ^ z0) | (c[1] ^ z1) | (c[2] ^ z0) | (c[3] ^ z1)) == 0;
+}
+
 __global__ __launch_bounds__(kThreads) void p2_fold_quad_kernel(uint32_t* io, uint64_t in_off, uint64_t out_off,
-                                                              uint64_t n) {
+                                                              uint64_t n, P2Zero z) {
   const uint64_t t = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   const uint64_t i = t >> 2;
   if (i >= n) return;  // whole quads: n * 4 lanes
@@ -132,9 +187,14 @@ __global__ __launch_bounds__(kThreads) void p2_fold_quad_kernel(uint32_t* io, ui
   uint32_t c[6];
 #pragma unroll
   for (int j = 0; j < 4; j++) c[j] = src[4 * j + q];
+  uint32_t* dst = io + (out_off + i) * 8;
+  if (z.on && wave_all(quad_zero(c, z.in, q))) {
+    dst[q] = sel4(z.out, q);
+    dst[4 + q] = sel4(z.out + 4, q);
+    return;
+  }
   c[4] = c[5] = 0;
   poseidon2_mix_quad(c);
-  uint32_t* dst = io + (out_off + i) * 8;
   dst[q] = c[0];
   dst[4 + q] = c[1];
 }
@@ -299,15 +359,27 @@ __global__ __launch_bounds__(kThreads) void sha_fold_kernel(uint32_t* io, uint64
 // per node, smaller layers one quad per node (poseidon2_mix_quad: a quarter of the
 // permutation's dependent instructions per lane, so a layer's latency is about a quarter)
 constexpr uint32_t kTopThreads = 1024;
+// zt (or null): the zero-subtree chain, zt + 8k = Z_k, with Z_k0 the top layer's children
 __global__ __launch_bounds__(kTopThreads) void p2_fold_top_kernel(uint32_t* io, uint32_t top_layer_size,
-                                                                 uint32_t quad_max) {
-  for (uint32_t out = top_layer_size; out >= 1; out >>= 1) {
+                                                                 uint32_t quad_max, const uint32_t* zt,
+                                                                 uint32_t k0) {
+  for (uint32_t out = top_layer_size, lvl = k0; out >= 1; out >>= 1, lvl++) {
+    const uint32_t* zin = zt ? zt + 8 * lvl : nullptr;
     if (out > quad_max) {
       for (uint32_t i = threadIdx.x; i < out; i += kTopThreads) {
         const uint32_t* src = io + (uint64_t(2 * out) + 2 * i) * 8;
         uint32_t c[24];
 #pragma unroll
         for (int k = 0; k < 16; k++) c[k] = src[k];
+        if (zin) {
+          uint32_t x = 0;
+#pragma unroll
+          for (int w = 0; w < 16; w++) x |= c[w] ^ zin[w & 7];
+          if (wave_all(x == 0)) {
+            store_digest(io + (uint64_t(out) + i) * 8, zin + 8);
+            continue;
+          }
+        }
 #pragma unroll
         for (int k = 16; k < 24; k++) c[k] = 0;
         poseidon2_mix(c);
@@ -321,9 +393,14 @@ __global__ __launch_bounds__(kTopThreads) void p2_fold_top_kernel(uint32_t* io, 
         uint32_t c[6];
 #pragma unroll
         for (int j = 0; j < 4; j++) c[j] = src[4 * j + q];
+        uint32_t* dst = io + (uint64_t(out) + i) * 8;
+        if (zin && wave_all(quad_zero(c, zin, q))) {
+          dst[q] = sel4(zin + 8, q);
+          dst[4 + q] = sel4(zin + 12, q);
+          continue;
+        }
         c[4] = c[5] = 0;
         poseidon2_mix_quad(c);
-        uint32_t* dst = io + (uint64_t(out) + i) * 8;
         dst[q] = c[0];
         dst[4 + q] = c[1];
       }
@@ -361,6 +438,56 @@ __global__ __launch_bounds__(kThreads) void fold_top_kernel(uint32_t* io, uint32
 
 }  // namespace
 
+// Z_0 .. Z_levels for rows of `cols` columns ((levels + 1) * 8 words, cached): Z_0 is
+// hash_rows of an all-zero row (p2_rows_kernel's sponge on the host), Z_{k+1} the fold of
+// (Z_k, Z_k) (p2_fold_kernel)
+static const std::vector<uint32_t>& p2_zero_chain(size_t cols, size_t levels) {
+  static std::mutex mu;
+  static std::map<std::pair<size_t, size_t>, std::vector<uint32_t>> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto& v = cache[{cols, levels}];
+  if (v.empty()) {
+    uint32_t c[24] = {0};
+    const size_t nblk = cols ? (cols + 15) / 16 : 1;
+    for (size_t b = 0; b < nblk; b++) {
+      for (int i = 0; i < 16; i++) c[i] = 0;
+      poseidon2_mix(c);
+    }
+    v.assign(c, c + 8);
+    for (size_t k = 0; k < levels; k++) {
+      uint32_t d[24] = {0};
+      for (int i = 0; i < 8; i++) d[i] = d[8 + i] = v[8 * k + i];
+      poseidon2_mix(d);
+      v.insert(v.end(), d, d + 8);
+    }
+  }
+  return v;
+}
+
+static P2Zero p2_zero_off() {
+  P2Zero z{};
+  return z;
+}
+
+// R0_P2_ZERO=0 turns the zero-subtree path off (same-box A/B)
+static bool p2_zero_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("R0_P2_ZERO");
+    return !e || strtoul(e, nullptr, 10) != 0;
+  }();
+  return v;
+}
+
+// the leaf constant for one-block Poseidon2 rows (the row kernels check zero rows only then)
+static P2Zero p2_zero_rows(int suite, size_t cols) {
+  P2Zero z{};
+  if (suite != 0 || (cols + 15) / 16 > 1 || !p2_zero_enabled()) return z;
+  const auto& ch = p2_zero_chain(cols, 0);
+  for (int i = 0; i < 8; i++) z.out[i] = ch[i];
+  z.on = 1;
+  return z;
+}
+
 void hash_rows(hipStream_t s, int suite, uint32_t* out, const uint32_t* matrix, size_t rows, size_t cols) {
   if (rows == 0) return;
   R0_REQUIRE(cols < (1ull << 31), "hash_rows: too many columns");
@@ -373,7 +500,7 @@ void hash_rows(hipStream_t s, int suite, uint32_t* out, const uint32_t* matrix, 
   const dim3 grid(div_up(rows, kThreads)), block(kThreads);
   if (suite == 0)
     hipLaunchKernelGGL((p2_rows_kernel<true, true>), grid, block, 0, s, out, nullptr, matrix, uint64_t(rows),
-                       uint32_t(cols));
+                       uint32_t(cols), p2_zero_rows(suite, cols));
   else if (suite == 1)
     hipLaunchKernelGGL((sha_rows_kernel<true, true>), grid, block, 0, s, out, nullptr, matrix, uint64_t(rows),
                        uint32_t(cols));
@@ -388,7 +515,7 @@ static void launch_rows_range(hipStream_t s, int suite, uint32_t* out, uint32_t*
   const dim3 grid(div_up(rows, kThreads)), block(kThreads);
   if (suite == 0)
     hipLaunchKernelGGL((p2_rows_kernel<FIRST, LAST>), grid, block, 0, s, out, state, chunk, uint64_t(rows),
-                       uint32_t(cols));
+                       uint32_t(cols), FIRST && LAST ? p2_zero_rows(suite, cols) : p2_zero_off());
   else
     hipLaunchKernelGGL((sha_rows_kernel<FIRST, LAST>), grid, block, 0, s, out, state, chunk, uint64_t(rows),
                        uint32_t(cols));
@@ -434,18 +561,22 @@ static bool fold_two() {
   return v;
 }
 
-void hash_fold(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t output_size) {
+// z: the zero-subtree pair of this layer (merkle_layers), or off (a standalone fold)
+static void hash_fold_z(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t output_size,
+                        const P2Zero& z) {
   if (output_size == 0) return;
   R0_REQUIRE(input_size == 2 * output_size, "hash_fold: input_size != 2*output_size");
   R0_REQUIRE(suite >= 0 && suite <= 2, "hash_fold: unknown hash suite");
   const dim3 grid(div_up(output_size, kThreads)), block(kThreads);
   const uint64_t in = input_size, out = output_size;
   if (suite == 0 && output_size <= quad_fold_max())
-    hipLaunchKernelGGL(p2_fold_quad_kernel, dim3(div_up(4 * output_size, kThreads)), block, 0, s, io, in, out, out);
+    hipLaunchKernelGGL(p2_fold_quad_kernel, dim3(div_up(4 * output_size, kThreads)), block, 0, s, io, in, out, out,
+                       z);
   else if (suite == 0 && fold_two())
-    hipLaunchKernelGGL(p2_fold2_kernel, dim3(div_up((output_size + 1) / 2, kThreads)), block, 0, s, io, in, out, out);
+    hipLaunchKernelGGL(p2_fold2_kernel, dim3(div_up((output_size + 1) / 2, kThreads)), block, 0, s, io, in, out, out,
+                       z);
   else if (suite == 0)
-    hipLaunchKernelGGL(p2_fold_kernel, grid, block, 0, s, io, in, out, out);
+    hipLaunchKernelGGL(p2_fold_kernel, grid, block, 0, s, io, in, out, out, z);
   else if (suite == 1)
     hipLaunchKernelGGL(sha_fold_kernel, grid, block, 0, s, io, in, out, out);
   else
@@ -453,10 +584,14 @@ void hash_fold(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t
   HIP_OK(hipGetLastError());
 }
 
+void hash_fold(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t output_size) {
+  hash_fold_z(s, suite, io, input_size, output_size, p2_zero_off());
+}
+
 // MerkleTreeProver::new (risc0/zkp/src/prove/merkle.rs:54-81): leaves, then every layer.
 void merkle_tree(hipStream_t s, int suite, uint32_t* nodes, const uint32_t* matrix, size_t rows, size_t cols) {
   hash_rows(s, suite, nodes + rows * 8, matrix, rows, cols);
-  merkle_layers(s, suite, nodes, rows);
+  merkle_layers(s, suite, nodes, rows, cols);
 }
 
 // Poseidon2 tree tops start at this many nodes (R0_P2_TOP_NODES, a power of two <= 512): the
@@ -472,16 +607,32 @@ static size_t p2_top_nodes() {
   return v;
 }
 
-void merkle_layers(hipStream_t s, int suite, uint32_t* nodes, size_t rows) {
+void merkle_layers(hipStream_t s, int suite, uint32_t* nodes, size_t rows, size_t cols) {
   static const char* names[3] = {"merkle_fold_poseidon2", "merkle_fold_sha256", "merkle_fold_poseidon254"};
   KScope ks(names[suite], double(rows) * 32 * 1.5, suite == 0 ? double(rows - 1) * kP2Modmuls : 0);
   size_t layer = rows / 2;
   const size_t top = suite == 0 ? std::min<size_t>(512, p2_top_nodes()) : 512;
-  for (; layer > top; layer /= 2) hash_fold(s, suite, nodes, 2 * layer, layer);
+  // zero-subtree chain of this tree (Poseidon2 with a known column count): the children of
+  // the layer of `out` nodes are at level log2(rows / (2 out))
+  size_t levels = 0;
+  while ((size_t(1) << levels) < rows) levels++;
+  const bool zon = suite == 0 && cols != SIZE_MAX && rows >= 2 && p2_zero_enabled();
+  const std::vector<uint32_t>* chain = zon ? &p2_zero_chain(cols, levels) : nullptr;
+  size_t k = 0;
+  for (; layer > top; layer /= 2, k++) {
+    P2Zero z = p2_zero_off();
+    if (chain) {
+      for (int i = 0; i < 8; i++) z.in[i] = (*chain)[8 * k + i], z.out[i] = (*chain)[8 * (k + 1) + i];
+      z.on = 1;
+    }
+    hash_fold_z(s, suite, nodes, 2 * layer, layer, z);
+  }
   if (layer >= 1) {
     const dim3 grid(1), block(kThreads);
+    const uint32_t* zt = nullptr;
+    if (chain) zt = dev_table("p2zero" + std::to_string(cols) + "_" + std::to_string(levels), [=] { return *chain; });
     if (suite == 0) hipLaunchKernelGGL(p2_fold_top_kernel, grid, dim3(kTopThreads), 0, s, nodes, uint32_t(layer),
-                                    quad_top_max());
+                                    quad_top_max(), zt, uint32_t(k));
     else if (suite == 1) hipLaunchKernelGGL(fold_top_kernel<1>, grid, block, 0, s, nodes, uint32_t(layer));
     else hipLaunchKernelGGL(fold_top_kernel<2>, grid, block, 0, s, nodes, uint32_t(layer));
     HIP_OK(hipGetLastError());

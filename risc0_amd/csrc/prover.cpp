@@ -96,7 +96,7 @@ struct MerkleTree {
   void build_from_leaves(int suite, DevBuf leaf_nodes, const uint32_t* m, size_t r, size_t c) {
     {
       Span sp("commit");
-      merkle_layers(stream(), suite, leaf_nodes.p, r);
+      merkle_layers(stream(), suite, leaf_nodes.p, r, c);
     }
     finish(std::move(leaf_nodes), m, r, c);
   }

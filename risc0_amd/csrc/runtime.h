@@ -232,8 +232,9 @@ void hash_rows_range(hipStream_t s, int suite, uint32_t* out, uint32_t* state, c
 void hash_fold(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t output_size);
 // Full merkle tree: nodes[rows..2rows) = leaves, hashes every layer up to the root.
 void merkle_tree(hipStream_t s, int suite, uint32_t* nodes, const uint32_t* matrix, size_t rows, size_t cols);
-// The layers above leaves already in nodes[rows..2rows).
-void merkle_layers(hipStream_t s, int suite, uint32_t* nodes, size_t rows);
+// The layers above leaves already in nodes[rows..2rows). `cols` (the matrix's column count,
+// SIZE_MAX if unknown) lets Poseidon2 layers skip zero subtrees (hash.hip, P2Zero).
+void merkle_layers(hipStream_t s, int suite, uint32_t* nodes, size_t rows, size_t cols = SIZE_MAX);
 
 // Element-wise and polynomial kernels (eltwise.hip).
 void eltwise_add(hipStream_t s, uint32_t* out, const uint32_t* a, const uint32_t* b, size_t n);

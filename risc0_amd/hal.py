@@ -85,6 +85,7 @@ def _declare(L):
         "r0hip_prefix_products": [vp, sz],
         "r0hip_hash_rows": [C.c_int, vp, vp, sz, sz],
         "r0hip_hash_fold": [C.c_int, vp, sz, sz],
+        "r0hip_merkle_tree": [C.c_int, vp, vp, sz, sz],
         "r0hip_eval_check": [C.c_char_p, vp, C.POINTER(vp), vp, vp, u32p, C.c_uint32],
         "r0hip_prove_segment": [C.c_char_p, C.c_int, C.c_uint32, vp, vp, vp, vp, C.c_int, C.c_uint32, u32p, sz,
                                 C.POINTER(sz), u32p],
@@ -295,6 +296,10 @@ class HipHal:
 
     def hash_fold(self, io, input_size, output_size):
         check(lib().r0hip_hash_fold(self.suite, io.ptr, input_size, output_size))
+
+    def merkle_tree(self, nodes, matrix, rows):
+        """nodes (2*rows digests) <- leaves and every layer (r0hip_merkle_tree)"""
+        check(lib().r0hip_merkle_tree(self.suite, nodes.ptr, matrix.ptr, rows, matrix.size // rows))
 
     def gather_sample(self, dst, src, idx, size, stride):
         check(lib().r0hip_gather_sample(dst.ptr, src.ptr, idx, size, stride))

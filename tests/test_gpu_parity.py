@@ -270,6 +270,45 @@ def test_hash_fold(hal, hal_sha, oracle, suite, inputs):
     assert np.array_equal(d.to_numpy(), io)
 
 
+@pytest.mark.parametrize("suite", ["poseidon2", "sha-256"])
+@pytest.mark.parametrize("rows,cols,pattern", [
+    (4096, 1, "zero"), (4096, 16, "zero"), (1 << 17, 1, "zero"), (4096, 211, "zero"),
+    (1 << 16, 1, "half"), (4096, 1, "one"), (4096, 16, "blocks"), (1 << 17, 1, "sparse"),
+    (1 << 15, 17, "blocks"), (2, 1, "zero"), (1, 1, "zero")])
+def test_merkle_tree_zero_subtrees(hal, hal_sha, oracle, suite, rows, cols, pattern):
+    """r0hip_merkle_tree (MerkleTreeProver::new in one call, prove/merkle.rs:54-81) equals the
+    oracle's hash_rows + hash_fold of every layer. Zero rows exercise the Poseidon2 zero-subtree
+    path (hash.hip, P2Zero): whole trees of zero rows (rv32im's code group), zero halves, one
+    nonzero row, 64-row and misaligned 96-row runs that give waves of mixed hits, and sparse rows."""
+    h, s = H(suite), S(oracle, suite)
+    rng = np.random.default_rng(rows * 31 + cols)
+    m = oracle.rand_elems(rng, rows * cols).reshape(cols, rows)
+    if pattern == "zero":
+        m[:] = 0
+    elif pattern == "half":
+        m[:, : rows // 2] = 0
+    elif pattern == "one":
+        m[:] = 0
+        m[:, 777] = 1
+    elif pattern == "blocks":
+        idx = np.arange(rows)
+        m[:, ((idx // 64) % 2 == 0) | ((idx // 96) % 3 == 1)] = 0
+    elif pattern == "sparse":
+        m[:, rng.random(rows) > 0.01] = 0
+    m = np.ascontiguousarray(m).reshape(-1)
+    nodes = h.alloc_digest("nodes", rows * 2)
+    h.merkle_tree(nodes, dev(h, m), rows)
+    io = np.zeros(rows * 2 * 8, np.uint32)
+    leaves = np.zeros(rows * 8, np.uint32)
+    oracle.hash_rows(s, leaves, m)
+    io[rows * 8:] = leaves
+    layer = rows
+    while layer > 1:
+        oracle.hash_fold(s, io, layer, layer // 2)
+        layer //= 2
+    assert np.array_equal(nodes.to_numpy()[8:], io[8:])
+
+
 @pytest.mark.parametrize("po2,last", [(4, 16), (10, 1000), (12, 4096), (20, (1 << 20) - 7), (16, 1), (13, 4097)])
 def test_rv32im_accum_finalize(hal, oracle, po2, last):
     # accumulation phases 2-3 (rv32im-sys/kernels/cxx/ffi.cpp:326-360): 103 accum columns,
