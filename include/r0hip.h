@@ -123,7 +123,7 @@ const char* r0hip_hash_fold(int suite, uint32_t* d_io, size_t input_size, size_t
 /* A whole tree in one call: MerkleTreeProver::new's hash_rows into nodes[rows..2rows) and
  * hash_fold of every layer down to the root at nodes[1] (prove/merkle.rs:54-81); d_nodes
  * holds 2*rows digests, rows a power of two. Same words as those calls; the fused form knows
- * each layer's height, so Poseidon2 layers over all-zero rows store the zero-subtree digests
+ * each layer's height, so Poseidon2 and SHA-256 layers over all-zero rows store the zero-subtree digests
  * instead of hashing them. */
 const char* r0hip_merkle_tree(int suite, uint32_t* d_nodes, const uint32_t* d_matrix, size_t rows, size_t cols);
 

@@ -13,9 +13,11 @@
 #include "poseidon2.h"
 #include "poseidon254.h"
 #include "runtime.h"
+#include "transcript.h"
 
 #include <map>
 #include <mutex>
+#include <tuple>
 
 namespace r0 {
 namespace {
@@ -29,17 +31,17 @@ __device__ __forceinline__ void store_digest(uint32_t* out, const uint32_t* d) {
   o[1] = make_uint4(d[4], d[5], d[6], d[7]);
 }
 
-// ---- zero subtrees (Poseidon2) ---------------------------------------------------------
-// An all-zero row hashes to a constant of the hash (Z_0: the permutation of the zero state
-// for rows of <= 16 columns), and a node whose two children are both Z_k is
+// ---- zero subtrees (Poseidon2, SHA-256) -------------------------------------------------
+// An all-zero row hashes to a constant of the hash (Z_0: one permutation / compression of
+// a zero block for rows of <= 16 columns), and a node whose two children are both Z_k is
 // Z_{k+1} = hash_pair(Z_k, Z_k): the empty-subtree digests of a sparse Merkle tree.
 // rv32im's code group is one column of zeros in every proof (the reference allocates it
 // zero-filled and zeroizes it: rv32im/src/prove/witgen/mod.rs:152,168), so its leaves and
 // every layer above them are these constants. A wave whose rows (or child pairs) all match
 // stores the constant and skips the permutation; any other wave hashes as before, so the
-// words are the same for every input (the host computes the chain with the same
-// permutation, poseidon2_mix).
-struct P2Zero {
+// words are the same for every input (the host computes the chain with the transcript's
+// hash functions, transcript.h, whose words the row and fold tests pin to the kernels').
+struct ZeroSub {
   uint32_t in[8];   // Z_k: the digest both children must equal (fold kernels)
   uint32_t out[8];  // Z_{k+1} (fold kernels) or Z_0 (row kernels)
   uint32_t on;
@@ -60,7 +62,7 @@ __device__ __forceinline__ uint32_t sel4(const uint32_t* z, uint32_t q) {
 template <bool FIRST, bool LAST>
 __global__ __launch_bounds__(kThreads) void p2_rows_kernel(uint32_t* out, uint32_t* state,
                                                          const uint32_t* __restrict__ m, uint64_t rows,
-                                                         uint32_t cols, P2Zero z) {
+                                                         uint32_t cols, ZeroSub z) {
   uint64_t row = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (row >= rows) return;
   uint32_t c[24];
@@ -109,7 +111,7 @@ __global__ __launch_bounds__(kThreads) void p2_rows_kernel(uint32_t* out, uint32
 }
 
 __global__ __launch_bounds__(kThreads) void p2_fold_kernel(uint32_t* io, uint64_t in_off, uint64_t out_off,
-                                                         uint64_t n, P2Zero z) {
+                                                         uint64_t n, ZeroSub z) {
   uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (i >= n) return;
   const uint4* src = reinterpret_cast<const uint4*>(io + (in_off + 2 * i) * 8);
@@ -131,7 +133,7 @@ __global__ __launch_bounds__(kThreads) void p2_fold_kernel(uint32_t* io, uint64_
 // two child digests are loaded before the first permutation, so those loads are in flight
 // while it runs (one node per lane waits for its loads with nothing to overlap them).
 __global__ __launch_bounds__(kThreads) void p2_fold2_kernel(uint32_t* io, uint64_t in_off, uint64_t out_off,
-                                                          uint64_t n, P2Zero z) {
+                                                          uint64_t n, ZeroSub z) {
   const uint64_t m = (n + 1) / 2;
   const uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (i >= m) return;
@@ -178,7 +180,7 @@ __device__ __forceinline__ bool quad_zero(const uint32_t* c, const uint32_t* zin
 }
 
 __global__ __launch_bounds__(kThreads) void p2_fold_quad_kernel(uint32_t* io, uint64_t in_off, uint64_t out_off,
-                                                              uint64_t n, P2Zero z) {
+                                                              uint64_t n, ZeroSub z) {
   const uint64_t t = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   const uint64_t i = t >> 2;
   if (i >= n) return;  // whole quads: n * 4 lanes
@@ -307,7 +309,7 @@ __device__ __forceinline__ void sha_init(uint32_t* s) {
 template <bool FIRST, bool LAST>
 __global__ __launch_bounds__(kThreads) void sha_rows_kernel(uint32_t* out, uint32_t* state,
                                                           const uint32_t* __restrict__ m, uint64_t rows,
-                                                          uint32_t cols) {
+                                                          uint32_t cols, ZeroSub z) {
   uint64_t row = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (row >= rows) return;
   uint32_t s[8], w[16], nxt[16];
@@ -323,6 +325,15 @@ __global__ __launch_bounds__(kThreads) void sha_rows_kernel(uint32_t* out, uint3
     for (int i = 0; i < 16; i++) nxt[i] = (col + i < cols) ? m[uint64_t(col + i) * rows + row] : 0u;
   };
   if (cols) load(0);
+  if (FIRST && LAST && cols <= 16 && z.on) {  // one block: a zero row hashes to Z_0
+    uint32_t any = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) any |= cols ? nxt[i] : 0u;
+    if (wave_all(any == 0)) {
+      store_digest(out + row * 8, z.out);
+      return;
+    }
+  }
   for (uint32_t col = 0; col < cols; col += 16) {
 #pragma unroll
     for (int i = 0; i < 16; i++) w[i] = __builtin_bswap32(nxt[i]);
@@ -340,10 +351,16 @@ __global__ __launch_bounds__(kThreads) void sha_rows_kernel(uint32_t* out, uint3
 }
 
 __global__ __launch_bounds__(kThreads) void sha_fold_kernel(uint32_t* io, uint64_t in_off, uint64_t out_off,
-                                                          uint64_t n) {
+                                                          uint64_t n, ZeroSub z) {
   uint64_t i = uint64_t(blockIdx.x) * kThreads + threadIdx.x;
   if (i >= n) return;
-  const uint32_t* src = io + (in_off + 2 * i) * 8;
+  const uint4* src4 = reinterpret_cast<const uint4*>(io + (in_off + 2 * i) * 8);
+  const uint4 a = src4[0], b = src4[1], c = src4[2], e = src4[3];
+  if (z.on && wave_all(eq_digest(a, b, z.in) && eq_digest(c, e, z.in))) {
+    store_digest(io + (out_off + i) * 8, z.out);
+    return;
+  }
+  const uint32_t src[16] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w, e.x, e.y, e.z, e.w};
   uint32_t s[8], w[16];
   sha_init(s);
 #pragma unroll
@@ -413,11 +430,22 @@ __global__ __launch_bounds__(kTopThreads) void p2_fold_top_kernel(uint32_t* io, 
 // SHA-256 / Poseidon254 tree top inside one workgroup: layers with <= 512 nodes, all
 // hashed by 256 lanes with a workgroup barrier between layers (same-CU visibility).
 template <int SUITE>
-__global__ __launch_bounds__(kThreads) void fold_top_kernel(uint32_t* io, uint32_t top_layer_size) {
-  for (uint32_t out = top_layer_size; out >= 1; out >>= 1) {
+__global__ __launch_bounds__(kThreads) void fold_top_kernel(uint32_t* io, uint32_t top_layer_size, const uint32_t* zt,
+                                                          uint32_t k0) {
+  for (uint32_t out = top_layer_size, lvl = k0; out >= 1; out >>= 1, lvl++) {
+    const uint32_t* zin = zt ? zt + 8 * lvl : nullptr;
     for (uint32_t i = threadIdx.x; i < out; i += kThreads) {
       const uint32_t* src = io + (uint64_t(2 * out) + 2 * i) * 8;
       uint32_t d[8];
+      if (zin) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int w = 0; w < 16; w++) x |= src[w] ^ zin[w & 7];
+        if (wave_all(x == 0)) {
+          store_digest(io + (uint64_t(out) + i) * 8, zin + 8);
+          continue;
+        }
+      }
       if (SUITE == 2) {
         p254_node(src, d);
       } else {
@@ -439,38 +467,41 @@ __global__ __launch_bounds__(kThreads) void fold_top_kernel(uint32_t* io, uint32
 }  // namespace
 
 // Z_0 .. Z_levels for rows of `cols` columns ((levels + 1) * 8 words, cached): Z_0 is
-// hash_rows of an all-zero row (p2_rows_kernel's sponge on the host), Z_{k+1} the fold of
-// (Z_k, Z_k) (p2_fold_kernel)
-static const std::vector<uint32_t>& p2_zero_chain(size_t cols, size_t levels) {
+// hash_rows of an all-zero row (the suite's unpadded row hash, transcript.h hash_elems),
+// Z_{k+1} the pair hash of (Z_k, Z_k). Suites 0 (Poseidon2) and 1 (SHA-256).
+static const std::vector<uint32_t>& zero_chain(int suite, size_t cols, size_t levels) {
   static std::mutex mu;
-  static std::map<std::pair<size_t, size_t>, std::vector<uint32_t>> cache;
+  static std::map<std::tuple<int, size_t, size_t>, std::vector<uint32_t>> cache;
   std::lock_guard<std::mutex> lk(mu);
-  auto& v = cache[{cols, levels}];
+  auto& v = cache[{suite, cols, levels}];
   if (v.empty()) {
-    uint32_t c[24] = {0};
-    const size_t nblk = cols ? (cols + 15) / 16 : 1;
-    for (size_t b = 0; b < nblk; b++) {
-      for (int i = 0; i < 16; i++) c[i] = 0;
-      poseidon2_mix(c);
-    }
-    v.assign(c, c + 8);
+    const std::vector<uint32_t> zeros(cols, 0u);
+    Digest d = hash_elems(suite, zeros.data(), cols);
+    v.assign(d.w, d.w + 8);
     for (size_t k = 0; k < levels; k++) {
-      uint32_t d[24] = {0};
-      for (int i = 0; i < 8; i++) d[i] = d[8 + i] = v[8 * k + i];
-      poseidon2_mix(d);
-      v.insert(v.end(), d, d + 8);
+      Digest a;
+      memcpy(a.w, &v[8 * k], 32);
+      if (suite == 0) {
+        uint32_t c[24] = {0};
+        for (int i = 0; i < 8; i++) c[i] = c[8 + i] = a.w[i];
+        poseidon2_mix(c);
+        memcpy(d.w, c, 32);
+      } else {
+        d = sha::hash_pair(a, a);
+      }
+      v.insert(v.end(), d.w, d.w + 8);
     }
   }
   return v;
 }
 
-static P2Zero p2_zero_off() {
-  P2Zero z{};
+static ZeroSub zero_off() {
+  ZeroSub z{};
   return z;
 }
 
 // R0_P2_ZERO=0 turns the zero-subtree path off (same-box A/B)
-static bool p2_zero_enabled() {
+static bool zero_enabled() {
   static const bool v = [] {
     const char* e = getenv("R0_P2_ZERO");
     return !e || strtoul(e, nullptr, 10) != 0;
@@ -478,11 +509,11 @@ static bool p2_zero_enabled() {
   return v;
 }
 
-// the leaf constant for one-block Poseidon2 rows (the row kernels check zero rows only then)
-static P2Zero p2_zero_rows(int suite, size_t cols) {
-  P2Zero z{};
-  if (suite != 0 || (cols + 15) / 16 > 1 || !p2_zero_enabled()) return z;
-  const auto& ch = p2_zero_chain(cols, 0);
+// the leaf constant for one-block rows (the row kernels check zero rows only then)
+static ZeroSub zero_rows(int suite, size_t cols) {
+  ZeroSub z{};
+  if (suite > 1 || cols > 16 || !zero_enabled()) return z;
+  const auto& ch = zero_chain(suite, cols, 0);
   for (int i = 0; i < 8; i++) z.out[i] = ch[i];
   z.on = 1;
   return z;
@@ -500,10 +531,10 @@ void hash_rows(hipStream_t s, int suite, uint32_t* out, const uint32_t* matrix, 
   const dim3 grid(div_up(rows, kThreads)), block(kThreads);
   if (suite == 0)
     hipLaunchKernelGGL((p2_rows_kernel<true, true>), grid, block, 0, s, out, nullptr, matrix, uint64_t(rows),
-                       uint32_t(cols), p2_zero_rows(suite, cols));
+                       uint32_t(cols), zero_rows(suite, cols));
   else if (suite == 1)
     hipLaunchKernelGGL((sha_rows_kernel<true, true>), grid, block, 0, s, out, nullptr, matrix, uint64_t(rows),
-                       uint32_t(cols));
+                       uint32_t(cols), zero_rows(suite, cols));
   else
     hipLaunchKernelGGL(p254_rows_kernel, grid, block, 0, s, out, matrix, uint64_t(rows), uint32_t(cols));
   HIP_OK(hipGetLastError());
@@ -515,10 +546,10 @@ static void launch_rows_range(hipStream_t s, int suite, uint32_t* out, uint32_t*
   const dim3 grid(div_up(rows, kThreads)), block(kThreads);
   if (suite == 0)
     hipLaunchKernelGGL((p2_rows_kernel<FIRST, LAST>), grid, block, 0, s, out, state, chunk, uint64_t(rows),
-                       uint32_t(cols), FIRST && LAST ? p2_zero_rows(suite, cols) : p2_zero_off());
+                       uint32_t(cols), FIRST && LAST ? zero_rows(suite, cols) : zero_off());
   else
     hipLaunchKernelGGL((sha_rows_kernel<FIRST, LAST>), grid, block, 0, s, out, state, chunk, uint64_t(rows),
-                       uint32_t(cols));
+                       uint32_t(cols), FIRST && LAST ? zero_rows(suite, cols) : zero_off());
   HIP_OK(hipGetLastError());
 }
 
@@ -563,7 +594,7 @@ static bool fold_two() {
 
 // z: the zero-subtree pair of this layer (merkle_layers), or off (a standalone fold)
 static void hash_fold_z(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t output_size,
-                        const P2Zero& z) {
+                        const ZeroSub& z) {
   if (output_size == 0) return;
   R0_REQUIRE(input_size == 2 * output_size, "hash_fold: input_size != 2*output_size");
   R0_REQUIRE(suite >= 0 && suite <= 2, "hash_fold: unknown hash suite");
@@ -578,14 +609,14 @@ static void hash_fold_z(hipStream_t s, int suite, uint32_t* io, size_t input_siz
   else if (suite == 0)
     hipLaunchKernelGGL(p2_fold_kernel, grid, block, 0, s, io, in, out, out, z);
   else if (suite == 1)
-    hipLaunchKernelGGL(sha_fold_kernel, grid, block, 0, s, io, in, out, out);
+    hipLaunchKernelGGL(sha_fold_kernel, grid, block, 0, s, io, in, out, out, z);
   else
     hipLaunchKernelGGL(p254_fold_kernel, grid, block, 0, s, io, in, out, out);
   HIP_OK(hipGetLastError());
 }
 
 void hash_fold(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t output_size) {
-  hash_fold_z(s, suite, io, input_size, output_size, p2_zero_off());
+  hash_fold_z(s, suite, io, input_size, output_size, zero_off());
 }
 
 // MerkleTreeProver::new (risc0/zkp/src/prove/merkle.rs:54-81): leaves, then every layer.
@@ -612,15 +643,15 @@ void merkle_layers(hipStream_t s, int suite, uint32_t* nodes, size_t rows, size_
   KScope ks(names[suite], double(rows) * 32 * 1.5, suite == 0 ? double(rows - 1) * kP2Modmuls : 0);
   size_t layer = rows / 2;
   const size_t top = suite == 0 ? std::min<size_t>(512, p2_top_nodes()) : 512;
-  // zero-subtree chain of this tree (Poseidon2 with a known column count): the children of
+  // zero-subtree chain of this tree (Poseidon2 or SHA-256 with a known column count): the children of
   // the layer of `out` nodes are at level log2(rows / (2 out))
   size_t levels = 0;
   while ((size_t(1) << levels) < rows) levels++;
-  const bool zon = suite == 0 && cols != SIZE_MAX && rows >= 2 && p2_zero_enabled();
-  const std::vector<uint32_t>* chain = zon ? &p2_zero_chain(cols, levels) : nullptr;
+  const bool zon = suite <= 1 && cols != SIZE_MAX && rows >= 2 && zero_enabled();
+  const std::vector<uint32_t>* chain = zon ? &zero_chain(suite, cols, levels) : nullptr;
   size_t k = 0;
   for (; layer > top; layer /= 2, k++) {
-    P2Zero z = p2_zero_off();
+    ZeroSub z = zero_off();
     if (chain) {
       for (int i = 0; i < 8; i++) z.in[i] = (*chain)[8 * k + i], z.out[i] = (*chain)[8 * (k + 1) + i];
       z.on = 1;
@@ -630,11 +661,14 @@ void merkle_layers(hipStream_t s, int suite, uint32_t* nodes, size_t rows, size_
   if (layer >= 1) {
     const dim3 grid(1), block(kThreads);
     const uint32_t* zt = nullptr;
-    if (chain) zt = dev_table("p2zero" + std::to_string(cols) + "_" + std::to_string(levels), [=] { return *chain; });
+    if (chain)
+      zt = dev_table("zero" + std::to_string(suite) + "_" + std::to_string(cols) + "_" + std::to_string(levels),
+                     [=] { return *chain; });
     if (suite == 0) hipLaunchKernelGGL(p2_fold_top_kernel, grid, dim3(kTopThreads), 0, s, nodes, uint32_t(layer),
                                     quad_top_max(), zt, uint32_t(k));
-    else if (suite == 1) hipLaunchKernelGGL(fold_top_kernel<1>, grid, block, 0, s, nodes, uint32_t(layer));
-    else hipLaunchKernelGGL(fold_top_kernel<2>, grid, block, 0, s, nodes, uint32_t(layer));
+    else if (suite == 1)
+      hipLaunchKernelGGL(fold_top_kernel<1>, grid, block, 0, s, nodes, uint32_t(layer), zt, uint32_t(k));
+    else hipLaunchKernelGGL(fold_top_kernel<2>, grid, block, 0, s, nodes, uint32_t(layer), nullptr, 0u);
     HIP_OK(hipGetLastError());
   }
 }

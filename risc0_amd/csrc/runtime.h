@@ -233,7 +233,7 @@ void hash_fold(hipStream_t s, int suite, uint32_t* io, size_t input_size, size_t
 // Full merkle tree: nodes[rows..2rows) = leaves, hashes every layer up to the root.
 void merkle_tree(hipStream_t s, int suite, uint32_t* nodes, const uint32_t* matrix, size_t rows, size_t cols);
 // The layers above leaves already in nodes[rows..2rows). `cols` (the matrix's column count,
-// SIZE_MAX if unknown) lets Poseidon2 layers skip zero subtrees (hash.hip, P2Zero).
+// SIZE_MAX if unknown) lets Poseidon2 and SHA-256 layers skip zero subtrees (hash.hip, ZeroSub).
 void merkle_layers(hipStream_t s, int suite, uint32_t* nodes, size_t rows, size_t cols = SIZE_MAX);
 
 // Element-wise and polynomial kernels (eltwise.hip).

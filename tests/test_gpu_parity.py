@@ -277,8 +277,8 @@ def test_hash_fold(hal, hal_sha, oracle, suite, inputs):
     (1 << 15, 17, "blocks"), (2, 1, "zero"), (1, 1, "zero")])
 def test_merkle_tree_zero_subtrees(hal, hal_sha, oracle, suite, rows, cols, pattern):
     """r0hip_merkle_tree (MerkleTreeProver::new in one call, prove/merkle.rs:54-81) equals the
-    oracle's hash_rows + hash_fold of every layer. Zero rows exercise the Poseidon2 zero-subtree
-    path (hash.hip, P2Zero): whole trees of zero rows (rv32im's code group), zero halves, one
+    oracle's hash_rows + hash_fold of every layer. Zero rows exercise the zero-subtree
+    path (hash.hip, ZeroSub; Poseidon2 and SHA-256): whole trees of zero rows (rv32im's code group), zero halves, one
     nonzero row, 64-row and misaligned 96-row runs that give waves of mixed hits, and sparse rows."""
     h, s = H(suite), S(oracle, suite)
     rng = np.random.default_rng(rows * 31 + cols)
