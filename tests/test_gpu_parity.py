@@ -307,6 +307,29 @@ def test_merkle_tree_zero_subtrees(hal, hal_sha, oracle, suite, rows, cols, patt
         oracle.hash_fold(s, io, layer, layer // 2)
         layer //= 2
     assert np.array_equal(nodes.to_numpy()[8:], io[8:])
+    # the per-op form (hash_rows into the heap's leaf range, then hash_fold per layer, as
+    # MerkleTreeProver::new drives a HAL): the library's heap note gives the folds their height
+    ops = h.alloc_digest("nodes_ops", rows * 2)
+    h.hash_rows(ops.slice(rows, rows), dev(h, m))
+    layer = rows
+    while layer > 1:
+        h.hash_fold(ops, layer, layer // 2)
+        layer //= 2
+    assert np.array_equal(ops.to_numpy()[8:], io[8:])
+    # the same heap refilled with other leaves (a stale note): still the oracle's words
+    if rows >= 4:
+        other = rng.integers(0, 2**32, rows * 8, dtype=np.uint64).astype(np.uint32) // 3
+        if suite == "poseidon2":
+            other[: rows * 4] = 0  # half the leaves equal to no Z_k: words, not zero digests
+        io2 = np.zeros(rows * 2 * 8, np.uint32)
+        io2[rows * 8:] = other
+        ops.copy_from(io2)  # same base as the noted heap
+        layer = rows
+        while layer > 1:
+            h.hash_fold(ops, layer, layer // 2)
+            oracle.hash_fold(s, io2, layer, layer // 2)
+            layer //= 2
+        assert np.array_equal(ops.to_numpy()[8:], io2[8:])
 
 
 @pytest.mark.parametrize("po2,last", [(4, 16), (10, 1000), (12, 4096), (20, (1 << 20) - 7), (16, 1), (13, 4097)])
