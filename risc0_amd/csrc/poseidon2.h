@@ -208,9 +208,18 @@ R0_HD void p2_m_ext64s(const int32_t* x, int64_t* y) {
 // and the round constants are stored pre-multiplied by sigma_r R^-1. One Montgomery
 // multiply by R^3 / sigma restores the Montgomery form (X * R) before the partial rounds
 // and at the end. Rounds 0 and 5 start from sigma = R, so their constants are unchanged.
+//
+// The constant enters the REDC's low word (round 6): with rcs = rc + (2^32 mod p) mod p (p if
+// that is 0), sredc(y + rcs - 2^32) is congruent to sredc(y + rc), and its REDC multiplier
+// m = lo(y + rcs - 2^32) p^-1 = (lo(y) + rcs) p^-1 needs only the 32-bit sum. The result is
+// then exactly hi(y - m p): the low word of y - m p is 2^32 - rcs (the REDC zeroes the low word
+// of y + rcs - 2^32 - m p), so adding rcs - 2^32 carries out and cancels. One full-rate
+// v_add_u32 replaces the 64-bit add of rc per cell (sredc_rc). |y + rcs - 2^32| < 110.6p, so
+// the output stays below 0.5p + 52.
 struct P2Scaled {
-  uint32_t rc[8 * 24];  // rounds 0-3 and 5-7 (round 4 uses kP2Full as it is)
+  uint32_t rc[8 * 24];   // rounds 0-3 and 5-7 (round 4 uses kP2Full as it is)
   uint32_t k_mid, k_end;
+  uint32_t rcs[8 * 24];  // rc + (2^32 mod p) mod p, in [1, p], for sredc_rc
 };
 constexpr uint32_t p2c_mul(uint32_t a, uint32_t b) { return uint32_t(uint64_t(a) * b % kP); }
 constexpr uint32_t p2c_pow(uint32_t a, uint64_t e) {
@@ -240,7 +249,16 @@ constexpr P2Scaled p2_make_scaled() {
     else t.k_mid = k;
   }
   for (int i = 0; i < 24; i++) t.rc[4 * 24 + i] = full[4 * 24 + i];
+  for (int i = 0; i < 8 * 24; i++) {
+    const uint32_t v = uint32_t((uint64_t(t.rc[i]) + R) % kP);
+    t.rcs[i] = v ? v : kP;
+  }
   return t;
+}
+// sredc(y + rc) (mod p) for the stored round constant rcs = rc + (2^32 mod p): above
+R0_HD int32_t sredc_rc(int64_t y, uint32_t rcs) {
+  const int32_t m = int32_t((uint32_t(uint64_t(y)) + rcs) * kPinv);
+  return int32_t(uint64_t(y - int64_t(m) * int64_t(kP)) >> 32);
 }
 #if defined(__HIP_DEVICE_COMPILE__)
 __constant__ static const P2Scaled kP2S = p2_make_scaled();
@@ -261,7 +279,7 @@ R0_HD void poseidon2_mix(uint32_t* c) {
 #pragma unroll 1
   for (int r = 0; r < 4; r++) {
 #pragma unroll
-    for (int i = 0; i < 24; i++) x[i] = p2_sbox_s(sredc(y[i] + int64_t(kP2S.rc[r * 24 + i])));
+    for (int i = 0; i < 24; i++) x[i] = p2_sbox_s(sredc_rc(y[i], kP2S.rcs[r * 24 + i]));
     p2_m_ext64s(x, y);
   }
 #pragma unroll
@@ -291,7 +309,7 @@ R0_HD void poseidon2_mix(uint32_t* c) {
 #pragma unroll 1
   for (int r = 5; r < 8; r++) {
 #pragma unroll
-    for (int i = 0; i < 24; i++) x[i] = p2_sbox_s(sredc(y[i] + int64_t(kP2S.rc[r * 24 + i])));
+    for (int i = 0; i < 24; i++) x[i] = p2_sbox_s(sredc_rc(y[i], kP2S.rcs[r * 24 + i]));
     p2_m_ext64s(x, y);
   }
 #pragma unroll

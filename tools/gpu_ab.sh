@@ -8,7 +8,8 @@ O=gpurun_out/$TAG; mkdir -p $O
 LEGS="$EXTRA --no-cpu-baseline --no-prove-only --e2e-steps 0 --accum-steps 0 --resident-steps 0 --per-op-steps 0"
 for i in $(seq 1 $N); do
   for v in $A $B; do
-    env $VAR=$v timeout -k 10 300 python -u bench.py $LEGS > $O/bench${SUF}_${VAR}_${v}_$i.json 2> $O/bench${SUF}_${VAR}_${v}_$i.err || { tail -20 $O/bench${SUF}_${VAR}_${v}_$i.err; exit 1; }
-    python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['ms_per_step'], d['value'], d['config'].get('ms_one_segment_unpipelined'))" $O/bench${SUF}_${VAR}_${v}_$i.json "$SUF $VAR=$v run $i" | tee -a $O/ab.txt
+    t=$(basename "$v")
+    env $VAR=$v timeout -k 10 300 python -u bench.py $LEGS > $O/bench${SUF}_${VAR}_${t}_$i.json 2> $O/bench${SUF}_${VAR}_${t}_$i.err || { tail -20 $O/bench${SUF}_${VAR}_${t}_$i.err; exit 1; }
+    python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['ms_per_step'], d['value'], d['config'].get('ms_one_segment_unpipelined'))" $O/bench${SUF}_${VAR}_${t}_$i.json "$SUF $VAR=$t run $i" | tee -a $O/ab.txt
   done
 done
