@@ -103,6 +103,12 @@ const char* r0hip_eltwise_copy_elem_slice(uint32_t* d_into, const uint32_t* d_fr
                                           size_t from_cols, size_t from_offset, size_t from_stride,
                                           size_t into_offset, size_t into_stride);
 const char* r0hip_gather_sample(uint32_t* d_dst, const uint32_t* d_src, size_t idx, size_t size, size_t stride);
+/* gather_sample straight to the host: h_dst[i] = d_src[idx + i*stride], i < size (no CUDA
+ * counterpart). For a HAL whose gather_sample destination is read back before the device uses it
+ * (MerkleTreeProver::prove's sample, merkle.rs:111-129: gather_sample, then view): one kernel,
+ * one copy and one sync instead of a device allocation, gather_sample, view and free. */
+const char* r0hip_gather_sample_host(uint32_t* h_dst, const uint32_t* d_src, size_t idx, size_t size,
+                                     size_t stride);
 /* CSR scatter (ffi.cu:108-114): index has cycles+1 entries */
 const char* r0hip_scatter(uint32_t* d_into, const uint32_t* d_index, const uint32_t* d_offsets,
                           const uint32_t* d_values, size_t cycles);

@@ -58,13 +58,18 @@ struct Buf {
   mutable uint32_t* host = nullptr;
   mutable bool host_ok = false;
   mutable void* pending = nullptr;  // the mirror's copy in flight
+  // gather_sample into a buffer with no device memory yet (hal_hip.rs DeviceAlloc::gathered):
+  // the words are gathered straight to the host (r0hip_gather_sample_host) and read from there;
+  // MerkleTreeProver::prove's sample is only viewed, so it never gets device memory
+  std::vector<uint32_t> gathered;
   Buf() = default;
   explicit Buf(size_t n) : words(n) {
     void* d = nullptr;
     ok(r0hip_alloc(&d, (n ? n : 1) * 4));
     p = static_cast<uint32_t*>(d);
   }
-  Buf(Buf&& o) noexcept : p(o.p), words(o.words), host(o.host), host_ok(o.host_ok), pending(o.pending) {
+  Buf(Buf&& o) noexcept
+      : p(o.p), words(o.words), host(o.host), host_ok(o.host_ok), pending(o.pending), gathered(std::move(o.gathered)) {
     o.p = nullptr;
     o.host = nullptr;
     o.pending = nullptr;
@@ -75,7 +80,24 @@ struct Buf {
     std::swap(host, o.host);
     std::swap(host_ok, o.host_ok);
     std::swap(pending, o.pending);
+    std::swap(gathered, o.gathered);
     return *this;
+  }
+  // alloc_elem as the HAL does it: the device allocation waits for the first device use
+  static Buf unallocated(size_t n) {
+    Buf b;
+    b.words = n;
+    return b;
+  }
+  // Hal::gather_sample(this, src, idx, size, stride) (cuda.rs:589-603)
+  void gather_sample(const Buf& src, size_t idx, size_t size, size_t stride) {
+    if (!p && size == words) {
+      gathered.resize(size);
+      ok(r0hip_gather_sample_host(gathered.data(), src.p, idx, size, stride));
+      return;
+    }
+    if (!p) *this = Buf(words);
+    ok(r0hip_gather_sample(p, src.p, idx, size, stride));
   }
   ~Buf() {
     settle();
@@ -125,6 +147,8 @@ struct Buf {
   }
   std::vector<uint32_t> to_host(size_t off = 0, size_t n = SIZE_MAX) const {
     if (n == SIZE_MAX) n = words - off;
+    if (!p && gathered.size() == words)
+      return std::vector<uint32_t>(gathered.begin() + off, gathered.begin() + off + n);
     std::vector<uint32_t> h(n);
     if (n) ok(r0hip_memcpy_d2h(h.data(), p + off, n * 4));
     return h;
@@ -172,9 +196,9 @@ struct Merkle {
   }
   // prove/merkle.rs:108-140: gather_sample, then one get_at per node up the tree
   void prove(WriteIOP& iop, size_t idx) const {
-    Buf sample(cols);
-    ok(r0hip_gather_sample(sample.p, matrix->p, idx, cols, rows));
-    auto s = sample.to_host();
+    Buf sample = Buf::unallocated(cols);  // hal.alloc_elem("sample", cols)
+    sample.gather_sample(*matrix, idx, cols, rows);
+    auto s = sample.to_host();  // sample.view
     iop.write(s.data(), s.size());
     idx += rows;
     while (idx >= 2 * top_size) {

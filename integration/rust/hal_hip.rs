@@ -15,6 +15,11 @@
 //     mirror of the heap, copied beside the next calls once hash_fold has built the root
 //     (r0hip_memcpy_d2h_start; a tree's ~50 x 17 node reads would otherwise be one synchronous
 //     copy each);
+//   * an allocation gets device memory at its first device use: `gather_sample` into a
+//     buffer that has none yet gathers straight to the host (r0hip_gather_sample_host) and
+//     `view` reads those words — MerkleTreeProver::prove's sample (merkle.rs:111-129) is only
+//     viewed, so its 350 openings per proof cost one call each instead of alloc, gather, view
+//     and free; a device use first uploads the gathered words;
 //   * combos_prepare / combos_divide are overridden with the device versions, as cuda.rs:
 //     986-1048 does (one batched call for every chunk instead of one per divisor).
 //
@@ -66,8 +71,12 @@ fn device_ordinal() -> i32 {
 /// MemoryTracker (hal/mod.rs:292-317) sees it like the CUDA HAL's RawBuffer.
 struct DeviceAlloc {
     name: &'static str,
-    ptr: *mut c_void,
+    /// device memory, allocated at the first device use (`device`)
+    ptr: Cell<*mut c_void>,
     bytes: usize,
+    /// words gather_sample put straight on the host while the allocation had no device memory
+    /// (the whole allocation): view/get_at read them, `device` uploads them first
+    gathered: RefCell<Option<Vec<u32>>>,
     /// Merkle node heaps: hash_fold's root layer starts a copy of the whole allocation into
     /// `mirror` (page-locked) beside the Prover's next calls (`pending`); get_at reads the mirror
     /// once that copy has landed and one element synchronously until then. The only Hal methods
@@ -81,12 +90,26 @@ struct DeviceAlloc {
 impl DeviceAlloc {
     fn new(name: &'static str, bytes: usize) -> Self {
         assert!(bytes > 0, "empty allocation: {name}");
-        let mut ptr = std::ptr::null_mut();
-        ffi_wrap(|| unsafe { r0hip_alloc(&mut ptr, bytes) })
-            .unwrap_or_else(|e| panic!("allocation failed on {name}: {bytes} bytes: {e}"));
         tracker().lock().unwrap().alloc(bytes);
-        Self { name, ptr, bytes, mirror: Cell::new(std::ptr::null_mut()), mirror_ok: Cell::new(false),
+        Self { name, ptr: Cell::new(std::ptr::null_mut()), bytes, gathered: RefCell::new(None),
+               mirror: Cell::new(std::ptr::null_mut()), mirror_ok: Cell::new(false),
                pending: Cell::new(std::ptr::null_mut()) }
+    }
+
+    /// the device memory, allocated now if this is the first device use; words gathered to the
+    /// host are uploaded first (a device op may read them, and any may write the buffer)
+    fn device(&self) -> *mut c_void {
+        if self.ptr.get().is_null() {
+            let (name, bytes) = (self.name, self.bytes);
+            let mut ptr = std::ptr::null_mut();
+            ffi_wrap(|| unsafe { r0hip_alloc(&mut ptr, bytes) })
+                .unwrap_or_else(|e| panic!("allocation failed on {name}: {bytes} bytes: {e}"));
+            self.ptr.set(ptr);
+        }
+        if let Some(g) = self.gathered.borrow_mut().take() {
+            check(unsafe { r0hip_memcpy_h2d(self.ptr.get(), g.as_ptr() as *const c_void, g.len() * 4) });
+        }
+        self.ptr.get()
     }
 
     /// wait out a mirror copy in flight (before the allocation is written or freed)
@@ -113,7 +136,7 @@ impl DeviceAlloc {
             self.mirror.set(h);
         }
         let mut c = std::ptr::null_mut();
-        check(unsafe { r0hip_memcpy_d2h_start(self.mirror.get(), self.ptr, self.bytes, &mut c) });
+        check(unsafe { r0hip_memcpy_d2h_start(self.mirror.get(), self.device(), self.bytes, &mut c) });
         self.pending.set(c);
         self.mirror_ok.set(true);
     }
@@ -140,7 +163,9 @@ impl Drop for DeviceAlloc {
     fn drop(&mut self) {
         self.settle();
         tracker().lock().unwrap().free(self.bytes);
-        unsafe { r0hip_free(self.ptr) };
+        if !self.ptr.get().is_null() {
+            unsafe { r0hip_free(self.ptr.get()) };
+        }
         if !self.mirror.get().is_null() {
             unsafe { r0hip_host_free(self.mirror.get()) };
         }
@@ -173,7 +198,7 @@ impl<T> BufferImpl<T> {
     }
 
     fn dev_void(&self) -> *mut c_void {
-        let base = self.alloc.borrow().ptr as *mut u8;
+        let base = self.alloc.borrow().device() as *mut u8;
         unsafe { base.add(self.offset * std::mem::size_of::<T>()) as *mut c_void }
     }
 
@@ -201,6 +226,14 @@ impl<T> BufferImpl<T> {
     fn read(&self, offset: usize, len: usize) -> Vec<T> {
         let mut out = Vec::<T>::with_capacity(len);
         let bytes = len * std::mem::size_of::<T>();
+        if let Some(g) = self.alloc.borrow().gathered.borrow().as_ref() {
+            let at = (self.offset + offset) * std::mem::size_of::<T>();
+            unsafe {
+                std::ptr::copy_nonoverlapping((g.as_ptr() as *const u8).add(at), out.as_mut_ptr() as *mut u8, bytes);
+                out.set_len(len);
+            }
+            return out;
+        }
         if bytes > 0 {
             check(unsafe { r0hip_memcpy_d2h(out.as_mut_ptr() as *mut c_void, self.dev_at(offset) as *const c_void, bytes) });
         }
@@ -538,6 +571,17 @@ impl<HS: HipHash> Hal for HipHal<HS> {
         stride: usize,
     ) {
         assert!(dst.size() >= size);
+        {
+            // a fresh whole-allocation destination: gather straight to the host (it is read back
+            // before any device use in MerkleTreeProver::prove; `device` uploads it otherwise)
+            let a = dst.alloc.borrow();
+            if a.ptr.get().is_null() && dst.offset == 0 && size * 4 == a.bytes {
+                let mut g = vec![0u32; size];
+                check(unsafe { r0hip_gather_sample_host(g.as_mut_ptr(), src.dev(), idx, size, stride) });
+                *a.gathered.borrow_mut() = Some(g);
+                return;
+            }
+        }
         check(unsafe { r0hip_gather_sample(dst.dev(), src.dev(), idx, size, stride) });
     }
 

@@ -170,6 +170,8 @@ unsafe extern "C" {
     ) -> *const c_char;
     pub fn r0hip_gather_sample(d_dst: *mut u32, d_src: *const u32, idx: usize, size: usize, stride: usize)
         -> *const c_char;
+    pub fn r0hip_gather_sample_host(h_dst: *mut u32, d_src: *const u32, idx: usize, size: usize, stride: usize)
+        -> *const c_char;
     pub fn r0hip_scatter(
         d_into: *mut u32,
         d_index: *const u32,

@@ -296,6 +296,16 @@ const char* r0hip_eltwise_copy_elem_slice(uint32_t* d_into, const uint32_t* d_fr
 const char* r0hip_gather_sample(uint32_t* d_dst, const uint32_t* d_src, size_t idx, size_t size, size_t stride) {
   return wrap([&] { gather_sample(stream(), d_dst, d_src, idx, size, stride); });
 }
+const char* r0hip_gather_sample_host(uint32_t* h_dst, const uint32_t* d_src, size_t idx, size_t size,
+                                     size_t stride) {
+  return wrap([&] {
+    if (!size) return;
+    R0_REQUIRE(h_dst && d_src, "gather_sample_host: null pointer");
+    uint32_t* d = static_cast<uint32_t*>(scratch(size * 4, kSlotApiGather));
+    gather_sample(stream(), d, d_src, idx, size, stride);
+    download(h_dst, d, size * 4);
+  });
+}
 const char* r0hip_scatter(uint32_t* d_into, const uint32_t* d_index, const uint32_t* d_offsets,
                           const uint32_t* d_values, size_t cycles) {
   return wrap([&] { scatter(stream(), d_into, d_index, d_offsets, d_values, cycles); });

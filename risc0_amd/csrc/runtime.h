@@ -91,6 +91,7 @@ enum ScratchSlot : int {
   kSlotApiDeltas = 51,
   kSlotApiRem = 52,
   kSlotApiRems = 53,
+  kSlotApiGather = 54,
   // accumulation (recursion_accum.hip, accum.hip, bigint.cpp)
   kSlotRecAccVals = 60,
   kSlotRecAccProds = 61,

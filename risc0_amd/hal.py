@@ -81,6 +81,7 @@ def _declare(L):
         "r0hip_eltwise_sum_extelem": [vp, vp, sz, sz],
         "r0hip_eltwise_copy_elem_slice": [vp, vp, sz, sz, sz, sz, sz, sz],
         "r0hip_gather_sample": [vp, vp, sz, sz, sz],
+        "r0hip_gather_sample_host": [vp, vp, sz, sz, sz],
         "r0hip_scatter": [vp, vp, vp, vp, sz],
         "r0hip_prefix_products": [vp, sz],
         "r0hip_hash_rows": [C.c_int, vp, vp, sz, sz],
@@ -303,6 +304,12 @@ class HipHal:
 
     def gather_sample(self, dst, src, idx, size, stride):
         check(lib().r0hip_gather_sample(dst.ptr, src.ptr, idx, size, stride))
+
+    def gather_sample_host(self, src, idx, size, stride):
+        """src[idx + i*stride], i < size, as a host array (r0hip_gather_sample_host)"""
+        out = np.zeros(size, np.uint32)
+        check(lib().r0hip_gather_sample_host(out.ctypes.data, src.ptr, idx, size, stride))
+        return out
 
     def scatter(self, into, index, offsets, values):
         index = np.asarray(index, dtype=np.uint32)

@@ -199,6 +199,14 @@ def test_gather_scatter_slice_prefix(hal, oracle):
     dst = hal.alloc_elem("dst", rows)
     hal.gather_sample(dst, dev(hal, src), idx, rows, cols)
     assert np.array_equal(dst.to_numpy(), src.reshape(rows, cols)[:, idx])
+    # the same straight to the host (r0hip_gather_sample_host), and a Merkle-opening shape:
+    # 211 columns of a 2^16-row matrix at the last row
+    dsrc = dev(hal, src)
+    assert np.array_equal(hal.gather_sample_host(dsrc, idx, rows, cols), src.reshape(rows, cols)[:, idx])
+    assert hal.gather_sample_host(dsrc, idx, 0, cols).size == 0
+    m = oracle.rand_elems(rng, 211 << 16)
+    assert np.array_equal(hal.gather_sample_host(dev(hal, m), (1 << 16) - 1, 211, 1 << 16),
+                          m.reshape(211, 1 << 16)[:, -1])
     # scatter (cpu.rs:598-615): CSR per cycle
     cycles = 300
     counts = rng.integers(0, 5, cycles)
