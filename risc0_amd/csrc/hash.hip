@@ -542,7 +542,7 @@ static void note_heap(int suite, const uint32_t* leaves, size_t rows, size_t col
 }
 static ZeroSub noted_layer(int suite, const uint32_t* io, size_t input_size) {
   ZeroSub z{};
-  if (suite > 1 || !zero_enabled()) return z;
+  if (suite > 1 || input_size < 2 || !zero_enabled()) return z;
   HeapNote n;
   {
     std::lock_guard<std::mutex> lk(g_note_mu);

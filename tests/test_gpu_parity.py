@@ -324,6 +324,10 @@ def test_merkle_tree_zero_subtrees(hal, hal_sha, oracle, suite, rows, cols, patt
         h.hash_fold(ops, layer, layer // 2)
         layer //= 2
     assert np.array_equal(ops.to_numpy()[8:], io[8:])
+    # degenerate folds on a noted heap: an empty fold is a no-op, a bad size is reported
+    h.hash_fold(ops, 0, 0)
+    with pytest.raises(Exception):
+        h.hash_fold(ops, 6, 4)
     # the same heap refilled with other leaves (a stale note): still the oracle's words
     if rows >= 4:
         other = rng.integers(0, 2**32, rows * 8, dtype=np.uint64).astype(np.uint32) // 3
