@@ -65,9 +65,14 @@ def test_witgen_ir_fails_where_the_reference_fails():
             "try:\n    RP.witgen(prog, pf, 11, raw=True)\n"
             "except RuntimeError as e:\n    print(e, flush=True)\n    os._exit(3)\n"
             "os._exit(0)\n") % (here, os.path.join(os.path.dirname(here), "oracle"))
-    res = subprocess.run([sys.executable, "-c", code], input=pickle.dumps((prog, pf)), capture_output=True,
-                         timeout=120)
     import signal
+    # the compiled reference can also die by SIGSEGV in its thread pool before its message
+    # reaches stdout (seen once in a full CPU run): such a child is run again, up to 4 times
+    for _ in range(4):
+        res = subprocess.run([sys.executable, "-c", code], input=pickle.dumps((prog, pf)), capture_output=True,
+                             timeout=120)
+        if b"wom.cpp:74" in res.stdout or res.returncode != -signal.SIGSEGV:
+            break
     assert b"wom.cpp:74" in res.stdout, (res.returncode, res.stdout, res.stderr)
     assert res.returncode in (3, -signal.SIGSEGV), \
         f"child exit {res.returncode} (expected 3, or SIGSEGV after the message): {res.stderr[-2000:]!r}"
